@@ -1,0 +1,509 @@
+/*
+ * rnnt_oracle.c -- CPU restatement of the reference RNN-T hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see rnnt_oracle.h).  Compiled with -ffp-contract=off so that
+ * every a*b+c written below is two roundings and every fmaf() is one: the numerics
+ * contract is defined by exactly these operations.
+ *
+ * Parity pinning: the reference's native ops are absent (plugin submodule un-vendored),
+ * so this file restates the reference's Python semantics; tests/test_oracle_golden.py pins
+ * the fp32 path and the quantisation math against fixtures generated from the reference's
+ * own Python modules (tests/golden/make_golden.py).
+ */
+#include "rnnt_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+enum { H_ENC = 1024, P = 320, J = 512, NLAB = 29, BLANK = 28, SOS = -1, MAXSYM = 30 };
+
+static inline float bits2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t f2bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+/* ---------------------------------------------------------------- activations ----
+ * Deterministic exp: Cephes expf range reduction + degree-6 polynomial, evaluated with
+ * explicit fmaf so the HIP engine reproduces it bit-for-bit (IEEE mul/add/fma/div and
+ * rint are identical on both sides).  Max rel. error vs libm ~1.2e-7. */
+float oracle_exp(float x) {
+  x = fminf(fmaxf(x, -87.0f), 88.0f);
+  const float n = rintf(x * 1.44269504088896341f);
+  float r = fmaf(n, -0.693359375f, x);
+  r = fmaf(n, 2.12194440e-4f, r);
+  const float z = r * r;
+  float p = 1.9875691500e-4f;
+  p = fmaf(p, r, 1.3981999507e-3f);
+  p = fmaf(p, r, 8.3334519073e-3f);
+  p = fmaf(p, r, 4.1665795894e-2f);
+  p = fmaf(p, r, 1.6666665459e-1f);
+  p = fmaf(p, r, 5.0000001201e-1f);
+  p = fmaf(p, z, r);
+  p = p + 1.0f;
+  const int e = (int)n;
+  return p * bits2f((uint32_t)(e + 127) << 23);
+}
+
+float oracle_sigmoid(float x) { return 1.0f / (1.0f + oracle_exp(-x)); }
+
+float oracle_tanh(float x) {
+  const float a = fabsf(x);
+  const float e = oracle_exp(-2.0f * a);
+  const float t = (1.0f - e) / (1.0f + e);
+  return copysignf(t, x);
+}
+
+/* ---------------------------------------------------------------- conversions ---- */
+uint16_t oracle_f2h(float f) {
+  const uint32_t x = f2bits(f), sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);
+  if (ax >= 0x38800000u) {
+    uint32_t r = ax - 0x38000000u;
+    r = r + 0xfffu + ((r >> 13) & 1u);
+    return (uint16_t)(sign | (r >> 13));
+  }
+  if (ax < 0x33000000u) return (uint16_t)sign;
+  {
+    const uint32_t e = ax >> 23, m = (ax & 0x7fffffu) | 0x800000u, shift = 126u - e;
+    uint32_t q = m >> shift;
+    const uint32_t rem = m & ((1u << shift) - 1u), half = 1u << (shift - 1u);
+    if (rem > half || (rem == half && (q & 1u))) q++;
+    return (uint16_t)(sign | q);
+  }
+}
+
+float oracle_h2f(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  if (e == 0) {
+    const float v = (float)m * 5.9604644775390625e-8f;
+    return sign ? -v : v;
+  }
+  if (e == 31) return bits2f(sign | 0x7f800000u | (m << 13));
+  return bits2f(sign | ((e + 112u) << 23) | (m << 13));
+}
+
+uint16_t oracle_f2bf(float f) {
+  const uint32_t u = f2bits(f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+float oracle_bf2f(uint16_t b) { return bits2f((uint32_t)b << 16); }
+static inline float bfr(float x) { return oracle_bf2f(oracle_f2bf(x)); }
+
+int8_t oracle_q8(float v) {
+  float r = rintf(v);
+  if (r > 127.0f) r = 127.0f;
+  if (r < -128.0f) r = -128.0f;
+  return (int8_t)r;
+}
+
+void oracle_quantize(const float* x, int64_t n, float scale, int8_t* out) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) out[i] = oracle_q8(x[i] * scale);
+}
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+/* ---------------------------------------------------------------- int8 LSTM ----
+ * Cell (quant_lstm.py:162-183 with the quantised parameters of :193-215):
+ *   acc   = x_q.W_ih_q^T + h_q.W_hh_q^T            (exact int32)
+ *   pre   = ((float)acc + b_q) * rb_scale           (fp32; rb = 1/(s_in*s_w))
+ *   i,f,o = sigmoid, g = tanh                       (chunk order i,f,g,o, :174)
+ *   c     = f*c_prev + i*g   (fp32, stored fp16 RNE: cx dtype, decoder.py:40-41)
+ *   h     = o*tanh(c)        (fp32 c, before the fp16 store)
+ *   h_q   = q8(h*in_s)   (recurrent state: calibrated on cat([x, h]), :169)
+ *   y     = q8(h*out_s) or h (skip_quant_y, quant_lstm.py:98)                          */
+void oracle_lstm_i8_layer(int T, int N, int I, int H, const int8_t* x, const int8_t* W,
+                          const float* bq, float rb, float in_s, float out_s, int skip_quant_y,
+                          int8_t* h, uint16_t* c, int8_t* y8, float* y32) {
+  const int K = I + H;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int n = 0; n < N; ++n) {
+    int32_t* acc = (int32_t*)malloc(sizeof(int32_t) * 4 * (size_t)H);
+    int8_t* hv = (int8_t*)malloc((size_t)H);
+    int8_t* hn = (int8_t*)malloc((size_t)H);
+    memcpy(hv, h + (size_t)n * H, (size_t)H);
+    uint16_t* cv = c + (size_t)n * H;
+    for (int t = 0; t < T; ++t) {
+      const int8_t* xt = x + ((size_t)t * N + n) * I;
+      for (int r = 0; r < 4 * H; ++r) {
+        const int8_t* w = W + (size_t)r * K;
+        int32_t s = 0;
+        for (int k = 0; k < I; ++k) s += (int32_t)xt[k] * (int32_t)w[k];
+        for (int k = 0; k < H; ++k) s += (int32_t)hv[k] * (int32_t)w[I + k];
+        acc[r] = s;
+      }
+      for (int j = 0; j < H; ++j) {
+        const float pi = ((float)acc[j] + bq[j]) * rb;
+        const float pf = ((float)acc[H + j] + bq[H + j]) * rb;
+        const float pg = ((float)acc[2 * H + j] + bq[2 * H + j]) * rb;
+        const float po = ((float)acc[3 * H + j] + bq[3 * H + j]) * rb;
+        const float ig = oracle_sigmoid(pi), fg = oracle_sigmoid(pf);
+        const float gg = oracle_tanh(pg), og = oracle_sigmoid(po);
+        const float cp = oracle_h2f(cv[j]);
+        const float cn = fg * cp + ig * gg;
+        cv[j] = oracle_f2h(cn);
+        const float hh = og * oracle_tanh(cn);
+        hn[j] = oracle_q8(hh * in_s);
+        const size_t o = ((size_t)t * N + n) * H + j;
+        if (skip_quant_y)
+          y32[o] = hh;
+        else
+          y8[o] = oracle_q8(hh * out_s);
+      }
+      memcpy(hv, hn, (size_t)H);
+    }
+    memcpy(h + (size_t)n * H, hv, (size_t)H);
+    free(acc);
+    free(hv);
+    free(hn);
+  }
+}
+
+/* StackTime.forward_f32 (modeling_rnnt.py:314-324) / intel_mlperf::stack_time (:327). */
+void oracle_stack_time_i8(int T, int N, int C, const int8_t* x, const int32_t* lens, int8_t* y) {
+  const int Tp = (T + 1) / 2;
+  for (int tp = 0; tp < Tp; ++tp)
+    for (int n = 0; n < N; ++n)
+      for (int half = 0; half < 2; ++half) {
+        const int t = 2 * tp + half;
+        int8_t* dst = y + ((size_t)tp * N + n) * 2 * C + (size_t)half * C;
+        if (t < T && t < lens[n])
+          memcpy(dst, x + ((size_t)t * N + n) * C, (size_t)C);
+        else
+          memset(dst, 0, (size_t)C);
+      }
+}
+
+void oracle_stack_time_f32(int T, int N, int C, const float* x, const int32_t* lens, float* y) {
+  const int Tp = (T + 1) / 2;
+  for (int tp = 0; tp < Tp; ++tp)
+    for (int n = 0; n < N; ++n)
+      for (int half = 0; half < 2; ++half) {
+        const int t = 2 * tp + half;
+        float* dst = y + ((size_t)tp * N + n) * 2 * C + (size_t)half * C;
+        if (t < T && t < lens[n])
+          memcpy(dst, x + ((size_t)t * N + n) * C, sizeof(float) * (size_t)C);
+        else
+          memset(dst, 0, sizeof(float) * (size_t)C);
+      }
+}
+
+void oracle_encoder_i8(int T, int N, const float* feat, const int32_t* lens,
+                       const int8_t* const* W, const float* const* bq, const float* rb,
+                       const float* in_s, const float* out_s, float* f_out,
+                       int8_t* h_state, uint16_t* c_state) {
+  const int H = H_ENC, Tp = (T + 1) / 2;
+  const size_t NH = (size_t)N * H;
+  int8_t* hs = h_state ? h_state : (int8_t*)calloc(5 * NH, 1);
+  uint16_t* cs = c_state ? c_state : (uint16_t*)calloc(5 * NH, 2);
+  int8_t* x0 = (int8_t*)malloc((size_t)T * N * 256);
+  int8_t* ya = (int8_t*)malloc((size_t)T * NH);
+  int8_t* yb = (int8_t*)malloc((size_t)T * NH);
+  int8_t* xs = (int8_t*)malloc((size_t)Tp * NH * 2);
+  oracle_quantize(feat, (int64_t)T * N * 256, in_s[0], x0);
+  oracle_lstm_i8_layer(T, N, 256, H, x0, W[0], bq[0], rb[0], in_s[0], out_s[0], 0, hs, cs, ya, 0);
+  oracle_lstm_i8_layer(T, N, H, H, ya, W[1], bq[1], rb[1], in_s[1], out_s[1], 0, hs + NH,
+                       cs + NH, yb, 0);
+  oracle_stack_time_i8(T, N, H, yb, lens, xs);
+  oracle_lstm_i8_layer(Tp, N, 2 * H, H, xs, W[2], bq[2], rb[2], in_s[2], out_s[2], 0,
+                       hs + 2 * NH, cs + 2 * NH, ya, 0);
+  oracle_lstm_i8_layer(Tp, N, H, H, ya, W[3], bq[3], rb[3], in_s[3], out_s[3], 0, hs + 3 * NH,
+                       cs + 3 * NH, yb, 0);
+  oracle_lstm_i8_layer(Tp, N, H, H, yb, W[4], bq[4], rb[4], in_s[4], 0.0f, 1, hs + 4 * NH,
+                       cs + 4 * NH, 0, f_out);
+  free(x0); free(ya); free(yb); free(xs);
+  if (!h_state) free(hs);
+  if (!c_state) free(cs);
+}
+
+/* ---------------------------------------------------------------- fp32 LSTM ---- */
+static void transpose_f32(const float* a, int R, int C, float* at) {
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < C; ++c) at[(size_t)c * R + r] = a[(size_t)r * C + c];
+}
+
+/* acc[r] = fmaf-chain over k of x[k]*WT[k][r], starting from acc[r] (R independent chains,
+ * each exactly k-ordered; the r loop vectorises without changing any chain). */
+static void chain_acc(float* acc, const float* x, const float* WT, int Kd, int R) {
+  for (int k = 0; k < Kd; ++k) {
+    const float xv = x[k];
+    const float* w = WT + (size_t)k * R;
+    for (int r = 0; r < R; ++r) acc[r] = fmaf(xv, w[r], acc[r]);
+  }
+}
+
+void oracle_lstm_f32_layer(int T, int N, int I, int H, const float* x, const float* Wih,
+                           const float* Whh, const float* bih, const float* bhh, float* h,
+                           float* c, float* y) {
+  float* WihT = (float*)malloc(sizeof(float) * (size_t)I * 4 * H);
+  float* WhhT = (float*)malloc(sizeof(float) * (size_t)H * 4 * H);
+  transpose_f32(Wih, 4 * H, I, WihT);
+  transpose_f32(Whh, 4 * H, H, WhhT);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int n = 0; n < N; ++n) {
+    float* ax = (float*)malloc(sizeof(float) * 4 * (size_t)H);
+    float* ah = (float*)malloc(sizeof(float) * 4 * (size_t)H);
+    float* hv = h + (size_t)n * H;
+    float* cv = c + (size_t)n * H;
+    for (int t = 0; t < T; ++t) {
+      memcpy(ax, bih, sizeof(float) * 4 * (size_t)H);
+      memcpy(ah, bhh, sizeof(float) * 4 * (size_t)H);
+      chain_acc(ax, x + ((size_t)t * N + n) * I, WihT, I, 4 * H);
+      chain_acc(ah, hv, WhhT, H, 4 * H);
+      for (int j = 0; j < H; ++j) {
+        const float ig = oracle_sigmoid(ax[j] + ah[j]);
+        const float fg = oracle_sigmoid(ax[H + j] + ah[H + j]);
+        const float gg = oracle_tanh(ax[2 * H + j] + ah[2 * H + j]);
+        const float og = oracle_sigmoid(ax[3 * H + j] + ah[3 * H + j]);
+        const float cn = fg * cv[j] + ig * gg;
+        cv[j] = cn;
+        hv[j] = og * oracle_tanh(cn);
+        y[((size_t)t * N + n) * H + j] = hv[j];
+      }
+    }
+    free(ax);
+    free(ah);
+  }
+  free(WihT);
+  free(WhhT);
+}
+
+void oracle_encoder_f32(int T, int N, int I0, const float* feat, const int32_t* lens,
+                        const float* const* Wih, const float* const* Whh,
+                        const float* const* bih, const float* const* bhh, float* f_out) {
+  const int H = H_ENC, Tp = (T + 1) / 2;
+  const size_t NH = (size_t)N * H;
+  float* h = (float*)calloc(NH, sizeof(float));
+  float* c = (float*)calloc(NH, sizeof(float));
+  float* ya = (float*)malloc(sizeof(float) * (size_t)T * NH);
+  float* yb = (float*)malloc(sizeof(float) * (size_t)T * NH);
+  float* xs = (float*)malloc(sizeof(float) * (size_t)Tp * NH * 2);
+  oracle_lstm_f32_layer(T, N, I0, H, feat, Wih[0], Whh[0], bih[0], bhh[0], h, c, ya);
+  memset(h, 0, sizeof(float) * NH); memset(c, 0, sizeof(float) * NH);
+  oracle_lstm_f32_layer(T, N, H, H, ya, Wih[1], Whh[1], bih[1], bhh[1], h, c, yb);
+  oracle_stack_time_f32(T, N, H, yb, lens, xs);
+  memset(h, 0, sizeof(float) * NH); memset(c, 0, sizeof(float) * NH);
+  oracle_lstm_f32_layer(Tp, N, 2 * H, H, xs, Wih[2], Whh[2], bih[2], bhh[2], h, c, ya);
+  memset(h, 0, sizeof(float) * NH); memset(c, 0, sizeof(float) * NH);
+  oracle_lstm_f32_layer(Tp, N, H, H, ya, Wih[3], Whh[3], bih[3], bhh[3], h, c, yb);
+  memset(h, 0, sizeof(float) * NH); memset(c, 0, sizeof(float) * NH);
+  oracle_lstm_f32_layer(Tp, N, H, H, yb, Wih[4], Whh[4], bih[4], bhh[4], h, c, f_out);
+  free(h); free(c); free(ya); free(yb); free(xs);
+}
+
+/* ---------------------------------------------------------------- decoder ----
+ * Per-row restatement of GreedyDecoder.greedy_decode_f32 (decoder.py:102-169), the readable
+ * spec of intel_mlperf::greedy_decode_update (modeling_rnnt.py:331-365).  Rows of the
+ * reference batch never interact, and prediction(pre_g, pre_hg, pre_cg) is a pure function
+ * of state that only changes on an emit, so evaluating it once per emit (instead of once per
+ * step for the whole batch) returns identical values. */
+typedef struct {
+  int bf16;
+  const float *embed, *const *Wih, *const *Whh, *const *bih, *const *bhh;
+  float *WihT[2], *WhhT[2];
+  const float *W1t, *W1p, *bt, *bp, *W2, *b2;
+  float *W1tT, *W1pT, *W2T;
+} dec_w;
+
+static void dec_w_init(dec_w* d) {
+  for (int l = 0; l < 2; ++l) {
+    d->WihT[l] = (float*)malloc(sizeof(float) * 4 * P * P);
+    d->WhhT[l] = (float*)malloc(sizeof(float) * 4 * P * P);
+    transpose_f32(d->Wih[l], 4 * P, P, d->WihT[l]);
+    transpose_f32(d->Whh[l], 4 * P, P, d->WhhT[l]);
+  }
+  d->W1tT = (float*)malloc(sizeof(float) * J * H_ENC);
+  d->W1pT = (float*)malloc(sizeof(float) * J * P);
+  d->W2T = (float*)malloc(sizeof(float) * NLAB * J);
+  transpose_f32(d->W1t, J, H_ENC, d->W1tT);
+  transpose_f32(d->W1p, J, P, d->W1pT);
+  transpose_f32(d->W2, NLAB, J, d->W2T);
+}
+
+static void dec_w_free(dec_w* d) {
+  for (int l = 0; l < 2; ++l) { free(d->WihT[l]); free(d->WhhT[l]); }
+  free(d->W1tT); free(d->W1pT); free(d->W2T);
+}
+
+/* Prediction.forward (modeling_rnnt.py:183-205): SOS -> zero embedding; 2-layer LSTM.
+ * bf16: gates = b_ih+b_hh then chain over x then h (lstm_amx_bf16 fused bias, :170-172);
+ * fp32: (b_ih + x.W_ih) + (b_hh + h.W_hh).  h stored bf16 in bf16 mode, c fp32. */
+static void pred_row(const dec_w* d, int pre_g, const float* ph, const float* pc, float* gh,
+                     float* gc) {
+  float x[P], ax[4 * P], ah[4 * P];
+  if (pre_g == SOS)
+    memset(x, 0, sizeof(x));
+  else
+    memcpy(x, d->embed + (size_t)pre_g * P, sizeof(x));
+  for (int l = 0; l < 2; ++l) {
+    const float* hp = ph + l * P;
+    const float* cp = pc + l * P;
+    if (d->bf16) {
+      for (int r = 0; r < 4 * P; ++r) ax[r] = d->bih[l][r] + d->bhh[l][r];
+      chain_acc(ax, x, d->WihT[l], P, 4 * P);
+      chain_acc(ax, hp, d->WhhT[l], P, 4 * P);
+      memset(ah, 0, sizeof(ah));
+    } else {
+      memcpy(ax, d->bih[l], sizeof(ax));
+      memcpy(ah, d->bhh[l], sizeof(ah));
+      chain_acc(ax, x, d->WihT[l], P, 4 * P);
+      chain_acc(ah, hp, d->WhhT[l], P, 4 * P);
+    }
+    for (int j = 0; j < P; ++j) {
+      float pi = ax[j], pf = ax[P + j], pg = ax[2 * P + j], po = ax[3 * P + j];
+      if (!d->bf16) { pi = pi + ah[j]; pf = pf + ah[P + j]; pg = pg + ah[2 * P + j]; po = po + ah[3 * P + j]; }
+      const float ig = oracle_sigmoid(pi), fg = oracle_sigmoid(pf);
+      const float gg = oracle_tanh(pg), og = oracle_sigmoid(po);
+      const float cn = fg * cp[j] + ig * gg;
+      float hh = og * oracle_tanh(cn);
+      if (d->bf16) hh = bfr(hh);
+      gc[l * P + j] = cn;
+      gh[l * P + j] = hh;
+    }
+    memcpy(x, gh + l * P, sizeof(x));
+  }
+}
+
+/* Joint (modeling_rnnt.py:259-289): F = b_t + f.W1t^T, G = b_p + g.W1p^T (fp32 path:
+ * linear1_trans(f) += linear1_pred(g)); y1 = relu(F+G) (bf16 in bf16 mode); logits =
+ * b2 + y1.W2^T over the 29 real labels. */
+static void joint_F(const dec_w* d, const float* f, float* F) {
+  float fin[H_ENC];
+  for (int k = 0; k < H_ENC; ++k) fin[k] = d->bf16 ? bfr(f[k]) : f[k];
+  memcpy(F, d->bt, sizeof(float) * J);
+  chain_acc(F, fin, d->W1tT, H_ENC, J);
+}
+static void joint_G(const dec_w* d, const float* g, float* G) {
+  memcpy(G, d->bp, sizeof(float) * J);
+  chain_acc(G, g, d->W1pT, P, J);
+}
+static void joint_logits(const dec_w* d, const float* F, const float* G, float* logits) {
+  float y1[J];
+  for (int j = 0; j < J; ++j) {
+    const float s = F[j] + G[j];
+    const float r = s > 0.0f ? s : 0.0f;
+    y1[j] = d->bf16 ? bfr(r) : r;
+  }
+  memcpy(logits, d->b2, sizeof(float) * NLAB);
+  chain_acc(logits, y1, d->W2T, J, NLAB);
+}
+static int argmax29(const float* v) {  /* torch.argmax: first maximal index */
+  int best = 0;
+  for (int j = 1; j < NLAB; ++j)
+    if (v[j] > v[best]) best = j;
+  return best;
+}
+
+void oracle_greedy_decode(int Tp, int N, const float* f, const int32_t* f_lens, int bf16,
+                          const float* embed, const float* const* pWih,
+                          const float* const* pWhh, const float* const* pbih,
+                          const float* const* pbhh, const float* W1t, const float* W1p,
+                          const float* bt, const float* bp, const float* W2, const float* b2,
+                          int32_t* res, int32_t* res_len, int max_res, int32_t* steps) {
+  dec_w d = {bf16, embed, pWih, pWhh, pbih, pbhh, {0, 0}, {0, 0}, W1t, W1p, bt, bp, W2, b2, 0, 0, 0};
+  dec_w_init(&d);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int n = 0; n < N; ++n) {
+    float ph[2 * P] = {0}, pc[2 * P] = {0}, gh[2 * P], gc[2 * P];
+    float F[J], G[J], logits[NLAB];
+    int32_t* r = res + (size_t)n * max_res;
+    for (int i = 0; i < max_res; ++i) r[i] = SOS;
+    int pre_g = SOS, time = 0, added = 0, idx = -1, cand = 0, ftime = -1;
+    int adv = 0, emit = 0;
+    const int flen = f_lens[n];
+    int finish = (flen == 0);
+    while (!finish) {
+      if (!cand) {
+        pred_row(&d, pre_g, ph, pc, gh, gc);
+        joint_G(&d, gh + P, G);
+        cand = 1;
+      }
+      if (ftime != time) {
+        joint_F(&d, f + ((size_t)time * N + n) * H_ENC, F);
+        ftime = time;
+      }
+      joint_logits(&d, F, G, logits);
+      const int sym = argmax29(logits);
+      if (sym != BLANK && added != MAXSYM) {
+        ++idx;
+        if (idx < max_res) r[idx] = sym;
+        ++added;
+        pre_g = sym;
+        memcpy(ph, gh, sizeof(ph));
+        memcpy(pc, gc, sizeof(pc));
+        cand = 0;
+        ++emit;
+      } else {
+        ++time;
+        finish = time >= flen;
+        if (time > flen - 1) time = flen - 1;
+        added = 0;
+        ++adv;
+      }
+    }
+    res_len[n] = idx + 1;
+    if (steps) { steps[2 * n] = adv; steps[2 * n + 1] = emit; }
+  }
+  dec_w_free(&d);
+}
+
+void oracle_joint(int N, const float* f, const float* g, int bf16, const float* W1t,
+                  const float* W1p, const float* bt, const float* bp, const float* W2,
+                  const float* b2, float* logits) {
+  dec_w d;
+  memset(&d, 0, sizeof(d));
+  d.bf16 = bf16; d.W1t = W1t; d.W1p = W1p; d.bt = bt; d.bp = bp; d.W2 = W2; d.b2 = b2;
+  d.W1tT = (float*)malloc(sizeof(float) * J * H_ENC);
+  d.W1pT = (float*)malloc(sizeof(float) * J * P);
+  d.W2T = (float*)malloc(sizeof(float) * NLAB * J);
+  transpose_f32(W1t, J, H_ENC, d.W1tT);
+  transpose_f32(W1p, J, P, d.W1pT);
+  transpose_f32(W2, NLAB, J, d.W2T);
+#pragma omp parallel for
+  for (int n = 0; n < N; ++n) {
+    float F[J], G[J];
+    joint_F(&d, f + (size_t)n * H_ENC, F);
+    joint_G(&d, g + (size_t)n * P, G);
+    joint_logits(&d, F, G, logits + (size_t)n * NLAB);
+  }
+  free(d.W1tT); free(d.W1pT); free(d.W2T);
+}
+
+void oracle_prediction(int N, const int32_t* pre_g, const float* h, const float* c, int bf16,
+                       const float* embed, const float* const* pWih, const float* const* pWhh,
+                       const float* const* pbih, const float* const* pbhh, float* g_out,
+                       float* h_out, float* c_out) {
+  dec_w d;
+  memset(&d, 0, sizeof(d));
+  d.bf16 = bf16; d.embed = embed; d.Wih = pWih; d.Whh = pWhh; d.bih = pbih; d.bhh = pbhh;
+  for (int l = 0; l < 2; ++l) {
+    d.WihT[l] = (float*)malloc(sizeof(float) * 4 * P * P);
+    d.WhhT[l] = (float*)malloc(sizeof(float) * 4 * P * P);
+    transpose_f32(pWih[l], 4 * P, P, d.WihT[l]);
+    transpose_f32(pWhh[l], 4 * P, P, d.WhhT[l]);
+  }
+#pragma omp parallel for
+  for (int n = 0; n < N; ++n) {
+    float ph[2 * P], pc[2 * P], gh[2 * P], gc[2 * P];
+    for (int l = 0; l < 2; ++l) {
+      memcpy(ph + l * P, h + ((size_t)l * N + n) * P, sizeof(float) * P);
+      memcpy(pc + l * P, c + ((size_t)l * N + n) * P, sizeof(float) * P);
+    }
+    pred_row(&d, pre_g[n], ph, pc, gh, gc);
+    memcpy(g_out + (size_t)n * P, gh + P, sizeof(float) * P);
+    for (int l = 0; l < 2; ++l) {
+      memcpy(h_out + ((size_t)l * N + n) * P, gh + l * P, sizeof(float) * P);
+      memcpy(c_out + ((size_t)l * N + n) * P, gc + l * P, sizeof(float) * P);
+    }
+  }
+  for (int l = 0; l < 2; ++l) { free(d.WihT[l]); free(d.WhhT[l]); }
+}
