@@ -1,0 +1,112 @@
+/*
+ * rnnt_mi355x.h -- C ABI of the MI355X RNN-T inference engine (librnnt_mi355x.so).
+ *
+ * The drop-in boundary for the reference's hot path:
+ *   - rnnt_engine_encode / rnnt_engine_decode replace the bodies of
+ *     TorchModel::encode / TorchModel::decode (reference csrc/rnnt_model.hpp:62-90, 92-124),
+ *     called per batch by OfflineSUT::thInstance (csrc/torch_sut.cpp:208-212) and
+ *     ServerSUT::thConsumer (:529-531).  Results use the State::res_ / res_idx_ contract
+ *     (csrc/metadata.hpp:58-59, metadata.cpp:59-60): res [N][max_res] int32 filled with
+ *     SOS (-1), res_len[n] = res_idx_[n] + 1, read by QuerySamplesComplete (torch_sut.cpp:221-236).
+ *   - rnnt_engine_infer = encode + decode (TorchModel::forward, rnnt_model.hpp:56-60).
+ *   - the rnnt_op_* entry points back the torch.ops.intel_mlperf operator names the reference
+ *     TorchScript graph binds to (models/_C.py:15-51; schemas implied by the call sites in
+ *     quant_lstm.py:92-101 and modeling_rnnt.py:202-365), through the Python mirror
+ *     rnnt_amd/ops.py.
+ *
+ * Plain pointers and sizes only.  Device pointers are HIP device allocations on the engine's
+ * device; `stream` is a hipStream_t (NULL = the engine's own stream).  Every entry point
+ * returns 0 on success or a negative errno-style code; rnnt_last_error() describes the last
+ * failure on the calling thread.  One engine per GPU, driven by one host thread at a time;
+ * distinct engines are independent (the reference's per-socket model clones, rnnt_model.hpp:45-46).
+ */
+#ifndef RNNT_MI355X_H
+#define RNNT_MI355X_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RNNT_ABI_VERSION 1
+
+#define RNNT_OK 0
+#define RNNT_EINVAL (-22)
+#define RNNT_ENOMEM (-12)
+#define RNNT_EDEVICE (-5)
+
+typedef struct rnnt_engine rnnt_engine;
+
+/* Quantised / bf16 model in the reference's natural layouts (row = gate*H + unit, gate
+ * order i,f,g,o).  Encoder layers l = 0..4 are pre_rnn.lstm0, lstm1, post_rnn.lstm0..2 with
+ * input widths I = 256 (240 + zero pad), 1024, 2048, 1024, 1024 and K_l = I_l + 1024:
+ * enc_w[l] = [W_ih_q | W_hh_q] int8 [4096][K_l]  (iLSTMLayer._quant_parameters, quant_lstm.py:193-215)
+ * enc_bq[l] = (b_ih + b_hh) * s_in * s_w          fp32 [4096]
+ * enc_rb / enc_in_s / enc_out_s                   the lstm_amx_int8 scale tensors (quant_lstm.py:92-101)
+ * bf16 arrays hold bf16 bit patterns (torch .to(torch.bfloat16) of the checkpoint). */
+typedef struct {
+  const int8_t* enc_w[5];
+  const float* enc_bq[5];
+  float enc_rb[5], enc_in_s[5], enc_out_s[5];
+  const uint16_t* embed;        /* bf16 [28][320] */
+  const uint16_t* pred_w_ih[2]; /* bf16 [1280][320] */
+  const uint16_t* pred_w_hh[2]; /* bf16 [1280][320] */
+  const float* pred_b_ih[2];    /* fp32 [1280] */
+  const float* pred_b_hh[2];    /* fp32 [1280] */
+  const uint16_t* joint_w1t;    /* bf16 [512][1024]  joint.linear1_trans */
+  const uint16_t* joint_w1p;    /* bf16 [512][320]   joint.linear1_pred */
+  const float* joint_bt;        /* fp32 [512] */
+  const float* joint_bp;        /* fp32 [512] */
+  const uint16_t* joint_w2;     /* bf16 [29][512]    joint.linear2 */
+  const float* joint_b2;        /* fp32 [29] */
+} rnnt_model_desc;
+
+typedef struct {
+  int max_batch;   /* utterances per encode/decode call (default 1024) */
+  int max_frames;  /* feature frames per utterance (default 500 = MAX_FEA_LEN, metadata.hpp:32) */
+  int max_res;     /* result row length (default max_frames/2*30 = 7500, metadata.hpp:58-59) */
+} rnnt_opts;
+
+int rnnt_abi_version(void);
+const char* rnnt_last_error(void);
+
+/* Packs the model into the engine's device layouts on `device` and sizes the workspace. */
+int rnnt_engine_create(const rnnt_model_desc* model, int device, const rnnt_opts* opts, rnnt_engine** out);
+void rnnt_engine_destroy(rnnt_engine* e);
+
+/* Encoder: feats device fp32 [T][n_pad][256] (the QSL's AssembleSamples layout, rnnt_qsl.cpp:150-188,
+ * zero past lens and in channels 240..255), lens device int32 [n_pad] (0 for batch padding), lens_host
+ * the same lengths on the host (drive the active-tile schedule; may be NULL = all T frames).
+ * Keeps the encoder output (f, f_lens = ceil(lens/2)) in the engine for rnnt_engine_decode; if
+ * f_out != NULL also writes f there, device fp32 [ceil(T/2)][n_pad][1024].
+ * n_pad must be >= n, a multiple of 128, <= max_batch rounded up to 128. */
+int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
+                       int T, int n, int n_pad, float* f_out, void* stream);
+
+/* Greedy decode of the last encoded batch: res device int32 [n][max_res] (filled with -1 first),
+ * res_len device int32 [n]. */
+int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream);
+
+/* encode + decode. */
+int rnnt_engine_infer(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host, int T,
+                      int n, int n_pad, int32_t* res, int32_t* res_len, int max_res, void* stream);
+
+/* ---- operator-level entry points (torch.ops.intel_mlperf mirror, rnnt_amd/ops.py) ---- */
+
+/* lstm_amx_int8 for the engine's encoder layers [first, first+count): x = layer `first` input
+ * (fp32 [T][n_pad][256] when first == 0, quantised in-kernel with in_s[0]; else int8
+ * [T][n_pad][I_first]); hx int8 [count][n_pad][1024] and cx fp16 [count][n_pad][1024] in/out;
+ * y: int8 [T][n_pad][1024], or fp32 when the last layer is the encoder's final layer (skip_quant_y).
+ * Stacking between layers 1 and 2 is NOT applied here (callers use rnnt_op_stack_time). */
+int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const void* x, int T, int n_pad, int8_t* hx,
+                      uint16_t* cx, void* y, void* stream);
+
+/* stack_time(x int8 [T][n_pad][C], x_lens int32 [n_pad], factor 2) -> y int8 [ceil(T/2)][n_pad][2C]
+ * (modeling_rnnt.py:326-328). */
+int rnnt_op_stack_time(rnnt_engine* e, const int8_t* x, const int32_t* x_lens, int T, int n_pad, int C,
+                       int8_t* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

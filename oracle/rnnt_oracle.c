@@ -125,47 +125,56 @@ void oracle_lstm_i8_layer(int T, int N, int I, int H, const int8_t* x, const int
                           const float* bq, float rb, float in_s, float out_s, int skip_quant_y,
                           int8_t* h, uint16_t* c, int8_t* y8, float* y32) {
   const int K = I + H;
-#pragma omp parallel for schedule(dynamic, 1)
-  for (int n = 0; n < N; ++n) {
-    int32_t* acc = (int32_t*)malloc(sizeof(int32_t) * 4 * (size_t)H);
-    int8_t* hv = (int8_t*)malloc((size_t)H);
-    int8_t* hn = (int8_t*)malloc((size_t)H);
-    memcpy(hv, h + (size_t)n * H, (size_t)H);
-    uint16_t* cv = c + (size_t)n * H;
-    for (int t = 0; t < T; ++t) {
-      const int8_t* xt = x + ((size_t)t * N + n) * I;
-      for (int r = 0; r < 4 * H; ++r) {
-        const int8_t* w = W + (size_t)r * K;
+  /* acc[n][r] for the whole batch per step: the loop runs gate rows outermost so each
+   * weight row is streamed once per step and reused across the N batch rows (int32 sums are
+   * exact, so the order is free). */
+  int32_t* acc = (int32_t*)malloc(sizeof(int32_t) * (size_t)N * 4 * H);
+  int8_t* hv = (int8_t*)malloc((size_t)N * H);
+  int8_t* hn = (int8_t*)malloc((size_t)N * H);
+  memcpy(hv, h, (size_t)N * H);
+  for (int t = 0; t < T; ++t) {
+    const int8_t* xt = x + (size_t)t * N * I;
+#pragma omp parallel for schedule(static)
+    for (int r = 0; r < 4 * H; ++r) {
+      const int8_t* w = W + (size_t)r * K;
+      for (int n = 0; n < N; ++n) {
+        const int8_t* xr = xt + (size_t)n * I;
+        const int8_t* hr = hv + (size_t)n * H;
         int32_t s = 0;
-        for (int k = 0; k < I; ++k) s += (int32_t)xt[k] * (int32_t)w[k];
-        for (int k = 0; k < H; ++k) s += (int32_t)hv[k] * (int32_t)w[I + k];
-        acc[r] = s;
+        for (int k = 0; k < I; ++k) s += (int32_t)xr[k] * (int32_t)w[k];
+        for (int k = 0; k < H; ++k) s += (int32_t)hr[k] * (int32_t)w[I + k];
+        acc[(size_t)n * 4 * H + r] = s;
       }
+    }
+#pragma omp parallel for schedule(static)
+    for (int n = 0; n < N; ++n) {
+      const int32_t* a = acc + (size_t)n * 4 * H;
+      uint16_t* cv = c + (size_t)n * H;
       for (int j = 0; j < H; ++j) {
-        const float pi = ((float)acc[j] + bq[j]) * rb;
-        const float pf = ((float)acc[H + j] + bq[H + j]) * rb;
-        const float pg = ((float)acc[2 * H + j] + bq[2 * H + j]) * rb;
-        const float po = ((float)acc[3 * H + j] + bq[3 * H + j]) * rb;
+        const float pi = ((float)a[j] + bq[j]) * rb;
+        const float pf = ((float)a[H + j] + bq[H + j]) * rb;
+        const float pg = ((float)a[2 * H + j] + bq[2 * H + j]) * rb;
+        const float po = ((float)a[3 * H + j] + bq[3 * H + j]) * rb;
         const float ig = oracle_sigmoid(pi), fg = oracle_sigmoid(pf);
         const float gg = oracle_tanh(pg), og = oracle_sigmoid(po);
         const float cp = oracle_h2f(cv[j]);
         const float cn = fg * cp + ig * gg;
         cv[j] = oracle_f2h(cn);
         const float hh = og * oracle_tanh(cn);
-        hn[j] = oracle_q8(hh * in_s);
+        hn[(size_t)n * H + j] = oracle_q8(hh * in_s);
         const size_t o = ((size_t)t * N + n) * H + j;
         if (skip_quant_y)
           y32[o] = hh;
         else
           y8[o] = oracle_q8(hh * out_s);
       }
-      memcpy(hv, hn, (size_t)H);
     }
-    memcpy(h + (size_t)n * H, hv, (size_t)H);
-    free(acc);
-    free(hv);
-    free(hn);
+    int8_t* tmp = hv; hv = hn; hn = tmp;
   }
+  memcpy(h, hv, (size_t)N * H);
+  free(acc);
+  free(hv);
+  free(hn);
 }
 
 /* StackTime.forward_f32 (modeling_rnnt.py:314-324) / intel_mlperf::stack_time (:327). */

@@ -1,0 +1,38 @@
+// decoder.hpp -- launch interface of the prediction / joint / greedy kernels (engine-internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rnnt {
+
+constexpr int DEC_ROWS = 16;  // utterances per greedy-decode workgroup
+
+struct DecWeights {
+  const uint16_t* embed;   // bf16 [28][320] natural
+  const uint16_t* wp[2];   // bf16 [1280][640] gate-interleaved rows, chain-permuted k ([W_ih | W_hh])
+  const float* bp_lstm[2]; // fp32 [1280] b_ih + b_hh, gate-interleaved
+  const uint16_t* w1t;     // bf16 [512][1024] chain-permuted k
+  const uint16_t* w1p;     // bf16 [512][320]  chain-permuted k
+  const float* bt;         // [512]
+  const float* bp;         // [512]
+  const uint16_t* w2;      // bf16 [32][512] chain-permuted k (rows 29..31 zero)
+  const float* b2;         // [32] (29..31 zero)
+};
+
+struct DecArgs {
+  DecWeights w;
+  const float* F;          // [Tp][Npad][512] joint trans half, F = b_t + bf16(f).W1t^T
+  const int32_t* f_lens;   // [Npad]
+  float* hc;               // [Npad][2 slots][4][320] (h0, h1, c0, c1) prediction state
+  float* G;                // [Npad][512] joint pred half of the current candidate
+  int32_t* res;            // [N][max_res]
+  int32_t* res_len;        // [N]
+  int N, Npad, max_res, max_iter;
+};
+
+// F = b_t + bf16(f) . W1t^T for every frame t < Tp and row tile holding a row with f_len > t.
+int launch_joint_trans(const DecWeights& w, const uint16_t* fperm, const int32_t* f_lens, float* F, int Tp,
+                       int Npad, hipStream_t st);
+int launch_greedy_decode(const DecArgs& a, hipStream_t st);
+
+}  // namespace rnnt

@@ -1,0 +1,34 @@
+// encoder.hpp -- launch interface of the int8 encoder kernels (internal to the engine).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rnnt {
+
+constexpr int ENC_BATCH_TILE = 128;  // batch rows per encoder workgroup (buffers padded to it)
+
+enum EncOutMode { ENC_OUT_I8 = 0, ENC_OUT_STACKED = 1, ENC_OUT_FINAL = 2 };
+
+struct EncStepArgs {
+  const int8_t* W;     // packed [4096][I+1024], gate-interleaved rows
+  const float* bq;     // packed [4096]
+  const int8_t* x;     // this frame's input rows: [Npad][I]
+  const int8_t* h_in;  // [Npad][1024] h_{t-1} (quantised with in_s)
+  int8_t* h_out;       // [Npad][1024] h_t
+  uint16_t* c;         // [Npad][1024] fp16 cell state, in place
+  int8_t* y8;          // I8: [Npad][1024] frame rows; STACKED: [Npad][2048] stacked frame rows
+  float* y32;          // FINAL: optional fp32 f rows [Npad][1024]
+  uint16_t* fperm;     // FINAL: bf16 f rows [Npad][1024] in chain-permuted k order
+  const int32_t* lens; // [Npad] feature lengths (STACKED masking)
+  int I;               // input width (256 / 1024 / 2048)
+  int mode;            // EncOutMode
+  int t;               // frame index (STACKED)
+  int half;            // t % 2 (STACKED)
+  int zero_next;       // STACKED: also zero the odd-T pad half
+  float rb, in_s, out_s;
+};
+
+int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStream_t st);
+int launch_lstm_i8_step(const EncStepArgs& a, int n_tiles, hipStream_t st);
+
+}  // namespace rnnt

@@ -1,0 +1,385 @@
+// engine.hip -- C ABI of the MI355X RNN-T engine (include/rnnt_mi355x.h).
+//
+// Host side: model packing into device layouts, workspace management and the per-batch
+// launch schedule (the replacement of TorchModel::encode / decode, reference
+// csrc/rnnt_model.hpp:62-124).  No torch types anywhere: plain pointers and sizes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/rnnt_mi355x.h"
+#include "decoder.hpp"
+#include "encoder.hpp"
+#include "rnnt_device.hpp"
+
+using namespace rnnt;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) return fail(RNNT_EDEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static const int ENC_I[5] = {256, 1024, 2048, 1024, 1024};
+
+struct rnnt_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  rnnt_opts opts{};
+  int np_max = 0, tp_max = 0;
+  // packed weights
+  int8_t* enc_w[5] = {};
+  float* enc_bq[5] = {};
+  float rb[5], in_s[5], out_s[5];
+  DecWeights dw{};
+  std::vector<void*> allocs;
+  // workspace
+  int8_t *x0q = nullptr, *yA = nullptr, *xs = nullptr, *yB = nullptr;
+  int8_t* h[5][2] = {};
+  uint16_t* c[5] = {};
+  uint16_t* fperm = nullptr;
+  float *F = nullptr, *hc = nullptr, *G = nullptr;
+  int32_t* flen = nullptr;
+  // last encoded batch
+  int last_T = 0, last_n = 0, last_npad = 0;
+};
+
+template <class T>
+static int dev_alloc(rnnt_engine* e, T** p, size_t count) {
+  void* q = nullptr;
+  if (hipMalloc(&q, count * sizeof(T) + 256) != hipSuccess) return fail(RNNT_ENOMEM, "hipMalloc failed");
+  e->allocs.push_back(q);
+  *p = (T*)q;
+  return 0;
+}
+template <class T>
+static int upload(rnnt_engine* e, T** p, const std::vector<T>& host) {
+  int r = dev_alloc(e, p, host.size());
+  if (r) return r;
+  HIPCHK(hipMemcpy(*p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+extern "C" int rnnt_abi_version(void) { return RNNT_ABI_VERSION; }
+extern "C" const char* rnnt_last_error(void) { return g_err.c_str(); }
+
+// ---- packing (natural layouts -> device layouts; see DESIGN.md "Data layout in HBM")
+static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
+  for (int l = 0; l < 5; ++l) {
+    if (!m->enc_w[l] || !m->enc_bq[l]) return fail(RNNT_EINVAL, "null encoder weight");
+    const int K = ENC_I[l] + H;
+    std::vector<int8_t> w((size_t)G4 * K);
+    std::vector<float> b(G4);
+    for (int g = 0; g < 4; ++g)
+      for (int u = 0; u < H; ++u) {
+        memcpy(&w[(size_t)(4 * u + g) * K], m->enc_w[l] + (size_t)(g * H + u) * K, K);
+        b[4 * u + g] = m->enc_bq[l][g * H + u];
+      }
+    int r = upload(e, &e->enc_w[l], w);
+    if (!r) r = upload(e, &e->enc_bq[l], b);
+    if (r) return r;
+    e->rb[l] = m->enc_rb[l];
+    e->in_s[l] = m->enc_in_s[l];
+    e->out_s[l] = m->enc_out_s[l];
+  }
+  // prediction LSTM: rows gate-interleaved, k = [W_ih | W_hh] chain-permuted, fused bias
+  for (int l = 0; l < 2; ++l) {
+    if (!m->pred_w_ih[l] || !m->pred_w_hh[l] || !m->pred_b_ih[l] || !m->pred_b_hh[l])
+      return fail(RNNT_EINVAL, "null prediction weight");
+    std::vector<uint16_t> w((size_t)PG4 * 640);
+    std::vector<float> b(PG4);
+    for (int g = 0; g < 4; ++g)
+      for (int u = 0; u < P; ++u) {
+        const int src = g * P + u, dst = 4 * u + g;
+        for (int k = 0; k < 640; ++k)
+          w[(size_t)dst * 640 + chain_pos(k)] =
+              k < P ? m->pred_w_ih[l][(size_t)src * P + k] : m->pred_w_hh[l][(size_t)src * P + k - P];
+        b[dst] = m->pred_b_ih[l][src] + m->pred_b_hh[l][src];  // fp32 add, as the oracle
+      }
+    uint16_t* dwp;
+    float* dbp;
+    int r = upload(e, &dwp, w);
+    if (!r) r = upload(e, &dbp, b);
+    if (r) return r;
+    e->dw.wp[l] = dwp;
+    e->dw.bp_lstm[l] = dbp;
+  }
+  auto permute_rows = [](const uint16_t* src, int rows, int rows_pad, int K) {
+    std::vector<uint16_t> w((size_t)rows_pad * K, 0);
+    for (int r = 0; r < rows; ++r)
+      for (int k = 0; k < K; ++k) w[(size_t)r * K + chain_pos(k)] = src[(size_t)r * K + k];
+    return w;
+  };
+  if (!m->embed || !m->joint_w1t || !m->joint_w1p || !m->joint_w2 || !m->joint_bt || !m->joint_bp || !m->joint_b2)
+    return fail(RNNT_EINVAL, "null joint/embedding weight");
+  uint16_t *emb, *w1t, *w1p, *w2;
+  float *bt, *bp, *b2;
+  int r = upload(e, &emb, std::vector<uint16_t>(m->embed, m->embed + 28 * P));
+  if (!r) r = upload(e, &w1t, permute_rows(m->joint_w1t, J, J, H));
+  if (!r) r = upload(e, &w1p, permute_rows(m->joint_w1p, J, J, P));
+  if (!r) r = upload(e, &w2, permute_rows(m->joint_w2, NLAB, NLAB_PAD, J));
+  if (!r) r = upload(e, &bt, std::vector<float>(m->joint_bt, m->joint_bt + J));
+  if (!r) r = upload(e, &bp, std::vector<float>(m->joint_bp, m->joint_bp + J));
+  if (!r) {
+    std::vector<float> b(NLAB_PAD, 0.0f);
+    std::copy(m->joint_b2, m->joint_b2 + NLAB, b.begin());
+    r = upload(e, &b2, b);
+  }
+  if (r) return r;
+  e->dw.embed = emb; e->dw.w1t = w1t; e->dw.w1p = w1p; e->dw.w2 = w2;
+  e->dw.bt = bt; e->dw.bp = bp; e->dw.b2 = b2;
+  return 0;
+}
+
+static int alloc_workspace(rnnt_engine* e) {
+  const size_t NP = e->np_max, TM = e->opts.max_frames, TPM = e->tp_max;
+  int r = 0;
+  r = r ? r : dev_alloc(e, &e->x0q, TM * NP * FEAT);
+  r = r ? r : dev_alloc(e, &e->yA, TM * NP * H);
+  r = r ? r : dev_alloc(e, &e->xs, TPM * NP * 2 * H);
+  r = r ? r : dev_alloc(e, &e->yB, TPM * NP * H);
+  for (int l = 0; l < 5 && !r; ++l) {
+    r = r ? r : dev_alloc(e, &e->h[l][0], NP * H);
+    r = r ? r : dev_alloc(e, &e->h[l][1], NP * H);
+    r = r ? r : dev_alloc(e, &e->c[l], NP * H);
+  }
+  r = r ? r : dev_alloc(e, &e->fperm, TPM * NP * H);
+  r = r ? r : dev_alloc(e, &e->F, TPM * NP * J);
+  r = r ? r : dev_alloc(e, &e->hc, NP * 2 * 4 * P);
+  r = r ? r : dev_alloc(e, &e->G, NP * J);
+  r = r ? r : dev_alloc(e, &e->flen, NP);
+  return r;
+}
+
+extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  for (void* p : e->allocs) (void)hipFree(p);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, const rnnt_opts* opts,
+                                  rnnt_engine** out) {
+  if (!model || !out) return fail(RNNT_EINVAL, "null argument");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RNNT_EDEVICE, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(RNNT_EINVAL, "bad device index");
+  rnnt_engine* e = new rnnt_engine();
+  e->device = device;
+  e->opts.max_batch = (opts && opts->max_batch > 0) ? opts->max_batch : 1024;
+  e->opts.max_frames = (opts && opts->max_frames > 0) ? opts->max_frames : 500;
+  e->opts.max_res = (opts && opts->max_res > 0) ? opts->max_res : (e->opts.max_frames / 2) * MAXSYM;
+  e->np_max = (e->opts.max_batch + ENC_BATCH_TILE - 1) / ENC_BATCH_TILE * ENC_BATCH_TILE;
+  e->tp_max = (e->opts.max_frames + 1) / 2;
+  int r = 0;
+  if (hipSetDevice(device) != hipSuccess) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
+  if (!r && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+    r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
+  if (!r) r = pack_model(e, model);
+  if (!r) r = alloc_workspace(e);
+  if (r) {
+    rnnt_engine_destroy(e);
+    return r;
+  }
+  *out = e;
+  return 0;
+}
+
+// ---- small utility kernels
+__global__ void flen_kernel(const int32_t* lens, int32_t* flen, int n_pad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_pad) flen[i] = (lens[i] + 1) / 2;  // ceil(x_lens / stack_time_factor)
+}
+__global__ void stack_time_kernel(const int8_t* x, const int32_t* lens, int T, int n_pad, int C, int8_t* y) {
+  const int tp = blockIdx.y, n = blockIdx.x;
+  for (int i = threadIdx.x * 16; i < 2 * C; i += blockDim.x * 16) {
+    const int half = i / C, t = 2 * tp + half, k = i % C;
+    uint4 v = {0, 0, 0, 0};
+    if (t < T && t < lens[n]) v = *(const uint4*)(x + ((size_t)t * n_pad + n) * C + k);
+    *(uint4*)(y + ((size_t)tp * n_pad + n) * 2 * C + i) = v;
+  }
+}
+
+static hipStream_t pick(rnnt_engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
+
+// number of leading 128-row tiles that hold a row with len > thr
+static int active_tiles(const std::vector<int>& tile_max, int thr) {
+  int last = -1;
+  for (int i = 0; i < (int)tile_max.size(); ++i)
+    if (tile_max[i] > thr) last = i;
+  return last + 1;
+}
+
+static int run_layer(rnnt_engine* e, int l, int T, int n_pad, const int8_t* x, int mode, void* y,
+                     float* y32, const std::vector<int>& tile_max, const int32_t* lens, hipStream_t st,
+                     int stacked_T = 0) {
+  const int I = ENC_I[l];
+  for (int t = 0; t < T; ++t) {
+    EncStepArgs a{};
+    a.W = e->enc_w[l];
+    a.bq = e->enc_bq[l];
+    a.x = x + (size_t)t * n_pad * I;
+    a.h_in = e->h[l][t & 1];
+    a.h_out = e->h[l][(t + 1) & 1];
+    a.c = e->c[l];
+    a.I = I;
+    a.mode = mode;
+    a.rb = e->rb[l];
+    a.in_s = e->in_s[l];
+    a.out_s = e->out_s[l];
+    a.lens = lens;
+    int thr;
+    if (mode == ENC_OUT_STACKED) {
+      a.y8 = (int8_t*)y + (size_t)(t / 2) * n_pad * 2 * H;
+      a.t = t;
+      a.half = t & 1;
+      a.zero_next = ((t & 1) == 0 && t + 1 == stacked_T);
+      thr = 2 * (t / 2);
+    } else if (mode == ENC_OUT_I8) {
+      a.y8 = (int8_t*)y + (size_t)t * n_pad * H;
+      thr = l < 2 ? 2 * (t / 2) : 2 * t;
+    } else {
+      a.y32 = y32 ? y32 + (size_t)t * n_pad * H : nullptr;
+      a.fperm = (uint16_t*)y + (size_t)t * n_pad * H;
+      thr = 2 * t;
+    }
+    const int nt = tile_max.empty() ? n_pad / ENC_BATCH_TILE : active_tiles(tile_max, thr);
+    if (launch_lstm_i8_step(a, nt, st)) return fail(RNNT_EDEVICE, "lstm step launch failed");
+  }
+  return 0;
+}
+
+static int check_batch(rnnt_engine* e, int T, int n, int n_pad) {
+  if (T <= 0 || T > e->opts.max_frames) return fail(RNNT_EINVAL, "T out of range");
+  if (n <= 0 || n_pad < n || n_pad % ENC_BATCH_TILE || n_pad > e->np_max)
+    return fail(RNNT_EINVAL, "n / n_pad out of range (n_pad must be a multiple of 128 <= max_batch)");
+  return 0;
+}
+
+static std::vector<int> tile_maxima(const int32_t* lens_host, int n, int n_pad) {
+  std::vector<int> tm;
+  if (!lens_host) return tm;
+  tm.assign(n_pad / ENC_BATCH_TILE, 0);
+  for (int i = 0; i < n; ++i) tm[i / ENC_BATCH_TILE] = std::max(tm[i / ENC_BATCH_TILE], (int)lens_host[i]);
+  return tm;
+}
+
+extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
+                                  int T, int n, int n_pad, float* f_out, void* stream) {
+  if (!e || !feats || !lens) return fail(RNNT_EINVAL, "null argument");
+  int r = check_batch(e, T, n, n_pad);
+  if (r) return r;
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = pick(e, stream);
+  const int Tp = (T + 1) / 2;
+  const std::vector<int> tm = tile_maxima(lens_host, n, n_pad);
+  for (int l = 0; l < 5; ++l) {
+    HIPCHK(hipMemsetAsync(e->h[l][0], 0, (size_t)n_pad * H, st));
+    HIPCHK(hipMemsetAsync(e->c[l], 0, (size_t)n_pad * H * 2, st));
+  }
+  if (launch_quantize(feats, (int64_t)T * n_pad * FEAT, e->in_s[0], e->x0q, st))
+    return fail(RNNT_EDEVICE, "quantize launch failed");
+  if ((r = run_layer(e, 0, T, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, tm, lens, st))) return r;
+  if ((r = run_layer(e, 1, T, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, tm, lens, st, T))) return r;
+  if ((r = run_layer(e, 2, Tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, tm, lens, st))) return r;
+  if ((r = run_layer(e, 3, Tp, n_pad, e->yB, ENC_OUT_I8, e->yA, nullptr, tm, lens, st))) return r;
+  if ((r = run_layer(e, 4, Tp, n_pad, e->yA, ENC_OUT_FINAL, e->fperm, f_out, tm, lens, st))) return r;
+  hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->flen, n_pad);
+  HIPCHK(hipGetLastError());
+  e->last_T = T;
+  e->last_n = n;
+  e->last_npad = n_pad;
+  return 0;
+}
+
+extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream) {
+  if (!e || !res || !res_len) return fail(RNNT_EINVAL, "null argument");
+  if (e->last_n <= 0) return fail(RNNT_EINVAL, "decode before encode");
+  if (max_res <= 0) return fail(RNNT_EINVAL, "max_res must be positive");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = pick(e, stream);
+  const int Tp = (e->last_T + 1) / 2;
+  if (launch_joint_trans(e->dw, e->fperm, e->flen, e->F, Tp, e->last_npad, st))
+    return fail(RNNT_EDEVICE, "joint_trans launch failed");
+  DecArgs a{};
+  a.w = e->dw;
+  a.F = e->F;
+  a.f_lens = e->flen;
+  a.hc = e->hc;
+  a.G = e->G;
+  a.res = res;
+  a.res_len = res_len;
+  a.N = e->last_n;
+  a.Npad = e->last_npad;
+  a.max_res = max_res;
+  a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
+  if (launch_greedy_decode(a, st)) return fail(RNNT_EDEVICE, "greedy launch failed");
+  return 0;
+}
+
+extern "C" int rnnt_engine_infer(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
+                                 int T, int n, int n_pad, int32_t* res, int32_t* res_len, int max_res, void* stream) {
+  int r = rnnt_engine_encode(e, feats, lens, lens_host, T, n, n_pad, nullptr, stream);
+  return r ? r : rnnt_engine_decode(e, res, res_len, max_res, stream);
+}
+
+extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const void* x, int T, int n_pad, int8_t* hx,
+                                 uint16_t* cx, void* y, void* stream) {
+  if (!e || !x || !hx || !cx || !y) return fail(RNNT_EINVAL, "null argument");
+  if (first < 0 || count <= 0 || first + count > 5) return fail(RNNT_EINVAL, "bad layer range");
+  if (T <= 0 || T > e->opts.max_frames || n_pad <= 0 || n_pad % ENC_BATCH_TILE || n_pad > e->np_max)
+    return fail(RNNT_EINVAL, "T / n_pad out of range");
+  if (first <= 1 && first + count > 2) return fail(RNNT_EINVAL, "a call covers pre_rnn or post_rnn, not both");
+  if (first >= 2 && T > e->tp_max) return fail(RNNT_EINVAL, "post_rnn T exceeds ceil(max_frames/2)");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = pick(e, stream);
+  const int8_t* cur = (const int8_t*)x;
+  if (first == 0) {
+    if (launch_quantize((const float*)x, (int64_t)T * n_pad * FEAT, e->in_s[0], e->x0q, st))
+      return fail(RNNT_EDEVICE, "quantize launch failed");
+    cur = e->x0q;
+  }
+  const std::vector<int> none;
+  for (int i = 0; i < count; ++i) {
+    const int l = first + i;
+    const size_t NH = (size_t)n_pad * H;
+    HIPCHK(hipMemcpyAsync(e->h[l][0], hx + i * NH, NH, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(e->c[l], cx + i * NH, NH * 2, hipMemcpyDeviceToDevice, st));
+    const bool last = (i == count - 1);
+    int8_t* dst = last ? (int8_t*)y : ((cur == e->yA) ? e->yB : e->yA);
+    int r;
+    if (l == 4)
+      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_FINAL, e->fperm, (float*)y, none, nullptr, st);
+    else
+      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_I8, dst, nullptr, none, nullptr, st);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(hx + i * NH, e->h[l][T & 1], NH, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(cx + i * NH, e->c[l], NH * 2, hipMemcpyDeviceToDevice, st));
+    cur = dst;
+  }
+  return 0;
+}
+
+extern "C" int rnnt_op_stack_time(rnnt_engine* e, const int8_t* x, const int32_t* x_lens, int T, int n_pad, int C,
+                                  int8_t* y, void* stream) {
+  if (!e || !x || !x_lens || !y) return fail(RNNT_EINVAL, "null argument");
+  if (T <= 0 || n_pad <= 0 || C <= 0 || C % 16) return fail(RNNT_EINVAL, "bad shape");
+  HIPCHK(hipSetDevice(e->device));
+  hipLaunchKernelGGL(stack_time_kernel, dim3(n_pad, (T + 1) / 2), dim3(64), 0, pick(e, stream), x, x_lens, T, n_pad,
+                     C, y);
+  HIPCHK(hipGetLastError());
+  return 0;
+}

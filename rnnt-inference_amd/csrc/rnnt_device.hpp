@@ -1,0 +1,103 @@
+// rnnt_device.hpp -- device numerics and fragment helpers shared by the engine's kernels.
+//
+// The numerics contract (DESIGN.md "Numerics contract") is defined operation-by-operation so
+// the HIP engine and the CPU restatement (oracle/rnnt_oracle.c) agree bit-for-bit:
+// IEEE fp32 mul/add/div/fma and round-to-nearest-even everywhere, explicit fmaf, and the
+// whole library is compiled with -ffp-contract=off.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rnnt {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int H = 1024;      // encoder hidden
+constexpr int G4 = 4 * H;    // encoder gate rows
+constexpr int P = 320;       // prediction hidden
+constexpr int PG4 = 4 * P;   // prediction gate rows
+constexpr int J = 512;       // joint hidden
+constexpr int NLAB = 29;
+constexpr int NLAB_PAD = 32;
+constexpr int BLANK = 28;
+constexpr int SOS = -1;
+constexpr int MAXSYM = 30;
+constexpr int FEAT = 256;    // padded feature channels
+
+__device__ __forceinline__ float bits2f(uint32_t u) { return __uint_as_float(u); }
+__device__ __forceinline__ uint32_t f2bits(float f) { return __float_as_uint(f); }
+
+// Cephes-style expf with explicit fmaf (bit-identical to oracle_exp).
+__device__ __forceinline__ float det_exp(float x) {
+  x = __builtin_fminf(__builtin_fmaxf(x, -87.0f), 88.0f);
+  const float n = __builtin_rintf(x * 1.44269504088896341f);
+  float r = __builtin_fmaf(n, -0.693359375f, x);
+  r = __builtin_fmaf(n, 2.12194440e-4f, r);
+  const float z = r * r;
+  float p = 1.9875691500e-4f;
+  p = __builtin_fmaf(p, r, 1.3981999507e-3f);
+  p = __builtin_fmaf(p, r, 8.3334519073e-3f);
+  p = __builtin_fmaf(p, r, 4.1665795894e-2f);
+  p = __builtin_fmaf(p, r, 1.6666665459e-1f);
+  p = __builtin_fmaf(p, r, 5.0000001201e-1f);
+  p = __builtin_fmaf(p, z, r);
+  p = p + 1.0f;
+  const int e = (int)n;
+  return p * bits2f((uint32_t)(e + 127) << 23);
+}
+__device__ __forceinline__ float det_sigmoid(float x) { return 1.0f / (1.0f + det_exp(-x)); }
+__device__ __forceinline__ float det_tanh(float x) {
+  const float a = __builtin_fabsf(x);
+  const float e = det_exp(-2.0f * a);
+  const float t = (1.0f - e) / (1.0f + e);
+  return __builtin_copysignf(t, x);
+}
+
+__device__ __forceinline__ uint16_t f2h(float f) {
+  const uint32_t x = f2bits(f), sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);
+  if (ax >= 0x38800000u) {
+    uint32_t r = ax - 0x38000000u;
+    r = r + 0xfffu + ((r >> 13) & 1u);
+    return (uint16_t)(sign | (r >> 13));
+  }
+  if (ax < 0x33000000u) return (uint16_t)sign;
+  const uint32_t e = ax >> 23, m = (ax & 0x7fffffu) | 0x800000u, shift = 126u - e;
+  uint32_t q = m >> shift;
+  const uint32_t rem = m & ((1u << shift) - 1u), half = 1u << (shift - 1u);
+  if (rem > half || (rem == half && (q & 1u))) q++;
+  return (uint16_t)(sign | q);
+}
+__device__ __forceinline__ float h2f(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  if (e == 0) {
+    const float v = (float)m * 5.9604644775390625e-8f;
+    return sign ? -v : v;
+  }
+  if (e == 31) return bits2f(sign | 0x7f800000u | (m << 13));
+  return bits2f(sign | ((e + 112u) << 23) | (m << 13));
+}
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  const uint32_t u = f2bits(f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf2f(uint16_t b) { return bits2f((uint32_t)b << 16); }
+__device__ __forceinline__ float bf_round(float x) { return bf2f(f2bf(x)); }
+__device__ __forceinline__ int8_t q8(float v) {
+  float r = __builtin_rintf(v);
+  r = __builtin_fminf(__builtin_fmaxf(r, -128.0f), 127.0f);
+  return (int8_t)(int)r;
+}
+
+// "chain-permuted" k layout used by every fp32-chain (f32 MFMA 16x16x4) operand: inside each
+// 32-wide k block, position 8q + i holds k = 4i + q, so one 16-byte (bf16) / 32-byte (f32)
+// per-lane read feeds lane-group q of 8 consecutive MFMAs (instruction i covers k = 4i..4i+3,
+// lane group q = lane>>4 holding k = 4i+q: a k-ordered fmaf chain, probe-verified).
+__host__ __device__ __forceinline__ int chain_pos(int k) {
+  const int b = k >> 5, r = k & 31;
+  return (b << 5) + ((r & 3) << 3) + (r >> 2);
+}
+
+}  // namespace rnnt

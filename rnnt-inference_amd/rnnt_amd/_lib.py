@@ -1,0 +1,90 @@
+"""ctypes binding of librnnt_mi355x.so (C ABI: include/rnnt_mi355x.h).
+
+The HIP engine is the only compute path: there is no CPU or eager-PyTorch fallback, and a
+missing or unloadable library raises instead of silently degrading.
+"""
+import ctypes as C
+import os
+import re
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librnnt_mi355x.so")
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "rnnt_mi355x.h")
+
+RNNT_OK, RNNT_EINVAL, RNNT_ENOMEM, RNNT_EDEVICE = 0, -22, -12, -5
+
+
+class RnntModelDesc(C.Structure):
+    _fields_ = [
+        ("enc_w", C.c_void_p * 5), ("enc_bq", C.c_void_p * 5),
+        ("enc_rb", C.c_float * 5), ("enc_in_s", C.c_float * 5), ("enc_out_s", C.c_float * 5),
+        ("embed", C.c_void_p),
+        ("pred_w_ih", C.c_void_p * 2), ("pred_w_hh", C.c_void_p * 2),
+        ("pred_b_ih", C.c_void_p * 2), ("pred_b_hh", C.c_void_p * 2),
+        ("joint_w1t", C.c_void_p), ("joint_w1p", C.c_void_p),
+        ("joint_bt", C.c_void_p), ("joint_bp", C.c_void_p),
+        ("joint_w2", C.c_void_p), ("joint_b2", C.c_void_p),
+    ]
+
+
+class RnntOpts(C.Structure):
+    _fields_ = [("max_batch", C.c_int), ("max_frames", C.c_int), ("max_res", C.c_int)]
+
+
+_SIGS = {
+    "rnnt_abi_version": (C.c_int, []),
+    "rnnt_last_error": (C.c_char_p, []),
+    "rnnt_engine_create": (C.c_int, [C.POINTER(RnntModelDesc), C.c_int, C.POINTER(RnntOpts), C.POINTER(C.c_void_p)]),
+    "rnnt_engine_destroy": (None, [C.c_void_p]),
+    "rnnt_engine_encode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                     C.c_void_p, C.c_void_p]),
+    "rnnt_engine_decode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "rnnt_engine_infer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                    C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "rnnt_op_lstm_int8": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rnnt_op_stack_time": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                     C.c_void_p]),
+}
+
+_lib = None
+
+
+def build():
+    """Compile the HIP engine in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", CSRC], check=True)
+
+
+def header_functions(path=HEADER):
+    """Function names declared in include/rnnt_mi355x.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rnnt_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP engine library missing: {LIB_PATH} (build it with `make -C {CSRC}`); "
+                           "rnnt_amd has no CPU fallback")
+    import torch  # noqa: F401  -- share torch's HIP runtime (same SONAME) before loading ours
+    _lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(_lib, name)
+        f.restype = res
+        f.argtypes = args
+    return _lib
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != RNNT_OK:
+        msg = lib().rnnt_last_error()
+        raise EngineError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

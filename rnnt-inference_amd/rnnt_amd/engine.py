@@ -1,0 +1,126 @@
+"""Engine: the per-GPU RNN-T worker object over the C ABI.
+
+One ``Engine`` per GPU replaces the reference's per-socket ``TorchModel`` clones
+(csrc/rnnt_model.hpp:39-137): ``encode``/``decode`` are TorchModel::encode / decode, with the
+same result contract (res [N][max_res] int32 filled with SOS=-1, res_len = res_idx+1).
+Device memory and streams come from PyTorch (plumbing only); all compute is in the HIP
+library.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .config import RNNTParam as R
+from .weights import PreparedModel, f32_to_bf16_bits
+
+BATCH_TILE = 128
+
+
+def pad_batch(n):
+    return (n + BATCH_TILE - 1) // BATCH_TILE * BATCH_TILE
+
+
+def _stream_handle(stream):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Engine:
+    def __init__(self, pm: PreparedModel, device=0, max_batch=1024, max_frames=R.MAX_FEA_LEN, max_res=None):
+        if not pm.bf16:
+            raise ValueError("the engine runs the int8 encoder + bf16 prediction/joint path (enable_bf16)")
+        lib = _lib.lib()
+        self.device = device
+        self.max_frames = max_frames
+        self.max_res = max_res or (max_frames // 2) * R.max_symbols_per_step
+        self.max_batch = pad_batch(max_batch)
+        keep = []
+
+        def arr(a, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a.ctypes.data
+
+        def bf(a):
+            return arr(f32_to_bf16_bits(np.asarray(a, np.float32)), np.uint16)
+
+        d = _lib.RnntModelDesc()
+        for l in range(5):
+            d.enc_w[l] = arr(pm.enc_w[l], np.int8)
+            d.enc_bq[l] = arr(pm.enc_bq[l], np.float32)
+            d.enc_rb[l] = float(pm.enc_rb[l])
+            d.enc_in_s[l] = float(pm.enc_in_s[l])
+            d.enc_out_s[l] = float(pm.enc_out_s[l])
+        d.embed = bf(pm.embed)
+        for l in range(2):
+            d.pred_w_ih[l] = bf(pm.pred_wih[l])
+            d.pred_w_hh[l] = bf(pm.pred_whh[l])
+            d.pred_b_ih[l] = arr(pm.pred_bih[l], np.float32)
+            d.pred_b_hh[l] = arr(pm.pred_bhh[l], np.float32)
+        d.joint_w1t = bf(pm.w1t)
+        d.joint_w1p = bf(pm.w1p)
+        d.joint_bt = arr(pm.bt, np.float32)
+        d.joint_bp = arr(pm.bp, np.float32)
+        d.joint_w2 = bf(pm.w2)
+        d.joint_b2 = arr(pm.b2, np.float32)
+        opts = _lib.RnntOpts(self.max_batch, max_frames, self.max_res)
+        h = C.c_void_p()
+        _lib.check(lib.rnnt_engine_create(C.byref(d), device, C.byref(opts), C.byref(h)), "rnnt_engine_create")
+        self._h = h
+        self._lib = lib
+
+    # ---------------------------------------------------------------- batch API
+    def encode(self, feats, lens, lens_host=None, n=None, f_out=None, stream=None):
+        """feats: cuda fp32 [T, n_pad, 256]; lens: cuda int32 [n_pad]; lens_host: numpy [n]."""
+        T, n_pad, ch = feats.shape
+        assert ch == R.PADDED_INPUT_SIZE and feats.is_contiguous() and lens.is_contiguous()
+        n = n if n is not None else (len(lens_host) if lens_host is not None else n_pad)
+        lh = None
+        if lens_host is not None:
+            lh = np.ascontiguousarray(lens_host, np.int32)
+        rc = self._lib.rnnt_engine_encode(self._h, _ptr(feats), _ptr(lens), lh.ctypes.data if lh is not None else None,
+                                          T, n, n_pad, _ptr(f_out), _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_encode")
+
+    def decode(self, res, res_len, stream=None):
+        """res: cuda int32 [n, max_res]; res_len: cuda int32 [n]."""
+        rc = self._lib.rnnt_engine_decode(self._h, _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_decode")
+
+    def infer(self, feats, lens, lens_host, res, res_len, n=None, stream=None):
+        T, n_pad, _ = feats.shape
+        n = n if n is not None else len(lens_host)
+        lh = np.ascontiguousarray(lens_host, np.int32)
+        rc = self._lib.rnnt_engine_infer(self._h, _ptr(feats), _ptr(lens), lh.ctypes.data, T, n, n_pad,
+                                         _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_infer")
+
+    # ---------------------------------------------------------------- op-level API
+    def lstm_int8(self, first, count, x, hx, cx, y, stream=None):
+        T, n_pad = x.shape[0], x.shape[1]
+        rc = self._lib.rnnt_op_lstm_int8(self._h, first, count, _ptr(x), T, n_pad, _ptr(hx), _ptr(cx), _ptr(y),
+                                         _stream_handle(stream))
+        _lib.check(rc, "rnnt_op_lstm_int8")
+
+    def stack_time(self, x, x_lens, y, stream=None):
+        T, n_pad, Cc = x.shape
+        rc = self._lib.rnnt_op_stack_time(self._h, _ptr(x), _ptr(x_lens), T, n_pad, Cc, _ptr(y), _stream_handle(stream))
+        _lib.check(rc, "rnnt_op_stack_time")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rnnt_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
