@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""MLPerf-Offline-style throughput of the MI355X RNN-T engine (utterances/s).
+
+Workload (BASELINE.json metric / config 4): an Offline query over a LibriSpeech-dev-clean-
+shaped QSL of 2513 synthetic utterances PER GPU (weak scaling: one process per GPU, each
+with its own shard, no data-path collective), sorted longest-first and run in batches of
+--batch through the int8 encoder + bf16 prediction/joint + device-side greedy decode.  One
+step = one pass over the rank's shard, features already resident in HBM; the host gather of
+each utterance's int32 tokens (QuerySamplesComplete payload) is inside the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "rnnt-inference_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rnnt_amd import synthetic, weights  # noqa: E402
+from rnnt_amd.config import encoder_frames, encoder_ops  # noqa: E402
+from rnnt_amd.engine import Engine, pad_batch  # noqa: E402
+
+METRIC = "MLPerf Offline utterances/sec at 1/2/4/8 MI355X; WER vs fp32 ref"
+INT8_DENSE_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 MFMA = 2x the ~2.5 PF dense bf16 rate
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--qsl", type=int, default=2513, help="utterances per GPU (mlperf.conf:13)")
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--cpu-sample", type=int, default=24, help="utterances timed on the CPU restatement")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                    help="per-launch HBM bytes from a rocprofv3 --pmc pass (profiles/), if present")
+    return ap.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return rank, local, world
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def all_max(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_batches(lens, batch, seed):
+    """Sorted (longest first, rnnt_qsl.cpp:104-133) batches, features staged in HBM."""
+    order = np.argsort(-lens, kind="stable")
+    out = []
+    for b, i in enumerate(range(0, len(order), batch)):
+        idx = order[i:i + batch]
+        bl = lens[idx].astype(np.int32)
+        n = len(idx)
+        n_pad = pad_batch(n)
+        lp = np.zeros(n_pad, np.int32)
+        lp[:n] = bl
+        T = int(bl.max())
+        x = synthetic.make_features(T, n_pad, seed=seed * 7919 + b, lens=lp)
+        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, lens=torch.from_numpy(lp).cuda(),
+                        x=torch.from_numpy(x).cuda(), x_host=x))
+    return out
+
+
+def run_step(engine, batches):
+    outs = []
+    for b in batches:
+        res = torch.empty((b["n"], engine.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(b["n"], dtype=torch.int32, device="cuda")
+        engine.infer(b["x"], b["lens"], b["lens_host"], res, rl, n=b["n"])
+        outs.append((res, rl))
+    # host gather of the responses: lengths, then each batch's used token columns
+    lens = [rl.to("cpu", non_blocking=True) for _, rl in outs]
+    torch.cuda.synchronize()
+    toks = [res[:, : max(1, int(l.max()))].cpu() for (res, _), l in zip(outs, lens)]
+    return lens, toks
+
+
+def cpu_baseline(pm, lens, n_sample, seed):
+    """The C restatement (oracle/, TEST INFRASTRUCTURE) timed on this host's cores on a bounded
+    sample of the same workload; also returns its tokens for a parity spot-check."""
+    from oracle import oracle
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(len(lens), size=min(n_sample, len(lens)), replace=False)
+    sl = np.sort(lens[idx])[::-1].astype(np.int32)
+    n_pad = pad_batch(len(sl))
+    lp = np.zeros(n_pad, np.int32)
+    lp[: len(sl)] = sl
+    x = synthetic.make_features(int(sl.max()), n_pad, seed=seed + 17, lens=lp)
+    oracle.lib()
+    t0 = time.perf_counter()
+    f = oracle.encoder_i8(pm, x[:, : len(sl)], sl)
+    res, rl, _ = oracle.greedy_decode(pm, f, (sl + 1) // 2, max_res=(500 // 2) * 30)
+    dt = time.perf_counter() - t0
+    return dict(value=len(sl) / dt, seconds=dt, x=x, lens=lp, n=len(sl), sl=sl, res=res, rl=rl,
+                cores=oracle.lib().oracle_num_threads(), frames=int(sl.sum()))
+
+
+def main():
+    args = parse()
+    rank, local, world = dist_setup()
+    pm, _ = weights.build_model()
+    lens = synthetic.devclean_lengths(args.qsl, seed=4 + 1000 * rank)
+    engine = Engine(pm, device=local, max_batch=args.batch, max_frames=500)
+    batches = make_batches(lens, args.batch, seed=4 + 1000 * rank)
+
+    for _ in range(args.warmup):
+        run_step(engine, batches)
+    torch.cuda.synchronize()
+    barrier(world)
+    engine.set_profiling(True)
+    engine.stats(reset=True)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lens_out, _ = run_step(engine, batches)
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    st = engine.stats(reset=True)
+    elapsed_max = all_max(elapsed, world)
+
+    utts = args.qsl * world * args.steps
+    value = utts / elapsed_max
+    emitted = int(sum(int(l.sum()) for l in lens_out))
+    enc_frames = int(sum(encoder_frames(l) for l in lens))
+    enc_ops = float(sum(encoder_ops(int(l)) for l in lens)) * args.steps  # SURVEY 8d E(T), valid frames
+    achieved = enc_ops / (st["encode_ms"] * 1e-3) / 1e12 if st["encode_ms"] > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("lstm_i8_step_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {
+        "bound": "mfma", "kernel": "lstm_i8_step_kernel (int8 encoder, all 5 layers)",
+        "achieved": round(achieved, 2), "peak": INT8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / INT8_DENSE_PEAK_TOPS, 4), "traffic": traffic,
+        "encode_ms_per_step": round(st["encode_ms"] / args.steps, 3),
+        "joint_trans_ms_per_step": round(st["joint_trans_ms"] / args.steps, 3),
+        "greedy_ms_per_step": round(st["greedy_ms"] / args.steps, 3),
+        "step_launches_per_step": int(st["step_launches"] // max(1, args.steps)),
+    }
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "utterances/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
+        "data": "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)",
+        "config": {"workload": "MLPerf Offline, LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
+                   "qsl_per_gpu": args.qsl, "batch_size": args.batch, "encoder": "int8 (lstm_amx_int8)",
+                   "decoder": "bf16 prediction/joint, fp32 accumulate, greedy (device loop)",
+                   "parallelism": f"dp{world} (one process per GPU, sharded queries)",
+                   "encoder_frames_per_gpu": enc_frames, "emitted_symbols_per_gpu": emitted // args.steps},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(pm, lens, args.cpu_sample, seed=99)
+        # parity spot-check of the same sample on the GPU
+        res = torch.empty((cb["n"], engine.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(cb["n"], dtype=torch.int32, device="cuda")
+        engine.infer(torch.from_numpy(cb["x"]).cuda(), torch.from_numpy(cb["lens"]).cuda(), cb["sl"], res, rl, n=cb["n"])
+        torch.cuda.synchronize()
+        same = bool(np.array_equal(rl.cpu().numpy(), cb["rl"]) and
+                    np.array_equal(res.cpu().numpy()[:, : cb["res"].shape[1]], cb["res"]))
+        out["cpu_baseline"] = {"value": round(cb["value"], 3), "unit": "utterances/s", "cores": cb["cores"],
+                               "kind": "port",
+                               "sample": f"{cb['n']} utterances ({cb['frames']} frames) drawn from the same QSL, "
+                                         f"int8 encoder + greedy decode, {cb['seconds']:.1f} s"}
+        out["parity_spot_check"] = {"utterances": cb["n"], "tokens_identical": same}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    engine.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

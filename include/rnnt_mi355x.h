@@ -91,6 +91,19 @@ int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
 int rnnt_engine_infer(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host, int T,
                       int n, int n_pad, int32_t* res, int32_t* res_len, int max_res, void* stream);
 
+/* ---- in-run measurement (bench.py's roofline leg): HIP events recorded on the launch stream
+ * around each call's encoder kernels and decoder kernels; rnnt_engine_get_stats synchronises
+ * on the recorded events and sums their elapsed times. */
+typedef struct {
+  double encode_ms;       /* first to last encoder kernel of each encode call (step kernels + gaps) */
+  double joint_trans_ms;  /* the F = b_t + f.W1t^T GEMM */
+  double greedy_ms;       /* the device-side greedy decode loop */
+  int64_t step_launches;  /* lstm step kernels launched */
+  int64_t encode_calls, decode_calls;
+} rnnt_stats;
+int rnnt_engine_set_profiling(rnnt_engine* e, int on);
+int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset);
+
 /* ---- operator-level entry points (torch.ops.intel_mlperf mirror, rnnt_amd/ops.py) ---- */
 
 /* lstm_amx_int8 for the engine's encoder layers [first, first+count): x = layer `first` input

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -53,7 +54,18 @@ struct rnnt_engine {
   int32_t* flen = nullptr;
   // last encoded batch
   int last_T = 0, last_n = 0, last_npad = 0;
+  // profiling
+  bool prof = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_enc;
+  std::vector<std::array<hipEvent_t, 3>> ev_dec;
+  int64_t step_launches = 0, encode_calls = 0, decode_calls = 0;
 };
+
+static hipEvent_t new_event(hipStream_t st) {
+  hipEvent_t ev = nullptr;
+  if (hipEventCreate(&ev) == hipSuccess) (void)hipEventRecord(ev, st);
+  return ev;
+}
 
 template <class T>
 static int dev_alloc(rnnt_engine* e, T** p, size_t count) {
@@ -258,6 +270,7 @@ static int run_layer(rnnt_engine* e, int l, int T, int n_pad, const int8_t* x, i
     }
     const int nt = tile_max.empty() ? n_pad / ENC_BATCH_TILE : active_tiles(tile_max, thr);
     if (launch_lstm_i8_step(a, nt, st)) return fail(RNNT_EDEVICE, "lstm step launch failed");
+    e->step_launches += nt > 0;
   }
   return 0;
 }
@@ -290,6 +303,7 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
     HIPCHK(hipMemsetAsync(e->h[l][0], 0, (size_t)n_pad * H, st));
     HIPCHK(hipMemsetAsync(e->c[l], 0, (size_t)n_pad * H * 2, st));
   }
+  hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
   if (launch_quantize(feats, (int64_t)T * n_pad * FEAT, e->in_s[0], e->x0q, st))
     return fail(RNNT_EDEVICE, "quantize launch failed");
   if ((r = run_layer(e, 0, T, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, tm, lens, st))) return r;
@@ -297,6 +311,8 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
   if ((r = run_layer(e, 2, Tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, tm, lens, st))) return r;
   if ((r = run_layer(e, 3, Tp, n_pad, e->yB, ENC_OUT_I8, e->yA, nullptr, tm, lens, st))) return r;
   if ((r = run_layer(e, 4, Tp, n_pad, e->yA, ENC_OUT_FINAL, e->fperm, f_out, tm, lens, st))) return r;
+  if (e->prof) e->ev_enc.push_back({ev0, new_event(st)});
+  e->encode_calls++;
   hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->flen, n_pad);
   HIPCHK(hipGetLastError());
   e->last_T = T;
@@ -312,8 +328,10 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   HIPCHK(hipSetDevice(e->device));
   hipStream_t st = pick(e, stream);
   const int Tp = (e->last_T + 1) / 2;
+  hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
   if (launch_joint_trans(e->dw, e->fperm, e->flen, e->F, Tp, e->last_npad, st))
     return fail(RNNT_EDEVICE, "joint_trans launch failed");
+  hipEvent_t ev1 = e->prof ? new_event(st) : nullptr;
   DecArgs a{};
   a.w = e->dw;
   a.F = e->F;
@@ -327,6 +345,45 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   a.max_res = max_res;
   a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
   if (launch_greedy_decode(a, st)) return fail(RNNT_EDEVICE, "greedy launch failed");
+  if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
+  e->decode_calls++;
+  return 0;
+}
+
+extern "C" int rnnt_engine_set_profiling(rnnt_engine* e, int on) {
+  if (!e) return fail(RNNT_EINVAL, "null engine");
+  e->prof = on != 0;
+  return 0;
+}
+
+extern "C" int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset) {
+  if (!e || !out) return fail(RNNT_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(e->device));
+  memset(out, 0, sizeof(*out));
+  for (auto& p : e->ev_enc) {
+    float ms = 0;
+    HIPCHK(hipEventSynchronize(p.second));
+    HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
+    out->encode_ms += ms;
+  }
+  for (auto& p : e->ev_dec) {
+    float a = 0, b = 0;
+    HIPCHK(hipEventSynchronize(p[2]));
+    HIPCHK(hipEventElapsedTime(&a, p[0], p[1]));
+    HIPCHK(hipEventElapsedTime(&b, p[1], p[2]));
+    out->joint_trans_ms += a;
+    out->greedy_ms += b;
+  }
+  out->step_launches = e->step_launches;
+  out->encode_calls = e->encode_calls;
+  out->decode_calls = e->decode_calls;
+  if (reset) {
+    for (auto& p : e->ev_enc) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+    for (auto& p : e->ev_dec) for (auto ev : p) (void)hipEventDestroy(ev);
+    e->ev_enc.clear();
+    e->ev_dec.clear();
+    e->step_launches = e->encode_calls = e->decode_calls = 0;
+  }
   return 0;
 }
 

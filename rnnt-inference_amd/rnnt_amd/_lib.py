@@ -33,7 +33,14 @@ class RnntOpts(C.Structure):
     _fields_ = [("max_batch", C.c_int), ("max_frames", C.c_int), ("max_res", C.c_int)]
 
 
+class RnntStats(C.Structure):
+    _fields_ = [("encode_ms", C.c_double), ("joint_trans_ms", C.c_double), ("greedy_ms", C.c_double),
+                ("step_launches", C.c_int64), ("encode_calls", C.c_int64), ("decode_calls", C.c_int64)]
+
+
 _SIGS = {
+    "rnnt_engine_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "rnnt_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(RnntStats), C.c_int]),
     "rnnt_abi_version": (C.c_int, []),
     "rnnt_last_error": (C.c_char_p, []),
     "rnnt_engine_create": (C.c_int, [C.POINTER(RnntModelDesc), C.c_int, C.POINTER(RnntOpts), C.POINTER(C.c_void_p)]),
@@ -71,7 +78,10 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"HIP engine library missing: {LIB_PATH} (build it with `make -C {CSRC}`); "
                            "rnnt_amd has no CPU fallback")
-    import torch  # noqa: F401  -- share torch's HIP runtime (same SONAME) before loading ours
+    # torch ships its own libamdhip64.so.7; importing it first makes our NEEDED entry resolve to
+    # the already-loaded runtime (same SONAME), so device pointers and streams are shared.  Loading
+    # ours first would bring up a second HIP runtime that then sees no device.
+    import torch  # noqa: F401
     _lib = C.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
         f = getattr(_lib, name)

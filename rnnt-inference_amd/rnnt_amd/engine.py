@@ -102,6 +102,15 @@ class Engine:
                                          _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))
         _lib.check(rc, "rnnt_engine_infer")
 
+    # ---------------------------------------------------------------- measurement
+    def set_profiling(self, on=True):
+        _lib.check(self._lib.rnnt_engine_set_profiling(self._h, int(bool(on))), "rnnt_engine_set_profiling")
+
+    def stats(self, reset=True):
+        st = _lib.RnntStats()
+        _lib.check(self._lib.rnnt_engine_get_stats(self._h, C.byref(st), int(bool(reset))), "rnnt_engine_get_stats")
+        return {k: getattr(st, k) for k, _ in st._fields_}
+
     # ---------------------------------------------------------------- op-level API
     def lstm_int8(self, first, count, x, hx, cx, y, stream=None):
         T, n_pad = x.shape[0], x.shape[1]

@@ -1,0 +1,110 @@
+"""Query Sample Library and Offline SUT over the HIP engine.
+
+Mirrors the reference's LoadGen-facing surface (the real MLPerf LoadGen is not installable
+offline, so the query / response types are plain Python):
+  * ``RNNTQSL``   csrc/rnnt_qsl.{hpp,cpp} / models/rnnt_qsl.py: holds per-sample features
+                  [T_i, 240] and lengths; ``sort`` is the length-descending bucket sort
+                  (rnnt_qsl.cpp:104-133); ``assemble`` pads a batch to [T_max, n_pad, 256]
+                  (AssembleSamples, rnnt_qsl.cpp:150-188).
+  * ``OfflineSUT`` csrc/torch_sut.cpp:88-236 / models/pytorch_sut.py:58-118: issue_queries
+                  sorts, takes <= batch_size samples per batch, runs encode+decode on its GPU
+                  and completes each sample with its int32 token row (res_len*4 bytes,
+                  QuerySamplesComplete, torch_sut.cpp:221-236).
+Multi-GPU: one process per GPU, each with its own engine; a query's sorted samples are dealt
+to ranks in batch-sized chunks (round-robin, so every rank gets the same length mix).  There
+is no data-path collective: results are completed per rank.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+from .config import RNNTParam as R
+from .engine import pad_batch
+
+
+@dataclass
+class QuerySample:
+    id: int
+    index: int
+
+
+class RNNTQSL:
+    def __init__(self, features, lengths):
+        """features: list of [T_i, 240] float32 arrays (or None for synthetic on-demand);
+        lengths: int array [count]."""
+        self.lengths = np.asarray(lengths, np.int32)
+        self.features = features
+        self.count = len(self.lengths)
+
+    @classmethod
+    def synthetic(cls, lengths, seed):
+        rng = np.random.default_rng(seed)
+        feats = [rng.standard_normal((int(l), R.trans_input_size), dtype=np.float32) for l in lengths]
+        return cls(feats, lengths)
+
+    def __len__(self):
+        return self.count
+
+    def sort(self, samples, reverse=True):
+        """Bucket sort by feature length, longest first (rnnt_qsl.cpp:104-133)."""
+        lmin, lmax = int(self.lengths.min()), int(self.lengths.max())
+        buckets = [[] for _ in range(lmax - lmin + 1)]
+        for s in samples:
+            L = int(self.lengths[s.index])
+            buckets[(lmax - L) if reverse else (L - lmin)].append(s)
+        return [s for b in buckets for s in b]
+
+    def assemble(self, indices, n_pad=None):
+        """-> (x [T_max, n_pad, 256] f32, lens [n_pad] int32), zero padded (rnnt_qsl.cpp:150-188)."""
+        n = len(indices)
+        n_pad = n_pad or pad_batch(n)
+        lens = np.zeros(n_pad, np.int32)
+        lens[:n] = self.lengths[list(indices)]
+        T = int(lens.max())
+        x = np.zeros((T, n_pad, R.PADDED_INPUT_SIZE), np.float32)
+        for i, idx in enumerate(indices):
+            f = self.features[idx]
+            x[: f.shape[0], i, : R.trans_input_size] = f
+        return x, lens
+
+
+def deal_batches(sorted_samples, batch_size, rank=0, world=1):
+    """Split a sorted query into batch_size chunks and deal them round-robin to ranks."""
+    chunks = [sorted_samples[i:i + batch_size] for i in range(0, len(sorted_samples), batch_size)]
+    return chunks[rank::world]
+
+
+class OfflineSUT:
+    def __init__(self, engine, qsl, batch_size=1024, rank=0, world=1, on_complete=None):
+        self.engine, self.qsl, self.batch_size = engine, qsl, batch_size
+        self.rank, self.world = rank, world
+        self.on_complete = on_complete
+        self.responses = {}
+
+    def issue_queries(self, samples):
+        import torch
+        batches = deal_batches(self.qsl.sort(samples), self.batch_size, self.rank, self.world)
+        pending = []
+        for batch in batches:
+            x, lens = self.qsl.assemble([s.index for s in batch])
+            n = len(batch)
+            res = torch.empty((n, self.engine.max_res), dtype=torch.int32, device="cuda")
+            rl = torch.empty(n, dtype=torch.int32, device="cuda")
+            self.engine.infer(torch.from_numpy(x).cuda(), torch.from_numpy(lens).cuda(), lens[:n], res, rl, n=n)
+            pending.append((batch, res, rl))
+        for batch, res, rl in pending:
+            self.query_samples_complete(batch, res, rl)
+
+    def query_samples_complete(self, batch, res, res_len):
+        """Response = int32 tokens [res_len] per sample (torch_sut.cpp:221-236)."""
+        rl = res_len.cpu().numpy()
+        width = int(rl.max()) if len(rl) else 0
+        toks = res[:, :max(width, 1)].cpu().numpy()
+        for i, s in enumerate(batch):
+            row = toks[i, : rl[i]].copy()
+            self.responses[s.id] = row
+            if self.on_complete:
+                self.on_complete(s, row)
+
+    def flush_queries(self):
+        pass

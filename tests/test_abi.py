@@ -1,6 +1,5 @@
 """CPU-side checks of the drop-in boundary: the C-ABI library builds, loads, and exports every
 symbol include/rnnt_mi355x.h declares (no compute calls: there is no GPU here)."""
-import ctypes
 import os
 
 import pytest
@@ -15,7 +14,7 @@ def test_library_built_in_tree():
 def test_exports_every_header_symbol():
     names = _lib.header_functions()
     assert "rnnt_engine_create" in names and "rnnt_op_lstm_int8" in names
-    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib = _lib.lib()
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert set(_lib._SIGS) == set(names), "python binding out of sync with the header"
