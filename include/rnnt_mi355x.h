@@ -15,7 +15,7 @@
  *     rnnt_amd/ops.py.
  *
  * Plain pointers and sizes only.  Device pointers are HIP device allocations on the engine's
- * device; `stream` is a hipStream_t (NULL = the engine's own stream).  Every entry point
+ * device; `stream` is a hipStream_t used as given (0 = the null stream).  Every entry point
  * returns 0 on success or a negative errno-style code; rnnt_last_error() describes the last
  * failure on the calling thread.  One engine per GPU, driven by one host thread at a time;
  * distinct engines are independent (the reference's per-socket model clones, rnnt_model.hpp:45-46).

@@ -7,10 +7,11 @@
 // bit-identical to a sequential fmaf chain), so the decode is bit-exact with the CPU
 // restatement and therefore token-identical.
 //
-// The whole greedy loop runs on the device: one workgroup owns DEC_ROWS utterances and
-// iterates emit/advance steps until all of them finish -- no host round trip per step, no
-// inter-workgroup synchronisation (rows never interact, decoder.py:125-167).  Two
-// algebraic shortcuts, both exact:
+// The greedy loop runs lock-step over the batch like the reference's (rnnt_model.hpp:92-124):
+// per step, weight-stationary kernels run the prediction network for the rows that emitted,
+// then one kernel does joint + argmax + greedy_decode_update for every live row; the host
+// only enqueues steps and polls a live-row counter one 32-step chunk behind (no per-step
+// round trip).  Two algebraic shortcuts, both exact:
 //   * the joint's encoder half F[t] = b_t + bf16(f_t).W1t^T depends only on the frame, so it is
 //     one batched GEMM over all frames before the loop (launch_joint_trans);
 //   * prediction(pre_g, pre_hg, pre_cg) depends only on state that changes on an emit, so it
@@ -76,208 +77,291 @@ __global__ void __launch_bounds__(256) joint_trans_kernel(DecWeights w, const ui
 }
 
 // ---------------------------------------------------------------- greedy decode
+// Lock-step over the batch, like the reference's loop (rnnt_model.hpp:92-124), but only the
+// rows that emitted at the previous step re-run the prediction network:
+//   pred(layer 0) -> pred(layer 1) -> G  for the listed rows      (weight-stationary grids)
+//   joint + argmax + greedy update for every unfinished row -> next step's emit list
 constexpr int XP = 640 + 4;  // LDS row pitch (floats) of staged B operands: conflict-free b128 reads
-constexpr int HP = 320 + 4;
+constexpr int GP = 320 + 4;
+constexpr int YP = 512 + 4;
 
-struct DecSmem {
-  float X[DEC_ROWS][XP];   // layer input [x | h_prev] (chain-permuted); y1 for the joint
-  float Hs[DEC_ROWS][HP];  // layer output h (chain-permuted): next layer's x / the joint's g
-  float L[DEC_ROWS][NLAB_PAD + 1];
-  int time[DEC_ROWS], added[DEC_ROWS], idx[DEC_ROWS], preg[DEC_ROWS], slot[DEC_ROWS];
-  int fin[DEC_ROWS], need[DEC_ROWS], flen[DEC_ROWS], list[DEC_ROWS];
-  int nlist, all_done;
-};
-
-// hc row layout: [slot][4][320] with parts 0:h0 1:h1 2:c0 3:c1
 __device__ __forceinline__ float* hc_part(float* hc, int row, int slot, int part) {
-  return hc + ((size_t)row * 2 + slot) * 4 * P + part * P;
+  return hc + ((size_t)row * 2 + slot) * 4 * P + part * P;  // parts 0:h0 1:h1 2:c0 3:c1
+}
+
+__global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= a.Npad) return;
+  const int fl = row < a.N ? a.f_lens[row] : 0;
+  DecState& s = a.s;
+  s.time[row] = 0; s.added[row] = 0; s.idx[row] = -1; s.preg[row] = SOS; s.slot[row] = 0;
+  s.fin[row] = fl <= 0;
+  float* h = hc_part(a.hc, row, 0, 0);
+  for (int k = 0; k < 4 * P; ++k) h[k] = 0.0f;  // committed state starts at zero (metadata.cpp:25-30)
+  if (fl > 0) {
+    s.list[atomicAdd(&s.count[0], 1)] = row;  // every live row needs its first (SOS) prediction
+    atomicAdd(s.unfinished, 1);
+  }
 }
 
 // One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates = (b_ih+b_hh) +
-// chain over [x | h_prev] of the gate-interleaved weights; c fp32, h bf16.
-__device__ void pred_layer(const DecArgs& a, DecSmem& s, int layer, int r0) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+// chain over [x | h_prev]; c fp32, h bf16.  Grid: x = 8-gate-tile group (128 gate rows),
+// y = 16-row tile of the emit list.
+__global__ void __launch_bounds__(256) dec_pred_kernel(DecArgs a, int layer, int parity) {
+  __shared__ __attribute__((aligned(16))) float X[16][XP];
+  __shared__ int rows[16], slots[16], pregs[16];
+  const DecState& s = a.s;
+  const int cnt = s.count[parity];
+  const int rt = blockIdx.y;
+  if (rt * 16 >= cnt) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  const int* list = s.list + parity * a.Npad;
+  if (tid < 16) {
+    const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
+    rows[tid] = row;
+    slots[tid] = row >= 0 ? s.slot[row] : 0;
+    pregs[tid] = row >= 0 ? s.preg[row] : SOS;
+  }
+  __syncthreads();
+  // stage [x | h_prev] for the 16 listed rows: 16 x 160 float4 groups, 10 per thread
+  for (int i = tid; i < 16 * 160; i += 256) {
+    const int mi = i / 160, k = (i % 160) * 4, row = rows[mi];
+    float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (row >= 0) {
+      const int sl = slots[mi];
+      if (layer == 0) {
+        if (k < P) {
+          const int g = pregs[mi];
+          if (g != SOS) {  // SOS -> zero embedding (modeling_rnnt.py:195-200)
+            const uint2 e2 = *(const uint2*)(a.w.embed + g * P + k);
+            v = float4{bits2f(e2.x << 16), bits2f(e2.x & 0xffff0000u), bits2f(e2.y << 16), bits2f(e2.y & 0xffff0000u)};
+          }
+        } else {
+          v = *(const float4*)(hc_part(a.hc, row, sl, 0) + k - P);
+        }
+      } else {
+        v = (k < P) ? *(const float4*)(hc_part(a.hc, row, sl ^ 1, 0) + k) : *(const float4*)(hc_part(a.hc, row, sl, 1) + k - P);
+      }
+    }
+    X[mi][chain_pos(k)] = v.x;
+    X[mi][chain_pos(k + 1)] = v.y;
+    X[mi][chain_pos(k + 2)] = v.z;
+    X[mi][chain_pos(k + 3)] = v.w;
+  }
+  __syncthreads();
   const uint16_t* W = a.w.wp[layer];
   const float* bias = a.w.bp_lstm[layer];
-  const float* xrow = &s.X[c][8 * q];
-  const int nl = s.nlist;
-  for (int gt = wave * 2; gt < PG4 / 16; gt += 8) {  // two gate tiles (independent chains) per pass
-    v4f acc0, acc1;
-    {
-      const float4 b0 = *(const float4*)(bias + gt * 16 + 4 * q);
-      const float4 b1 = *(const float4*)(bias + (gt + 1) * 16 + 4 * q);
-      acc0 = v4f{b0.x, b0.y, b0.z, b0.w};
-      acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
+  const int gt = blockIdx.x * 8 + wave * 2;
+  v4f acc0, acc1;
+  {
+    const float4 b0 = *(const float4*)(bias + gt * 16 + 4 * q);
+    const float4 b1 = *(const float4*)(bias + (gt + 1) * 16 + 4 * q);
+    acc0 = v4f{b0.x, b0.y, b0.z, b0.w};
+    acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
+  }
+  const uint16_t* w0 = W + (size_t)(gt * 16 + c) * 640 + 8 * q;
+  const uint16_t* w1 = w0 + 16 * 640;
+  const float* xrow = &X[c][8 * q];
+  uint4 wa = *(const uint4*)w0, wb = *(const uint4*)w1;
+#pragma unroll 4
+  for (int b = 0; b < 640 / 32; ++b) {
+    uint4 na = wa, nb = wb;
+    if (b + 1 < 640 / 32) {
+      na = *(const uint4*)(w0 + 32 * (b + 1));
+      nb = *(const uint4*)(w1 + 32 * (b + 1));
     }
-    const uint16_t* w0 = W + (size_t)(gt * 16 + c) * 640 + 8 * q;
-    const uint16_t* w1 = w0 + 16 * 640;
-    for (int b = 0; b < 640 / 32; ++b) {
-      const uint4 wa = *(const uint4*)(w0 + 32 * b);
-      const uint4 wb = *(const uint4*)(w1 + 32 * b);
-      float x[8];
-      *(float4*)&x[0] = *(const float4*)(xrow + 32 * b);
-      *(float4*)&x[4] = *(const float4*)(xrow + 32 * b + 4);
-      acc0 = chain8(wa, x, acc0);
-      acc1 = chain8(wb, x, acc1);
-    }
-    // epilogue: lane (q, c) holds i,f,g,o of unit gt*4+q (and (gt+1)*4+q) for listed row c
-    if (c < nl) {
-      const int m = s.list[c], row = r0 + m, sl = s.slot[m];
+    float x[8];
+    *(float4*)&x[0] = *(const float4*)(xrow + 32 * b);
+    *(float4*)&x[4] = *(const float4*)(xrow + 32 * b + 4);
+    acc0 = chain8(wa, x, acc0);
+    acc1 = chain8(wb, x, acc1);
+    wa = na;
+    wb = nb;
+  }
+  const int row = rows[c];
+  if (row >= 0) {
+    const int sl = slots[c];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const v4f g = half ? acc1 : acc0;
-        const int u = (gt + half) * 4 + q;
-        const float ig = det_sigmoid(g[0]), fg = det_sigmoid(g[1]), gg = det_tanh(g[2]), og = det_sigmoid(g[3]);
-        const float cp = hc_part(a.hc, row, sl, 2 + layer)[u];
-        const float cn = fg * cp + ig * gg;
-        const float hh = bf_round(og * det_tanh(cn));
-        hc_part(a.hc, row, sl ^ 1, 2 + layer)[u] = cn;
-        hc_part(a.hc, row, sl ^ 1, layer)[u] = hh;
-        s.Hs[c][chain_pos(u)] = hh;
-      }
+    for (int half = 0; half < 2; ++half) {
+      const v4f g = half ? acc1 : acc0;
+      const int u = (gt + half) * 4 + q;
+      const float ig = det_sigmoid(g[0]), fg = det_sigmoid(g[1]), gg = det_tanh(g[2]), og = det_sigmoid(g[3]);
+      const float cp = hc_part(a.hc, row, sl, 2 + layer)[u];
+      const float cn = fg * cp + ig * gg;
+      const float hh = bf_round(og * det_tanh(cn));
+      hc_part(a.hc, row, sl ^ 1, 2 + layer)[u] = cn;
+      hc_part(a.hc, row, sl ^ 1, layer)[u] = hh;
     }
   }
 }
 
-__global__ void __launch_bounds__(256) greedy_decode_kernel(DecArgs a) {
-  __shared__ DecSmem s;
+// G = b_p + g . W1p^T for the listed rows' new candidates.  Grid: x = 128-column group,
+// y = 16-row tile.  Also clears the other parity's emit list for the joint that follows.
+__global__ void __launch_bounds__(256) dec_g_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) float X[16][GP];
+  __shared__ int rows[16], slots[16];
+  DecState& s = a.s;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) s.count[parity ^ 1] = 0;
+  const int cnt = s.count[parity];
+  const int rt = blockIdx.y;
+  if (rt * 16 >= cnt) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
-  const int r0 = blockIdx.x * DEC_ROWS;
-
-  if (tid < DEC_ROWS) {
-    const int row = r0 + tid;
-    const int fl = row < a.N ? a.f_lens[row] : 0;
-    s.flen[tid] = fl;
-    s.time[tid] = 0; s.added[tid] = 0; s.idx[tid] = -1; s.preg[tid] = SOS; s.slot[tid] = 0;
-    s.fin[tid] = (fl <= 0); s.need[tid] = 1;
-  }
-  // committed state (slot 0) starts at zero (decoder.py:67-78 / metadata.cpp:25-30)
-  for (int i = tid; i < DEC_ROWS * 4 * P; i += 256) {
-    const int m = i / (4 * P), k = i % (4 * P);
-    if (r0 + m < a.Npad) hc_part(a.hc, r0 + m, 0, 0)[k] = 0.0f;
-  }
-  for (int i = tid; i < DEC_ROWS * a.max_res; i += 256) {
-    const int m = i / a.max_res;
-    if (r0 + m < a.N) a.res[(size_t)(r0 + m) * a.max_res + i % a.max_res] = SOS;
+  const int* list = s.list + parity * a.Npad;
+  if (tid < 16) {
+    const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
+    rows[tid] = row;
+    slots[tid] = row >= 0 ? s.slot[row] : 0;
   }
   __syncthreads();
-
-  for (int iter = 0; iter < a.max_iter; ++iter) {
-    if (tid == 0) {
-      int nl = 0, done = 1;
-      for (int m = 0; m < DEC_ROWS; ++m) {
-        if (!s.fin[m]) {
-          done = 0;
-          if (s.need[m]) s.list[nl++] = m;
-        }
-      }
-      s.nlist = nl;
-      s.all_done = done;
-    }
-    __syncthreads();
-    if (s.all_done) break;
-
-    if (s.nlist > 0) {
-      // ---- prediction for rows whose committed state changed (Prediction.forward)
-      for (int i = tid; i < DEC_ROWS * 640; i += 256) {
-        const int mi = i / 640, k = i % 640;
-        float v = 0.0f;
-        if (mi < s.nlist) {
-          const int m = s.list[mi];
-          if (k < P) {
-            const int g = s.preg[m];
-            v = (g == SOS) ? 0.0f : bf2f(a.w.embed[g * P + k]);  // SOS -> zero embedding
-          } else {
-            v = hc_part(a.hc, r0 + m, s.slot[m], 0)[k - P];
-          }
-        }
-        s.X[mi][chain_pos(k)] = v;
-      }
-      __syncthreads();
-      pred_layer(a, s, 0, r0);
-      __syncthreads();
-      for (int i = tid; i < DEC_ROWS * 640; i += 256) {
-        const int mi = i / 640, k = i % 640;
-        float v = 0.0f;
-        if (mi < s.nlist) {
-          // chain_pos maps k<320 within the first 320 positions, so Hs copies straight over
-          v = (k < P) ? s.Hs[mi][k] : hc_part(a.hc, r0 + s.list[mi], s.slot[s.list[mi]], 1)[k - P];
-        }
-        s.X[mi][k < P ? k : chain_pos(k)] = v;
-      }
-      __syncthreads();
-      pred_layer(a, s, 1, r0);
-      __syncthreads();
-      // ---- G = b_p + g . W1p^T for the new candidates (joint prediction half)
-      for (int jt = wave; jt < J / 16; jt += 4) {
-        const float4 b0 = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
-        v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
-        const uint16_t* wr = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
-        const float* xr = &s.Hs[c][8 * q];
-        for (int b = 0; b < P / 32; ++b) {
-          float x[8];
-          *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
-          *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-          acc = chain8(*(const uint4*)(wr + 32 * b), x, acc);
-        }
-        if (c < s.nlist)
-          *(float4*)(a.G + (size_t)(r0 + s.list[c]) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
-      }
-      __syncthreads();
-      if (tid < s.nlist) s.need[s.list[tid]] = 0;
-    }
-
-    // ---- joint: y1 = bf16(relu(F[t] + G)), logits = b2 + y1 . W2^T
-    for (int i = tid; i < DEC_ROWS * J; i += 256) {
-      const int m = i / J, k = i % J, row = r0 + m;
-      float v = 0.0f;
-      if (!s.fin[m]) {
-        const float sum = a.F[((size_t)s.time[m] * a.Npad + row) * J + k] + a.G[(size_t)row * J + k];
-        v = bf_round(sum > 0.0f ? sum : 0.0f);
-      }
-      s.X[m][chain_pos(k)] = v;
-    }
-    __syncthreads();
-    if (wave < 2) {
-      const float4 b0 = *(const float4*)(a.w.b2 + wave * 16 + 4 * q);
-      v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
-      const uint16_t* wr = a.w.w2 + (size_t)(wave * 16 + c) * J + 8 * q;
-      const float* xr = &s.X[c][8 * q];
-      for (int b = 0; b < J / 32; ++b) {
-        float x[8];
-        *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
-        *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-        acc = chain8(*(const uint4*)(wr + 32 * b), x, acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s.L[c][wave * 16 + 4 * q + r] = acc[r];
-    }
-    __syncthreads();
-    // ---- greedy update (greedy_decode_update; decoder.py:137-167), one thread per row
-    if (tid < DEC_ROWS && !s.fin[tid]) {
-      const int m = tid;
-      int best = 0;
-      float bv = s.L[m][0];
-      for (int j = 1; j < NLAB; ++j)
-        if (s.L[m][j] > bv) { bv = s.L[m][j]; best = j; }  // torch.argmax: first maximum
-      if (best != BLANK && s.added[m] != MAXSYM) {
-        const int id = ++s.idx[m];
-        if (id < a.max_res) a.res[(size_t)(r0 + m) * a.max_res + id] = best;
-        s.added[m]++;
-        s.preg[m] = best;
-        s.slot[m] ^= 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
-        s.need[m] = 1;
-      } else {
-        int t = s.time[m] + 1;
-        if (t >= s.flen[m]) s.fin[m] = 1;
-        if (t > s.flen[m] - 1) t = s.flen[m] - 1;
-        s.time[m] = t;
-        s.added[m] = 0;
-      }
-    }
-    __syncthreads();
+  for (int i = tid; i < 16 * (P / 4); i += 256) {
+    const int mi = i / (P / 4), k = (i % (P / 4)) * 4, row = rows[mi];
+    const float4 v = row >= 0 ? *(const float4*)(hc_part(a.hc, row, slots[mi] ^ 1, 1) + k) : float4{0.0f, 0.0f, 0.0f, 0.0f};
+    X[mi][chain_pos(k)] = v.x;
+    X[mi][chain_pos(k + 1)] = v.y;
+    X[mi][chain_pos(k + 2)] = v.z;
+    X[mi][chain_pos(k + 3)] = v.w;
   }
-  if (tid < DEC_ROWS && r0 + tid < a.N) a.res_len[r0 + tid] = s.idx[tid] + 1;
+  __syncthreads();
+  const int jt = blockIdx.x * 8 + wave * 2;
+  v4f acc0, acc1;
+  {
+    const float4 b0 = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
+    const float4 b1 = *(const float4*)(a.w.bp + (jt + 1) * 16 + 4 * q);
+    acc0 = v4f{b0.x, b0.y, b0.z, b0.w};
+    acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
+  }
+  const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
+  const uint16_t* w1 = w0 + 16 * P;
+  const float* xr = &X[c][8 * q];
+#pragma unroll 2
+  for (int b = 0; b < P / 32; ++b) {
+    float x[8];
+    *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
+    *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
+    acc0 = chain8(*(const uint4*)(w0 + 32 * b), x, acc0);
+    acc1 = chain8(*(const uint4*)(w1 + 32 * b), x, acc1);
+  }
+  const int row = rows[c];
+  if (row >= 0) {
+    *(float4*)(a.G + (size_t)row * J + jt * 16 + 4 * q) = float4{acc0[0], acc0[1], acc0[2], acc0[3]};
+    *(float4*)(a.G + (size_t)row * J + (jt + 1) * 16 + 4 * q) = float4{acc1[0], acc1[1], acc1[2], acc1[3]};
+  }
+}
+
+// joint (y1 = bf16(relu(F[t] + G)), logits = b2 + y1.W2^T) + argmax + greedy_decode_update
+// (decoder.py:137-167) for 16 rows per workgroup; emitting rows go to the next emit list.
+__global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) float X[16][YP];
+  __shared__ float L[16][NLAB_PAD + 1];
+  __shared__ int live[16], tidx[16];
+  DecState& s = a.s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  const int r0 = blockIdx.x * 16;
+  if (tid < 16) {
+    const int row = r0 + tid;
+    const int lv = (row < a.N) && !s.fin[row];
+    live[tid] = lv;
+    tidx[tid] = lv ? s.time[row] : 0;
+  }
+  __syncthreads();
+  bool any = false;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) any |= live[m] != 0;
+  if (!any) return;
+  for (int i = tid; i < 16 * (J / 4); i += 256) {
+    const int m = i / (J / 4), k = (i % (J / 4)) * 4, row = r0 + m;
+    float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (live[m]) {
+      const float4 f4 = *(const float4*)(a.F + ((size_t)tidx[m] * a.Npad + row) * J + k);
+      const float4 g4 = *(const float4*)(a.G + (size_t)row * J + k);
+      const float s0 = f4.x + g4.x, s1 = f4.y + g4.y, s2 = f4.z + g4.z, s3 = f4.w + g4.w;
+      v = float4{bf_round(s0 > 0.0f ? s0 : 0.0f), bf_round(s1 > 0.0f ? s1 : 0.0f), bf_round(s2 > 0.0f ? s2 : 0.0f),
+                 bf_round(s3 > 0.0f ? s3 : 0.0f)};
+    }
+    X[m][chain_pos(k)] = v.x;
+    X[m][chain_pos(k + 1)] = v.y;
+    X[m][chain_pos(k + 2)] = v.z;
+    X[m][chain_pos(k + 3)] = v.w;
+  }
+  __syncthreads();
+  if (wave < 2) {
+    const float4 b0 = *(const float4*)(a.w.b2 + wave * 16 + 4 * q);
+    v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
+    const uint16_t* wr = a.w.w2 + (size_t)(wave * 16 + c) * J + 8 * q;
+    const float* xr = &X[c][8 * q];
+#pragma unroll 4
+    for (int b = 0; b < J / 32; ++b) {
+      float x[8];
+      *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
+      *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
+      acc = chain8(*(const uint4*)(wr + 32 * b), x, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) L[c][wave * 16 + 4 * q + r] = acc[r];
+  }
+  __syncthreads();
+  if (tid < 16 && live[tid]) {
+    const int m = tid, row = r0 + m;
+    int best = 0;
+    float bv = L[m][0];
+    for (int j = 1; j < NLAB; ++j)
+      if (L[m][j] > bv) { bv = L[m][j]; best = j; }  // torch.argmax: first maximum
+    if (best != BLANK && s.added[row] != MAXSYM) {
+      const int id = ++s.idx[row];
+      if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
+      s.added[row]++;
+      s.preg[row] = best;
+      s.slot[row] ^= 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+      s.list[(parity ^ 1) * a.Npad + atomicAdd(&s.count[parity ^ 1], 1)] = row;
+    } else {
+      const int fl = a.f_lens[row];
+      int t = tidx[m] + 1;
+      if (t >= fl) {
+        s.fin[row] = 1;
+        atomicSub(s.unfinished, 1);
+      }
+      if (t > fl - 1) t = fl - 1;
+      s.time[row] = t;
+      s.added[row] = 0;
+    }
+  }
+}
+
+__global__ void dec_finish_kernel(DecArgs a) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row < a.N) a.res_len[row] = a.s.idx[row] + 1;
+}
+
+int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st) {
+  const int rt = a.Npad / 16;
+  if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(a.s.unfinished, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
+  if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
+  hipLaunchKernelGGL(dec_init_kernel, dim3((a.Npad + 255) / 256), dim3(256), 0, st, a);
+  constexpr int CHUNK = 32;
+  int step = 0, chunk = 0;
+  bool done = false;
+  while (!done && step < a.max_iter) {
+    for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
+      const int p = step & 1;
+      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rt), dim3(256), 0, st, a, 0, p);
+      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rt), dim3(256), 0, st, a, 1, p);
+      hipLaunchKernelGGL(dec_g_kernel, dim3(J / 128, rt), dim3(256), 0, st, a, p);
+      hipLaunchKernelGGL(dec_joint_kernel, dim3(rt), dim3(256), 0, st, a, p);
+    }
+    // poll the live-row counter one chunk behind, so the host never drains the queue
+    if (hipMemcpyAsync(host_flags + (chunk & 1), a.s.unfinished, sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
+        hipSuccess)
+      return -1;
+    if (hipEventRecord(evs[chunk & 1], st) != hipSuccess) return -1;
+    if (chunk > 0) {
+      if (hipEventSynchronize(evs[(chunk - 1) & 1]) != hipSuccess) return -1;
+      done = host_flags[(chunk - 1) & 1] == 0;
+    }
+    ++chunk;
+  }
+  hipLaunchKernelGGL(dec_finish_kernel, dim3((a.N + 255) / 256), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_joint_trans(const DecWeights& w, const uint16_t* fperm, const int32_t* f_lens, float* F, int Tp,
@@ -287,11 +371,6 @@ int launch_joint_trans(const DecWeights& w, const uint16_t* fperm, const int32_t
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_greedy_decode(const DecArgs& a, hipStream_t st) {
-  const int nwg = (a.N + DEC_ROWS - 1) / DEC_ROWS;
-  if (nwg <= 0) return 0;
-  hipLaunchKernelGGL(greedy_decode_kernel, dim3(nwg), dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
+
 
 }  // namespace rnnt

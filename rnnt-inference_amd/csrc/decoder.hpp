@@ -5,7 +5,6 @@
 
 namespace rnnt {
 
-constexpr int DEC_ROWS = 16;  // utterances per greedy-decode workgroup
 
 struct DecWeights {
   const uint16_t* embed;   // bf16 [28][320] natural
@@ -19,6 +18,13 @@ struct DecWeights {
   const float* b2;         // [32] (29..31 zero)
 };
 
+struct DecState {           // per-row greedy state, device arrays [Npad]
+  int32_t *time, *added, *idx, *preg, *slot, *fin;
+  int32_t* list;             // [2][Npad] emit lists (by step parity)
+  int32_t* count;            // [4] list lengths (2 used)
+  int32_t* unfinished;       // [4] live-row counter (1 used)
+};
+
 struct DecArgs {
   DecWeights w;
   const float* F;          // [Tp][Npad][512] joint trans half, F = b_t + bf16(f).W1t^T
@@ -27,12 +33,15 @@ struct DecArgs {
   float* G;                // [Npad][512] joint pred half of the current candidate
   int32_t* res;            // [N][max_res]
   int32_t* res_len;        // [N]
+  DecState s;
   int N, Npad, max_res, max_iter;
 };
 
 // F = b_t + bf16(f) . W1t^T for every frame t < Tp and row tile holding a row with f_len > t.
 int launch_joint_trans(const DecWeights& w, const uint16_t* fperm, const int32_t* f_lens, float* F, int Tp,
                        int Npad, hipStream_t st);
-int launch_greedy_decode(const DecArgs& a, hipStream_t st);
+// Host-driven lock-step loop; polls the live-row counter (host_flags: 2 pinned words, evs: 2
+// events) one 32-step chunk behind.
+int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st);
 
 }  // namespace rnnt

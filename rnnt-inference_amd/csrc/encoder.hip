@@ -30,44 +30,37 @@ __global__ void __launch_bounds__(256) quantize_kernel(const float4* __restrict_
 }
 
 // ---------------------------------------------------------------- LSTM step
-constexpr int BM = 128;        // gate rows per workgroup (32 units x 4 gates)
-constexpr int BN = 128;        // batch rows per workgroup
-constexpr int BK = 64;         // k bytes per stage (one 16x16x64 MFMA depth)
-constexpr int PITCH = BK + 16; // LDS row pitch (bytes): breaks the 64-B power-of-two stride
+constexpr int BM = 128;  // gate rows per workgroup (32 units x 4 gates)
+constexpr int BN = 128;  // batch rows per workgroup
+constexpr int BK = 64;   // k bytes per stage (one 16x16x64 MFMA depth)
 
-__global__ void __launch_bounds__(256, 2) lstm_i8_step_kernel(EncStepArgs a) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[2 * 2 * BM * PITCH];
-  int8_t* As = smem;                    // [2][BM][PITCH]
-  int8_t* Bs = smem + 2 * BM * PITCH;   // [2][BN][PITCH]
+// LDS image of a [128][64 B] tile: 16-byte column c of row r is stored at column
+// c ^ h[(r >> 2) & 3] with h = {0, 2, 3, 1}.  A fragment read (lane l: row l&15, column l>>4)
+// is a ds_read_b128 whose four 16-lane groups each touch rows {0-3,12-15} at one column and
+// rows 4-11 at the next; with this h every group lands on 16 distinct 16-byte bank slots
+// (the plain c ^ ((r>>2)&3) swizzle leaves them 2-way conflicted).
+__device__ __forceinline__ int swz(int row, int col16) {
+  const int h = (0x1320 >> (((row >> 2) & 3) * 4)) & 3;  // nibbles: h[0]=0 h[1]=2 h[2]=3 h[3]=1
+  return row * BK + ((col16 ^ h) << 4);
+}
+
+__device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int tile, int8_t* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.x * BM;       // packed gate row base
-  const int n0 = blockIdx.y * BN;       // batch row base
+  const int m0 = blockIdx.x * BM;  // packed gate row base
+  const int n0 = tile * BN;        // batch row base
   const int K = a.I + H;
   const int nK = K / BK;
 
-  // global -> register staging: 2 A chunks + 2 B chunks of 16 B per thread per stage
-  uint4 ra[2], rb[2];
-  auto load_stage = [&](int ks) {
-    const int k0 = ks * BK;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int ch = tid + c * 256, row = ch >> 2, col = (ch & 3) * 16;
-      ra[c] = *(const uint4*)(a.W + (size_t)(m0 + row) * K + k0 + col);
-      const int n = n0 + row;
-      const int8_t* src = (k0 < a.I) ? a.x + (size_t)n * a.I + k0 + col
-                                      : a.h_in + (size_t)n * H + (k0 - a.I) + col;
-      rb[c] = *(const uint4*)src;
-    }
-  };
-  auto store_stage = [&](int buf) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int ch = tid + c * 256, row = ch >> 2, col = (ch & 3) * 16;
-      *(uint4*)(As + (buf * BM + row) * PITCH + col) = ra[c];
-      *(uint4*)(Bs + (buf * BN + row) * PITCH + col) = rb[c];
-    }
-  };
+  // staging assignment: chunk ch = tid (+256): row ch>>2, 16-byte column ch&3
+  const int r0 = tid >> 2, r1 = r0 + 64, cc = tid & 3;
+  const int8_t* wa0 = a.W + (size_t)(m0 + r0) * K + cc * 16;
+  const int8_t* wa1 = a.W + (size_t)(m0 + r1) * K + cc * 16;
+  const int8_t* xb0 = a.x + (size_t)(n0 + r0) * a.I + cc * 16;
+  const int8_t* xb1 = a.x + (size_t)(n0 + r1) * a.I + cc * 16;
+  const int8_t* hb0 = a.h_in + (size_t)(n0 + r0) * H + cc * 16 - a.I;
+  const int8_t* hb1 = a.h_in + (size_t)(n0 + r1) * H + cc * 16 - a.I;
+  const int sa0 = swz(r0, cc), sa1 = swz(r1, cc);
 
   v4i acc[4][4];
 #pragma unroll
@@ -75,26 +68,57 @@ __global__ void __launch_bounds__(256, 2) lstm_i8_step_kernel(EncStepArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
 
-  load_stage(0);
-  store_stage(0);
+  uint4 ra0 = *(const uint4*)(wa0), ra1 = *(const uint4*)(wa1);
+  uint4 rb0 = *(const uint4*)(a.I > 0 ? xb0 : hb0), rb1 = *(const uint4*)(a.I > 0 ? xb1 : hb1);
+  {
+    int8_t* As = smem;
+    int8_t* Bs = smem + BM * BK;
+    *(uint4*)(As + sa0) = ra0; *(uint4*)(As + sa1) = ra1;
+    *(uint4*)(Bs + sa0) = rb0; *(uint4*)(Bs + sa1) = rb1;
+  }
   __syncthreads();
-  int cur = 0;
+
+  // fragment read offsets (rows wm*64 + i*16 + (lane&15), 16-byte column lane>>4)
+  int fa_off[4], fb_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    fa_off[i] = swz(wm * 64 + i * 16 + (lane & 15), lane >> 4);
+    fb_off[i] = swz(wn * 64 + i * 16 + (lane & 15), lane >> 4);
+  }
+
   for (int ks = 0; ks < nK; ++ks) {
-    if (ks + 1 < nK) load_stage(ks + 1);
+    const int cur = ks & 1;
+    const bool more = ks + 1 < nK;
+    if (more) {
+      const int k1 = (ks + 1) * BK;
+      ra0 = *(const uint4*)(wa0 + k1);
+      ra1 = *(const uint4*)(wa1 + k1);
+      if (k1 < a.I) {
+        rb0 = *(const uint4*)(xb0 + k1);
+        rb1 = *(const uint4*)(xb1 + k1);
+      } else {
+        rb0 = *(const uint4*)(hb0 + k1);
+        rb1 = *(const uint4*)(hb1 + k1);
+      }
+    }
+    const int8_t* As = smem + cur * (BM + BN) * BK;
+    const int8_t* Bs = As + BM * BK;
     v4i fa[4], fb[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      fa[i] = *(const v4i*)(As + (cur * BM + wm * 64 + i * 16 + (lane & 15)) * PITCH + (lane >> 4) * 16);
+    for (int i = 0; i < 4; ++i) fa[i] = *(const v4i*)(As + fa_off[i]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fb[j] = *(const v4i*)(Bs + (cur * BN + wn * 64 + j * 16 + (lane & 15)) * PITCH + (lane >> 4) * 16);
+    for (int j = 0; j < 4; ++j) fb[j] = *(const v4i*)(Bs + fb_off[j]);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    if (ks + 1 < nK) store_stage(cur ^ 1);
+    if (more) {
+      int8_t* An = smem + (cur ^ 1) * (BM + BN) * BK;
+      int8_t* Bn = An + BM * BK;
+      *(uint4*)(An + sa0) = ra0; *(uint4*)(An + sa1) = ra1;
+      *(uint4*)(Bn + sa0) = rb0; *(uint4*)(Bn + sa1) = rb1;
+    }
     __syncthreads();
-    cur ^= 1;
   }
 
   // ---- fused LSTM cell epilogue (quant_lstm.py:162-183 semantics; see oracle_lstm_i8_layer)
@@ -133,6 +157,24 @@ __global__ void __launch_bounds__(256, 2) lstm_i8_step_kernel(EncStepArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(256, 2) lstm_i8_tick_kernel(EncTickArgs args) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[2 * (BM + BN) * BK];
+  const int y = blockIdx.y;
+  // wave-uniform job lookup; each case inlines the body with a constant job index so the
+  // job's arguments stay in the kernarg segment (scalar loads, no private copy)
+  if (y < args.tile_start[1]) {
+    lstm_i8_step(args.job[0], y, smem);
+  } else if (y < args.tile_start[2]) {
+    lstm_i8_step(args.job[1], y - args.tile_start[1], smem);
+  } else if (y < args.tile_start[3]) {
+    lstm_i8_step(args.job[2], y - args.tile_start[2], smem);
+  } else if (y < args.tile_start[4]) {
+    lstm_i8_step(args.job[3], y - args.tile_start[3], smem);
+  } else {
+    lstm_i8_step(args.job[4], y - args.tile_start[4], smem);
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStream_t st) {
   const int64_t n4 = n / 4;
@@ -143,9 +185,10 @@ int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStrea
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_lstm_i8_step(const EncStepArgs& a, int n_tiles, hipStream_t st) {
-  if (n_tiles <= 0) return 0;
-  hipLaunchKernelGGL(lstm_i8_step_kernel, dim3(G4 / BM, n_tiles), dim3(256), 0, st, a);
+int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
+  const int tiles = a.tile_start[a.njobs];
+  if (tiles <= 0) return 0;
+  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(G4 / BM, tiles), dim3(256), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

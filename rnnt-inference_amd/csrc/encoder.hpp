@@ -28,7 +28,16 @@ struct EncStepArgs {
   float rb, in_s, out_s;
 };
 
+// One launch runs up to ENC_MAX_JOBS independent layer-steps (the wavefront schedule of
+// engine.hip: layer l at its own frame); grid.y enumerates (job, batch tile) pairs.
+constexpr int ENC_MAX_JOBS = 5;
+struct EncTickArgs {
+  EncStepArgs job[ENC_MAX_JOBS];
+  int tile_start[ENC_MAX_JOBS + 1];  // prefix sums of each job's active batch tiles
+  int njobs;
+};
+
 int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStream_t st);
-int launch_lstm_i8_step(const EncStepArgs& a, int n_tiles, hipStream_t st);
+int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st);
 
 }  // namespace rnnt

@@ -46,12 +46,15 @@ struct rnnt_engine {
   DecWeights dw{};
   std::vector<void*> allocs;
   // workspace
-  int8_t *x0q = nullptr, *yA = nullptr, *xs = nullptr, *yB = nullptr;
+  int8_t *x0q = nullptr, *yA = nullptr, *xs = nullptr, *yB = nullptr, *yC = nullptr;
   int8_t* h[5][2] = {};
   uint16_t* c[5] = {};
   uint16_t* fperm = nullptr;
   float *F = nullptr, *hc = nullptr, *G = nullptr;
   int32_t* flen = nullptr;
+  DecState ds{};
+  int32_t* host_flags = nullptr;
+  hipEvent_t poll_ev[2] = {nullptr, nullptr};
   // last encoded batch
   int last_T = 0, last_n = 0, last_npad = 0;
   // profiling
@@ -161,6 +164,7 @@ static int alloc_workspace(rnnt_engine* e) {
   r = r ? r : dev_alloc(e, &e->yA, TM * NP * H);
   r = r ? r : dev_alloc(e, &e->xs, TPM * NP * 2 * H);
   r = r ? r : dev_alloc(e, &e->yB, TPM * NP * H);
+  r = r ? r : dev_alloc(e, &e->yC, TPM * NP * H);
   for (int l = 0; l < 5 && !r; ++l) {
     r = r ? r : dev_alloc(e, &e->h[l][0], NP * H);
     r = r ? r : dev_alloc(e, &e->h[l][1], NP * H);
@@ -171,6 +175,16 @@ static int alloc_workspace(rnnt_engine* e) {
   r = r ? r : dev_alloc(e, &e->hc, NP * 2 * 4 * P);
   r = r ? r : dev_alloc(e, &e->G, NP * J);
   r = r ? r : dev_alloc(e, &e->flen, NP);
+  int32_t** ints[] = {&e->ds.time, &e->ds.added, &e->ds.idx, &e->ds.preg, &e->ds.slot, &e->ds.fin};
+  for (auto pp : ints) r = r ? r : dev_alloc(e, pp, NP);
+  r = r ? r : dev_alloc(e, &e->ds.list, 2 * NP);
+  r = r ? r : dev_alloc(e, &e->ds.count, 4);
+  r = r ? r : dev_alloc(e, &e->ds.unfinished, 4);
+  if (!r && hipHostMalloc((void**)&e->host_flags, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
+    r = fail(RNNT_ENOMEM, "hipHostMalloc failed");
+  for (int i = 0; i < 2 && !r; ++i)
+    if (hipEventCreateWithFlags(&e->poll_ev[i], hipEventDisableTiming) != hipSuccess)
+      r = fail(RNNT_EDEVICE, "hipEventCreate failed");
   return r;
 }
 
@@ -178,6 +192,9 @@ extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   for (void* p : e->allocs) (void)hipFree(p);
+  if (e->host_flags) (void)hipHostFree(e->host_flags);
+  for (auto ev : e->poll_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -225,7 +242,9 @@ __global__ void stack_time_kernel(const int8_t* x, const int32_t* lens, int T, i
   }
 }
 
-static hipStream_t pick(rnnt_engine* e, void* s) { return s ? (hipStream_t)s : e->stream; }
+// `stream` is used as given: 0 is the legacy default (null) stream, which is what torch's
+// default stream is; the engine's own stream is only used by rnnt_engine_create.
+static hipStream_t pick(rnnt_engine*, void* s) { return (hipStream_t)s; }
 
 // number of leading 128-row tiles that hold a row with len > thr
 static int active_tiles(const std::vector<int>& tile_max, int thr) {
@@ -235,42 +254,63 @@ static int active_tiles(const std::vector<int>& tile_max, int thr) {
   return last + 1;
 }
 
-static int run_layer(rnnt_engine* e, int l, int T, int n_pad, const int8_t* x, int mode, void* y,
-                     float* y32, const std::vector<int>& tile_max, const int32_t* lens, hipStream_t st,
-                     int stacked_T = 0) {
+// Build the step job of encoder layer l at frame t (layers 0/1: feature frame, 2..4: stacked frame).
+static EncStepArgs make_job(rnnt_engine* e, int l, int t, int n_pad, const int8_t* x, int mode, void* y, float* y32,
+                            const int32_t* lens, int stacked_T) {
   const int I = ENC_I[l];
+  EncStepArgs a{};
+  a.W = e->enc_w[l];
+  a.bq = e->enc_bq[l];
+  a.x = x + (size_t)t * n_pad * I;
+  a.h_in = e->h[l][t & 1];
+  a.h_out = e->h[l][(t + 1) & 1];
+  a.c = e->c[l];
+  a.I = I;
+  a.mode = mode;
+  a.rb = e->rb[l];
+  a.in_s = e->in_s[l];
+  a.out_s = e->out_s[l];
+  a.lens = lens;
+  if (mode == ENC_OUT_STACKED) {
+    a.y8 = (int8_t*)y + (size_t)(t / 2) * n_pad * 2 * H;
+    a.t = t;
+    a.half = t & 1;
+    a.zero_next = ((t & 1) == 0 && t + 1 == stacked_T);
+  } else if (mode == ENC_OUT_I8) {
+    a.y8 = (int8_t*)y + (size_t)t * n_pad * H;
+  } else {
+    a.y32 = y32 ? y32 + (size_t)t * n_pad * H : nullptr;
+    a.fperm = (uint16_t*)y + (size_t)t * n_pad * H;
+  }
+  return a;
+}
+
+struct TickBuilder {
+  EncTickArgs args{};
+  int n = 0;
+  void add(const EncStepArgs& a, int tiles) {
+    if (tiles <= 0) return;
+    args.job[n] = a;
+    args.tile_start[n + 1] = args.tile_start[n] + tiles;
+    ++n;
+  }
+  int launch(rnnt_engine* e, hipStream_t st) {
+    if (n == 0) return 0;
+    args.njobs = n;
+    for (int j = n + 1; j <= ENC_MAX_JOBS; ++j) args.tile_start[j] = args.tile_start[n];
+    e->step_launches++;
+    return launch_lstm_i8_tick(args, st) ? fail(RNNT_EDEVICE, "lstm tick launch failed") : 0;
+  }
+};
+
+// One layer over T steps, one launch per step (op-level API).
+static int run_layer(rnnt_engine* e, int l, int T, int n_pad, const int8_t* x, int mode, void* y, float* y32,
+                     hipStream_t st) {
   for (int t = 0; t < T; ++t) {
-    EncStepArgs a{};
-    a.W = e->enc_w[l];
-    a.bq = e->enc_bq[l];
-    a.x = x + (size_t)t * n_pad * I;
-    a.h_in = e->h[l][t & 1];
-    a.h_out = e->h[l][(t + 1) & 1];
-    a.c = e->c[l];
-    a.I = I;
-    a.mode = mode;
-    a.rb = e->rb[l];
-    a.in_s = e->in_s[l];
-    a.out_s = e->out_s[l];
-    a.lens = lens;
-    int thr;
-    if (mode == ENC_OUT_STACKED) {
-      a.y8 = (int8_t*)y + (size_t)(t / 2) * n_pad * 2 * H;
-      a.t = t;
-      a.half = t & 1;
-      a.zero_next = ((t & 1) == 0 && t + 1 == stacked_T);
-      thr = 2 * (t / 2);
-    } else if (mode == ENC_OUT_I8) {
-      a.y8 = (int8_t*)y + (size_t)t * n_pad * H;
-      thr = l < 2 ? 2 * (t / 2) : 2 * t;
-    } else {
-      a.y32 = y32 ? y32 + (size_t)t * n_pad * H : nullptr;
-      a.fperm = (uint16_t*)y + (size_t)t * n_pad * H;
-      thr = 2 * t;
-    }
-    const int nt = tile_max.empty() ? n_pad / ENC_BATCH_TILE : active_tiles(tile_max, thr);
-    if (launch_lstm_i8_step(a, nt, st)) return fail(RNNT_EDEVICE, "lstm step launch failed");
-    e->step_launches += nt > 0;
+    TickBuilder tb;
+    tb.add(make_job(e, l, t, n_pad, x, mode, y, y32, nullptr, 0), n_pad / ENC_BATCH_TILE);
+    int r = tb.launch(e, st);
+    if (r) return r;
   }
   return 0;
 }
@@ -306,15 +346,34 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
   hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
   if (launch_quantize(feats, (int64_t)T * n_pad * FEAT, e->in_s[0], e->x0q, st))
     return fail(RNNT_EDEVICE, "quantize launch failed");
-  if ((r = run_layer(e, 0, T, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, tm, lens, st))) return r;
-  if ((r = run_layer(e, 1, T, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, tm, lens, st, T))) return r;
-  if ((r = run_layer(e, 2, Tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, tm, lens, st))) return r;
-  if ((r = run_layer(e, 3, Tp, n_pad, e->yB, ENC_OUT_I8, e->yA, nullptr, tm, lens, st))) return r;
-  if ((r = run_layer(e, 4, Tp, n_pad, e->yA, ENC_OUT_FINAL, e->fperm, f_out, tm, lens, st))) return r;
-  if (e->prof) e->ev_enc.push_back({ev0, new_event(st)});
-  e->encode_calls++;
+  // Wavefront schedule: tick tau runs layer 0 at frame tau, layer 1 at frame tau-1, and the
+  // post_rnn layers 2/3/4 at stacked frame t' on ticks 2t'+3 / 2t'+4 / 2t'+5, i.e. as soon as
+  // their inputs exist.  Every job of a tick is independent (inputs come from earlier ticks).
+  const int nt_all = n_pad / ENC_BATCH_TILE;
+  auto tiles = [&](int thr) { return tm.empty() ? nt_all : active_tiles(tm, thr); };
+  const int n_ticks = std::max(T + 1, 2 * Tp + 4);
+  for (int tau = 0; tau < n_ticks; ++tau) {
+    TickBuilder tb;
+    if (tau < T) tb.add(make_job(e, 0, tau, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, lens, T), tiles(2 * (tau / 2)));
+    if (tau >= 1 && tau - 1 < T) {
+      const int t = tau - 1;
+      tb.add(make_job(e, 1, t, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, lens, T), tiles(2 * (t / 2)));
+    }
+    for (int l = 2; l < 5; ++l) {
+      const int d = tau - (l + 1);  // = 2t'
+      if (d >= 0 && (d & 1) == 0 && d / 2 < Tp) {
+        const int tp = d / 2;
+        if (l == 2) tb.add(make_job(e, 2, tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, lens, T), tiles(2 * tp));
+        if (l == 3) tb.add(make_job(e, 3, tp, n_pad, e->yB, ENC_OUT_I8, e->yC, nullptr, lens, T), tiles(2 * tp));
+        if (l == 4) tb.add(make_job(e, 4, tp, n_pad, e->yC, ENC_OUT_FINAL, e->fperm, f_out, lens, T), tiles(2 * tp));
+      }
+    }
+    if ((r = tb.launch(e, st))) return r;
+  }
   hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->flen, n_pad);
   HIPCHK(hipGetLastError());
+  if (e->prof) e->ev_enc.push_back({ev0, new_event(st)});
+  e->encode_calls++;
   e->last_T = T;
   e->last_n = n;
   e->last_npad = n_pad;
@@ -343,8 +402,9 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   a.N = e->last_n;
   a.Npad = e->last_npad;
   a.max_res = max_res;
+  a.s = e->ds;
   a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
-  if (launch_greedy_decode(a, st)) return fail(RNNT_EDEVICE, "greedy launch failed");
+  if (launch_greedy_decode(a, e->host_flags, e->poll_ev, st)) return fail(RNNT_EDEVICE, "greedy launch failed");
   if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
   e->decode_calls++;
   return 0;
@@ -409,7 +469,6 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
       return fail(RNNT_EDEVICE, "quantize launch failed");
     cur = e->x0q;
   }
-  const std::vector<int> none;
   for (int i = 0; i < count; ++i) {
     const int l = first + i;
     const size_t NH = (size_t)n_pad * H;
@@ -419,9 +478,9 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
     int8_t* dst = last ? (int8_t*)y : ((cur == e->yA) ? e->yB : e->yA);
     int r;
     if (l == 4)
-      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_FINAL, e->fperm, (float*)y, none, nullptr, st);
+      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_FINAL, e->fperm, (float*)y, st);
     else
-      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_I8, dst, nullptr, none, nullptr, st);
+      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_I8, dst, nullptr, st);
     if (r) return r;
     HIPCHK(hipMemcpyAsync(hx + i * NH, e->h[l][T & 1], NH, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(cx + i * NH, e->c[l], NH * 2, hipMemcpyDeviceToDevice, st));

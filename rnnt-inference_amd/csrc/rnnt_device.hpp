@@ -54,7 +54,15 @@ __device__ __forceinline__ float det_tanh(float x) {
   return __builtin_copysignf(t, x);
 }
 
+// f32 -> f16 round-half-even and f16 -> f32 on the hardware converters (v_cvt_f16_f32 /
+// v_cvt_f32_f16, default RNE, f16 denormals preserved): bit-identical to oracle_f2h/h2f.
 __device__ __forceinline__ uint16_t f2h(float f) {
+  const _Float16 h = (_Float16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float h2f(uint16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
+
+__device__ __forceinline__ uint16_t f2h_soft(float f) {
   const uint32_t x = f2bits(f), sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
   if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));
   if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);
@@ -70,7 +78,7 @@ __device__ __forceinline__ uint16_t f2h(float f) {
   if (rem > half || (rem == half && (q & 1u))) q++;
   return (uint16_t)(sign | q);
 }
-__device__ __forceinline__ float h2f(uint16_t h) {
+__device__ __forceinline__ float h2f_soft(uint16_t h) {
   const uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
   if (e == 0) {
     const float v = (float)m * 5.9604644775390625e-8f;
