@@ -98,7 +98,8 @@ typedef struct {
   double encode_ms;       /* first to last encoder kernel of each encode call (step kernels + gaps) */
   double joint_trans_ms;  /* the F = b_t + f.W1t^T GEMM */
   double greedy_ms;       /* the device-side greedy decode loop */
-  int64_t step_launches;  /* lstm step kernels launched */
+  int64_t step_launches;  /* encoder tick kernels launched */
+  int64_t decode_steps;   /* greedy lock-step iterations enqueued */
   int64_t encode_calls, decode_calls;
 } rnnt_stats;
 int rnnt_engine_set_profiling(rnnt_engine* e, int on);

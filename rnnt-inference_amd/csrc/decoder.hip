@@ -116,6 +116,17 @@ __global__ void __launch_bounds__(256) dec_pred_kernel(DecArgs a, int layer, int
   if (rt * 16 >= cnt) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   const int* list = s.list + parity * a.Npad;
+  // this wave's weight fragments (2 gate tiles x 20 k-blocks = 160 VGPRs) in one burst, issued
+  // before the operand staging so the L2 round trip overlaps it
+  const int gt = blockIdx.x * 8 + wave * 2;
+  const uint16_t* w0 = a.w.wp[layer] + (size_t)(gt * 16 + c) * 640 + 8 * q;
+  const uint16_t* w1 = w0 + 16 * 640;
+  uint4 wa[20], wb[20];
+#pragma unroll
+  for (int b = 0; b < 20; ++b) {
+    wa[b] = *(const uint4*)(w0 + 32 * b);
+    wb[b] = *(const uint4*)(w1 + 32 * b);
+  }
   if (tid < 16) {
     const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
     rows[tid] = row;
@@ -149,9 +160,12 @@ __global__ void __launch_bounds__(256) dec_pred_kernel(DecArgs a, int layer, int
     X[mi][chain_pos(k + 3)] = v.w;
   }
   __syncthreads();
-  const uint16_t* W = a.w.wp[layer];
+#pragma unroll
+  for (int b = 0; b < 20; ++b)  // weights are live (waited for) here, behind the staging
+    asm volatile("" ::"v"(wa[b].x), "v"(wa[b].y), "v"(wa[b].z), "v"(wa[b].w), "v"(wb[b].x), "v"(wb[b].y),
+                 "v"(wb[b].z), "v"(wb[b].w));
   const float* bias = a.w.bp_lstm[layer];
-  const int gt = blockIdx.x * 8 + wave * 2;
+  const float* xrow = &X[c][8 * q];
   v4f acc0, acc1;
   {
     const float4 b0 = *(const float4*)(bias + gt * 16 + 4 * q);
@@ -159,24 +173,13 @@ __global__ void __launch_bounds__(256) dec_pred_kernel(DecArgs a, int layer, int
     acc0 = v4f{b0.x, b0.y, b0.z, b0.w};
     acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
   }
-  const uint16_t* w0 = W + (size_t)(gt * 16 + c) * 640 + 8 * q;
-  const uint16_t* w1 = w0 + 16 * 640;
-  const float* xrow = &X[c][8 * q];
-  uint4 wa = *(const uint4*)w0, wb = *(const uint4*)w1;
-#pragma unroll 4
+#pragma unroll
   for (int b = 0; b < 640 / 32; ++b) {
-    uint4 na = wa, nb = wb;
-    if (b + 1 < 640 / 32) {
-      na = *(const uint4*)(w0 + 32 * (b + 1));
-      nb = *(const uint4*)(w1 + 32 * (b + 1));
-    }
     float x[8];
     *(float4*)&x[0] = *(const float4*)(xrow + 32 * b);
     *(float4*)&x[4] = *(const float4*)(xrow + 32 * b + 4);
-    acc0 = chain8(wa, x, acc0);
-    acc1 = chain8(wb, x, acc1);
-    wa = na;
-    wb = nb;
+    acc0 = chain8(wa[b], x, acc0);
+    acc1 = chain8(wb[b], x, acc1);
   }
   const int row = rows[c];
   if (row >= 0) {
@@ -233,13 +236,19 @@ __global__ void __launch_bounds__(256) dec_g_kernel(DecArgs a, int parity) {
   const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
   const uint16_t* w1 = w0 + 16 * P;
   const float* xr = &X[c][8 * q];
-#pragma unroll 2
+  uint4 wa[P / 32], wb[P / 32];
+#pragma unroll
+  for (int b = 0; b < P / 32; ++b) {
+    wa[b] = *(const uint4*)(w0 + 32 * b);
+    wb[b] = *(const uint4*)(w1 + 32 * b);
+  }
+#pragma unroll
   for (int b = 0; b < P / 32; ++b) {
     float x[8];
     *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
     *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-    acc0 = chain8(*(const uint4*)(w0 + 32 * b), x, acc0);
-    acc1 = chain8(*(const uint4*)(w1 + 32 * b), x, acc1);
+    acc0 = chain8(wa[b], x, acc0);
+    acc1 = chain8(wb[b], x, acc1);
   }
   const int row = rows[c];
   if (row >= 0) {
@@ -289,12 +298,15 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
     const uint16_t* wr = a.w.w2 + (size_t)(wave * 16 + c) * J + 8 * q;
     const float* xr = &X[c][8 * q];
-#pragma unroll 4
+    uint4 wv[J / 32];
+#pragma unroll
+    for (int b = 0; b < J / 32; ++b) wv[b] = *(const uint4*)(wr + 32 * b);
+#pragma unroll
     for (int b = 0; b < J / 32; ++b) {
       float x[8];
       *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
       *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-      acc = chain8(*(const uint4*)(wr + 32 * b), x, acc);
+      acc = chain8(wv[b], x, acc);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) L[c][wave * 16 + 4 * q + r] = acc[r];
@@ -361,7 +373,7 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     ++chunk;
   }
   hipLaunchKernelGGL(dec_finish_kernel, dim3((a.N + 255) / 256), dim3(256), 0, st, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  return hipGetLastError() == hipSuccess ? step : -1;
 }
 
 int launch_joint_trans(const DecWeights& w, const uint16_t* fperm, const int32_t* f_lens, float* F, int Tp,

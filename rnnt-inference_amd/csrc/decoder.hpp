@@ -42,6 +42,7 @@ int launch_joint_trans(const DecWeights& w, const uint16_t* fperm, const int32_t
                        int Npad, hipStream_t st);
 // Host-driven lock-step loop; polls the live-row counter (host_flags: 2 pinned words, evs: 2
 // events) one 32-step chunk behind.
+// Returns the number of steps enqueued (>= 0) or -1.
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st);
 
 }  // namespace rnnt

@@ -61,7 +61,7 @@ struct rnnt_engine {
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_enc;
   std::vector<std::array<hipEvent_t, 3>> ev_dec;
-  int64_t step_launches = 0, encode_calls = 0, decode_calls = 0;
+  int64_t step_launches = 0, decode_steps = 0, encode_calls = 0, decode_calls = 0;
 };
 
 static hipEvent_t new_event(hipStream_t st) {
@@ -404,7 +404,9 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   a.max_res = max_res;
   a.s = e->ds;
   a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
-  if (launch_greedy_decode(a, e->host_flags, e->poll_ev, st)) return fail(RNNT_EDEVICE, "greedy launch failed");
+  const int steps = launch_greedy_decode(a, e->host_flags, e->poll_ev, st);
+  if (steps < 0) return fail(RNNT_EDEVICE, "greedy launch failed");
+  e->decode_steps += steps;
   if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
   e->decode_calls++;
   return 0;
@@ -435,6 +437,7 @@ extern "C" int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset)
     out->greedy_ms += b;
   }
   out->step_launches = e->step_launches;
+  out->decode_steps = e->decode_steps;
   out->encode_calls = e->encode_calls;
   out->decode_calls = e->decode_calls;
   if (reset) {
@@ -442,7 +445,7 @@ extern "C" int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset)
     for (auto& p : e->ev_dec) for (auto ev : p) (void)hipEventDestroy(ev);
     e->ev_enc.clear();
     e->ev_dec.clear();
-    e->step_launches = e->encode_calls = e->decode_calls = 0;
+    e->step_launches = e->decode_steps = e->encode_calls = e->decode_calls = 0;
   }
   return 0;
 }

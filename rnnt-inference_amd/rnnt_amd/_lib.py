@@ -35,7 +35,7 @@ class RnntOpts(C.Structure):
 
 class RnntStats(C.Structure):
     _fields_ = [("encode_ms", C.c_double), ("joint_trans_ms", C.c_double), ("greedy_ms", C.c_double),
-                ("step_launches", C.c_int64), ("encode_calls", C.c_int64), ("decode_calls", C.c_int64)]
+                ("step_launches", C.c_int64), ("decode_steps", C.c_int64), ("encode_calls", C.c_int64), ("decode_calls", C.c_int64)]
 
 
 _SIGS = {
