@@ -11,7 +11,7 @@ offline, so the query / response types are plain Python):
                   and completes each sample with its int32 token row (res_len*4 bytes,
                   QuerySamplesComplete, torch_sut.cpp:221-236).
 Multi-GPU: one process per GPU, each with its own engine; a query's sorted samples are dealt
-to ranks in batch-sized chunks (round-robin, so every rank gets the same length mix).  There
+to ranks in batch-sized chunks (snake order, so every rank gets the same length mix).  There
 is no data-path collective: results are completed per rank.
 """
 from dataclasses import dataclass
@@ -69,9 +69,16 @@ class RNNTQSL:
 
 
 def deal_batches(sorted_samples, batch_size, rank=0, world=1):
-    """Split a sorted query into batch_size chunks and deal them round-robin to ranks."""
+    """Split a length-sorted query into batch_size chunks and deal them to ranks in snake
+    order (0,1,..,w-1,w-1,..,0,0,..) so every rank gets a similar share of long and short
+    utterances; returns this rank's chunks."""
     chunks = [sorted_samples[i:i + batch_size] for i in range(0, len(sorted_samples), batch_size)]
-    return chunks[rank::world]
+    mine = []
+    for i, ch in enumerate(chunks):
+        r = i % world if (i // world) % 2 == 0 else world - 1 - (i % world)
+        if r == rank:
+            mine.append(ch)
+    return mine
 
 
 class OfflineSUT:

@@ -1,0 +1,91 @@
+"""The intel_mlperf operator mirror (rnnt_amd.ops) and the GreedyDecoder mirror on the GPU,
+against the CPU restatement, at batch sizes that are not multiples of the engine's tile."""
+import numpy as np
+import pytest
+
+from rnnt_amd import synthetic, weights
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def model():
+    return weights.build_model()[0]
+
+
+@pytest.fixture(scope="module")
+def dec(model):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rnnt_amd.decoder import GreedyDecoder
+    d = GreedyDecoder(model, "quant", True, split_len=2, batch_size=64, max_frames=128)
+    yield d
+    d.close()
+
+
+def test_lstm_amx_int8_pre_and_post(dec, model, oracle):
+    from rnnt_amd import ops
+    T, N = 6, 5
+    x = synthetic.make_features(T, N, seed=9)[:, :, :240]
+    hx = [torch.zeros((N, 1024), dtype=torch.int8, device="cuda") for _ in range(2)]
+    cx = [torch.zeros((N, 1024), dtype=torch.float16, device="cuda") for _ in range(2)]
+    w = [[torch.from_numpy(model.enc_w[l][:, :I]), torch.from_numpy(model.enc_w[l][:, I:]), None, None]
+         for l, I in ((0, 256), (1, 1024))]
+    y, h, c = ops.lstm_amx_int8(torch.from_numpy(x.copy()).cuda(), hx, cx, w, model.enc_rb[:2], model.enc_in_s[:2],
+                                model.enc_out_s[:2], False)
+    xq = oracle.quantize(np.pad(x, ((0, 0), (0, 0), (0, 16))), model.enc_in_s[0])
+    y0, h0, c0 = oracle.lstm_i8_layer(xq, model.enc_w[0], model.enc_bq[0], model.enc_rb[0], model.enc_in_s[0],
+                                      model.enc_out_s[0], False, np.zeros((N, 1024), np.int8), np.zeros((N, 1024), np.uint16))
+    y1, h1, c1 = oracle.lstm_i8_layer(y0, model.enc_w[1], model.enc_bq[1], model.enc_rb[1], model.enc_in_s[1],
+                                      model.enc_out_s[1], False, np.zeros((N, 1024), np.int8), np.zeros((N, 1024), np.uint16))
+    np.testing.assert_array_equal(y.cpu().numpy(), y1)
+    np.testing.assert_array_equal(h[1].cpu().numpy(), h1)
+    np.testing.assert_array_equal(c[0].cpu().numpy().view(np.uint16), c0)
+    # stack_time + post_rnn through the same surface
+    lens = torch.tensor([6, 3, 6, 1, 0], dtype=torch.int32)
+    xs = ops.stack_time(y, lens.cuda(), 2)
+    np.testing.assert_array_equal(xs.cpu().numpy(), oracle.stack_time_i8(y1, lens.numpy()))
+    hx3 = [torch.zeros((N, 1024), dtype=torch.int8, device="cuda") for _ in range(3)]
+    cx3 = [torch.zeros((N, 1024), dtype=torch.float16, device="cuda") for _ in range(3)]
+    w3 = [[torch.from_numpy(model.enc_w[l][:, :-1024]), torch.from_numpy(model.enc_w[l][:, -1024:]), None, None] for l in (2, 3, 4)]
+    f, _, _ = ops.lstm_amx_int8(xs, hx3, cx3, w3, model.enc_rb[2:], model.enc_in_s[2:], model.enc_out_s[2:], True)
+    cur = xs.cpu().numpy()
+    for l in (2, 3, 4):
+        cur, _, _ = oracle.lstm_i8_layer(cur, model.enc_w[l], model.enc_bq[l], model.enc_rb[l], model.enc_in_s[l],
+                                         model.enc_out_s[l], l == 4, np.zeros((N, 1024), np.int8), np.zeros((N, 1024), np.uint16))
+    np.testing.assert_array_equal(f.cpu().numpy().view(np.uint32), cur.view(np.uint32))
+
+
+def test_greedy_decoder_mirror(dec, model, oracle):
+    """GreedyDecoder.forward contract (decoder.py:21-94): res [N, 30*max_len] SOS-filled, lens."""
+    lens = np.array([77, 40, 3, 60, 11], np.int32)
+    T = int(lens.max())
+    x = synthetic.make_features(T, len(lens), seed=12, lens=lens)[:, :, :240]
+    res, rl = dec(torch.from_numpy(x.copy()).cuda(), torch.from_numpy(lens))
+    assert res.shape == (5, 30 * T)
+    fo = oracle.encoder_i8(model, np.pad(x, ((0, 0), (0, 0), (0, 16))), lens)
+    ro, rlo, _ = oracle.greedy_decode(model, fo, (lens + 1) // 2, max_res=30 * T)
+    np.testing.assert_array_equal(rl.cpu().numpy(), rlo)
+    np.testing.assert_array_equal(res.cpu().numpy(), ro)
+
+
+def test_offline_sut_end_to_end(dec, model, oracle):
+    """OfflineSUT.issue_queries (torch_sut.cpp:140-236 semantics): sorted batches through the
+    engine, each sample completed with its own token row; identical to the CPU restatement."""
+    from rnnt_amd.sut import OfflineSUT, QuerySample, RNNTQSL
+    lengths = synthetic.devclean_lengths(37, seed=31)
+    lengths = np.minimum(lengths, 128)
+    qsl = RNNTQSL.synthetic(lengths, seed=32)
+    done = []
+    sut = OfflineSUT(dec.engine, qsl, batch_size=16, on_complete=lambda s, row: done.append(s.id))
+    samples = [QuerySample(id=1000 + i, index=i) for i in range(len(lengths))]
+    sut.issue_queries(samples)
+    assert sorted(done) == [s.id for s in samples]
+    for s in samples[:8]:
+        L = int(lengths[s.index])
+        x = np.zeros((L, 1, 256), np.float32)
+        x[:, 0, :240] = qsl.features[s.index]
+        fo = oracle.encoder_i8(model, x, np.array([L], np.int32))
+        ro, rlo, _ = oracle.greedy_decode(model, fo, np.array([(L + 1) // 2], np.int32))
+        np.testing.assert_array_equal(sut.responses[s.id], ro[0, : rlo[0]])
