@@ -7,6 +7,15 @@ namespace rnnt {
 
 constexpr int ENC_BATCH_TILE = 128;  // batch rows per encoder workgroup (buffers padded to it)
 
+// Packed row of (unit u, gate g) in the encoder weight image.  A 128-row workgroup tile
+// holds 32 units; inside it, wave half wm = (u>>4)&1, MFMA tile i = u&3, lane group
+// q = (u>>2)&3 and accumulator register g: row = 128*(u>>5) + 64*wm + 16*i + 4*q + g.  One
+// lane then owns the four gates of units u0..u0+3 (u0 = 32*(u>>5) + 16*wm + 4*q) for its
+// batch row, so the cell epilogue reads/writes 4 consecutive units per access.
+__host__ __device__ __forceinline__ int enc_packed_row(int u, int g) {
+  return ((u >> 5) << 7) + (((u >> 4) & 1) << 6) + ((u & 3) << 4) + (((u >> 2) & 3) << 2) + g;
+}
+
 enum EncOutMode { ENC_OUT_I8 = 0, ENC_OUT_STACKED = 1, ENC_OUT_FINAL = 2 };
 
 struct EncStepArgs {

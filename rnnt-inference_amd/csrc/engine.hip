@@ -98,8 +98,9 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
     std::vector<float> b(G4);
     for (int g = 0; g < 4; ++g)
       for (int u = 0; u < H; ++u) {
-        memcpy(&w[(size_t)(4 * u + g) * K], m->enc_w[l] + (size_t)(g * H + u) * K, K);
-        b[4 * u + g] = m->enc_bq[l][g * H + u];
+        const int pr = enc_packed_row(u, g);
+        memcpy(&w[(size_t)pr * K], m->enc_w[l] + (size_t)(g * H + u) * K, K);
+        b[pr] = m->enc_bq[l][g * H + u];
       }
     int r = upload(e, &e->enc_w[l], w);
     if (!r) r = upload(e, &e->enc_bq[l], b);

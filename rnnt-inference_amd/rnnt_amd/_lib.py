@@ -9,7 +9,8 @@ import re
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librnnt_mi355x.so")
+# RNNT_MI355X_LIB: development override (kernel variants built by tools/ into build_dev/)
+LIB_PATH = os.environ.get("RNNT_MI355X_LIB") or os.path.join(_HERE, "librnnt_mi355x.so")
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 HEADER = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "rnnt_mi355x.h")
 
