@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """MLPerf-Offline-style throughput of the MI355X RNN-T engine (utterances/s).
 
-Workload (BASELINE.json metric / config 4): an Offline query over a LibriSpeech-dev-clean-
-shaped QSL of 2513 synthetic utterances PER GPU (weak scaling: one process per GPU, each
-with its own shard, no data-path collective), sorted longest-first and run in batches of
---batch through the int8 encoder + bf16 prediction/joint + device-side greedy decode.  One
-step = one pass over the rank's shard, features already resident in HBM; the host gather of
-each utterance's int32 tokens (QuerySamplesComplete payload) is inside the timed region.
+Workload (BASELINE.json metric / config 4): LoadGen's Offline scenario.  Each GPU holds a
+LibriSpeech-dev-clean-shaped QSL of 2513 synthetic utterances (mlperf.conf:13) and serves one
+Offline query of --query samples (default 24576 = *.Offline.min_query_count, mlperf.conf:63;
+LoadGen fills it by repeating the QSL), weak scaling: one process per GPU, each with its own
+query, no data-path collective.  The SUT sorts the query longest-first (rnnt_qsl.cpp:104-133)
+and runs it in batches of --batch through the int8 encoder + bf16 prediction/joint +
+device-side greedy decode.  One step = one whole query, features already resident in HBM;
+the host gather of each utterance's int32 tokens (QuerySamplesComplete payload) is inside
+the timed region.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -37,9 +40,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--qsl", type=int, default=2513, help="utterances per GPU (mlperf.conf:13)")
-    ap.add_argument("--batch", type=int, default=2560, help="utterances per encode+decode call (one call covers the 2513-sample shard)")
-    ap.add_argument("--cpu-sample", type=int, default=24, help="utterances timed on the CPU restatement")
+    ap.add_argument("--qsl", type=int, default=2513, help="QSL utterances per GPU (mlperf.conf:13)")
+    ap.add_argument("--query", type=int, default=24576, help="samples per Offline query per GPU (mlperf.conf:63)")
+    ap.add_argument("--batch", type=int, default=8192, help="utterances per encode+decode call")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (profiles/), if present")
@@ -72,21 +76,41 @@ def all_max(x, world):
     return float(t.item())
 
 
-def make_batches(lens, batch, seed):
-    """Sorted (longest first, rnnt_qsl.cpp:104-133) batches, features staged in HBM."""
-    order = np.argsort(-lens, kind="stable")
+def build_qsl(count, seed):
+    """QSL: per-utterance features [T_i, 240] ~ N(0,1) (normalised log-mel stand-in), stored
+    ragged in HBM (LoadSamplesToRam), lengths dev-clean-shaped."""
+    lens = synthetic.devclean_lengths(count, seed=seed)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    feats = torch.randn((int(lens.sum()), 240), device="cuda", generator=g)
+    return dict(lens=lens, offs=offs, feats=feats)
+
+
+def make_batches(qsl, query, batch):
+    """The Offline query (sample i -> QSL index i % count, as LoadGen repeats the QSL),
+    sorted longest-first and split into batches; each batch assembled in HBM as
+    [T_max, n_pad, 256] fp32, zero padded (AssembleSamples, rnnt_qsl.cpp:150-188)."""
+    count = len(qsl["lens"])
+    ids = np.arange(query) % count
+    ids = ids[np.argsort(-qsl["lens"][ids], kind="stable")]
     out = []
-    for b, i in enumerate(range(0, len(order), batch)):
-        idx = order[i:i + batch]
-        bl = lens[idx].astype(np.int32)
+    for i in range(0, len(ids), batch):
+        idx = ids[i:i + batch]
+        bl = qsl["lens"][idx].astype(np.int32)
         n = len(idx)
         n_pad = pad_batch(n)
         lp = np.zeros(n_pad, np.int32)
         lp[:n] = bl
         T = int(bl.max())
-        x = synthetic.make_features(T, n_pad, seed=seed * 7919 + b, lens=lp)
-        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, lens=torch.from_numpy(lp).cuda(),
-                        x=torch.from_numpy(x).cuda(), x_host=x))
+        t = torch.arange(T, device="cuda")[:, None]
+        ln = torch.from_numpy(bl).cuda()[None, :]
+        rows = torch.from_numpy(qsl["offs"][idx]).cuda()[None, :] + t
+        valid = t < ln
+        x = torch.zeros((T, n_pad, 256), dtype=torch.float32, device="cuda")
+        x[:, :n, :240] = qsl["feats"][torch.where(valid, rows, 0)] * valid[..., None]
+        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, lens=torch.from_numpy(lp).cuda(), x=x))
+    torch.cuda.synchronize()
     return out
 
 
@@ -128,9 +152,10 @@ def main():
     args = parse()
     rank, local, world = dist_setup()
     pm, _ = weights.build_model()
-    lens = synthetic.devclean_lengths(args.qsl, seed=4 + 1000 * rank)
-    engine = Engine(pm, device=local, max_batch=args.batch, max_frames=500)
-    batches = make_batches(lens, args.batch, seed=4 + 1000 * rank)
+    qsl = build_qsl(args.qsl, seed=4 + 1000 * rank)
+    lens = qsl["lens"]
+    engine = Engine(pm, device=local, max_batch=min(args.batch, args.query), max_frames=500)
+    batches = make_batches(qsl, args.query, args.batch)
 
     for _ in range(args.warmup):
         run_step(engine, batches)
@@ -149,11 +174,12 @@ def main():
     st = engine.stats(reset=True)
     elapsed_max = all_max(elapsed, world)
 
-    utts = args.qsl * world * args.steps
+    utts = args.query * world * args.steps
     value = utts / elapsed_max
     emitted = int(sum(int(l.sum()) for l in lens_out))
-    enc_frames = int(sum(encoder_frames(l) for l in lens))
-    enc_ops = float(sum(encoder_ops(int(l)) for l in lens)) * args.steps  # SURVEY 8d E(T), valid frames
+    qlens = np.concatenate([b["lens_host"] for b in batches])
+    enc_frames = int(sum(encoder_frames(l) for l in qlens))
+    enc_ops = float(sum(encoder_ops(int(l)) for l in qlens)) * args.steps  # SURVEY 8d E(T), valid frames
     achieved = enc_ops / (st["encode_ms"] * 1e-3) / 1e12 if st["encode_ms"] > 0 else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -175,11 +201,12 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
         "data": "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)",
-        "config": {"workload": "MLPerf Offline, LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
-                   "qsl_per_gpu": args.qsl, "batch_size": args.batch, "encoder": "int8 (lstm_amx_int8)",
+        "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
+                   "qsl_per_gpu": args.qsl, "query_samples_per_gpu": args.query, "batch_size": args.batch,
+                   "encoder": "int8 (lstm_amx_int8)",
                    "decoder": "bf16 prediction/joint, fp32 accumulate, greedy (device loop)",
                    "parallelism": f"dp{world} (one process per GPU, sharded queries)",
-                   "encoder_frames_per_gpu": enc_frames, "emitted_symbols_per_gpu": emitted},
+                   "encoder_frames_per_query": enc_frames, "emitted_symbols_per_query": emitted},
         "roofline": roofline,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

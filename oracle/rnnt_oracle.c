@@ -55,6 +55,48 @@ float oracle_tanh(float x) {
   return copysignf(t, x);
 }
 
+/* ---------------------------------------------------------------- int8 LSTM cell ----
+ * The quantised encoder's cell (quant_lstm.py:162-183 semantics), in the division-light
+ * form the HIP epilogue evaluates (rnnt-inference_amd/csrc/rnnt_device.hpp enc_cell):
+ *   e2(z) = 2^z: z clamped to [-40, 40], n = rint(z), degree-5 minimax polynomial in
+ *           z - n (max rel. error 2.2e-7), scaled by ldexp (exact);
+ *   sigma(x) = 1 / (1 + e2(-x log2 e)), tanh(x) = (1 - e2(-2x log2 e)) / (1 + e2(-2x log2 e));
+ *   c = f c_prev + i g = (c_prev (1+ei)(1+eg) + (1-eg)(1+ef)) / ((1+ef)(1+ei)(1+eg))
+ *   h = o tanh(c)      = (1 - ec) / ((1+eo)(1+ec))
+ * i.e. two IEEE divisions per cell instead of five.  The clamp is exact in fp32 (sigma and
+ * tanh round to +-1 / 0 long before it) and keeps every product below 2^121. */
+float oracle_e2(float z) {
+  z = fminf(fmaxf(z, -40.0f), 40.0f);
+  const float n = rintf(z);
+  const float f = z - n;
+  float p = 1.327606732957065e-3f;
+  p = fmaf(p, f, 9.675402194261551e-3f);
+  p = fmaf(p, f, 5.550713464617729e-2f);
+  p = fmaf(p, f, 2.4022123217582703e-1f);
+  p = fmaf(p, f, 6.931469440460205e-1f);
+  p = fmaf(p, f, 1.0000001192092896f);
+  return ldexpf(p, (int)n);
+}
+
+#define NL2E (-1.44269504088896341f)
+#define NL2E2 (-2.88539008177792682f)
+
+void oracle_enc_cell(const int32_t acc[4], const float bqr[4], float rb, float c_prev,
+                     float* c_out, float* h_out) {
+  const float pi = fmaf((float)acc[0], rb, bqr[0]);
+  const float pf = fmaf((float)acc[1], rb, bqr[1]);
+  const float pg = fmaf((float)acc[2], rb, bqr[2]);
+  const float po = fmaf((float)acc[3], rb, bqr[3]);
+  const float ei = oracle_e2(pi * NL2E), ef = oracle_e2(pf * NL2E);
+  const float eg = oracle_e2(pg * NL2E2), eo = oracle_e2(po * NL2E);
+  const float A = 1.0f + ef, B = (1.0f + ei) * (1.0f + eg);
+  const float num = fmaf(c_prev, B, (1.0f - eg) * A);
+  const float c = num / (A * B);
+  const float ec = oracle_e2(c * NL2E2);
+  *c_out = c;
+  *h_out = (1.0f - ec) / ((1.0f + eo) * (1.0f + ec));
+}
+
 /* ---------------------------------------------------------------- conversions ---- */
 uint16_t oracle_f2h(float f) {
   const uint32_t x = f2bits(f), sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
@@ -151,16 +193,12 @@ void oracle_lstm_i8_layer(int T, int N, int I, int H, const int8_t* x, const int
       const int32_t* a = acc + (size_t)n * 4 * H;
       uint16_t* cv = c + (size_t)n * H;
       for (int j = 0; j < H; ++j) {
-        const float pi = ((float)a[j] + bq[j]) * rb;
-        const float pf = ((float)a[H + j] + bq[H + j]) * rb;
-        const float pg = ((float)a[2 * H + j] + bq[2 * H + j]) * rb;
-        const float po = ((float)a[3 * H + j] + bq[3 * H + j]) * rb;
-        const float ig = oracle_sigmoid(pi), fg = oracle_sigmoid(pf);
-        const float gg = oracle_tanh(pg), og = oracle_sigmoid(po);
-        const float cp = oracle_h2f(cv[j]);
-        const float cn = fg * cp + ig * gg;
+        /* bias pre-scaled once: bqr = bq * rb (fp32), pre = fma(acc, rb, bqr) */
+        const int32_t ag[4] = {a[j], a[H + j], a[2 * H + j], a[3 * H + j]};
+        const float br[4] = {bq[j] * rb, bq[H + j] * rb, bq[2 * H + j] * rb, bq[3 * H + j] * rb};
+        float cn, hh;
+        oracle_enc_cell(ag, br, rb, oracle_h2f(cv[j]), &cn, &hh);
         cv[j] = oracle_f2h(cn);
-        const float hh = og * oracle_tanh(cn);
         hn[(size_t)n * H + j] = oracle_q8(hh * in_s);
         const size_t o = ((size_t)t * N + n) * H + j;
         if (skip_quant_y)

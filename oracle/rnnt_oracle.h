@@ -25,6 +25,9 @@ extern "C" {
 float oracle_exp(float x);
 float oracle_sigmoid(float x);
 float oracle_tanh(float x);
+float oracle_e2(float z);         /* 2^z of the int8 cell (see rnnt_oracle.c) */
+void oracle_enc_cell(const int32_t acc[4], const float bqr[4], float rb, float c_prev,
+                     float* c_out, float* h_out);
 uint16_t oracle_f2h(float x);      /* f32 -> f16 bits, round-half-even */
 float oracle_h2f(uint16_t h);
 uint16_t oracle_f2bf(float x);     /* f32 -> bf16 bits, round-half-even */

@@ -30,17 +30,29 @@ __global__ void __launch_bounds__(256) quantize_kernel(const float4* __restrict_
 }
 
 // ---------------------------------------------------------------- LSTM step
-constexpr int BM = 128;  // gate rows per workgroup (32 units x 4 gates)
-constexpr int BN = 128;  // batch rows per workgroup
-constexpr int BK = 64;   // k bytes per stage (one 16x16x64 MFMA depth)
-constexpr int NSTAGE = 3;                       // LDS ring depth (2 stages in flight)
-constexpr int STAGE_BYTES = (BM + BN) * BK;     // 16 KiB: A image then B image
-constexpr int GLDS_PER_STAGE = 4;               // per wave: 2 x 1 KiB pieces of A, 2 of B
+// Workgroup tile: 256 packed gate rows (64 units) x 256 batch rows, K swept in 64-byte
+// steps.  8 waves as 4 (gate) x 2 (batch); each wave owns 64 gate rows x 128 batch rows =
+// 4 x 8 MFMA 16x16x64 tiles.  The 256x256 tile halves the L2->LDS bytes per MFMA of a 128x128
+// tile: staging through the per-CU load path (~70 GB/s/CU from L2), not the MFMA, bounds this
+// GEMM (DESIGN.md "Encoder kernel").
+constexpr int BM = 256;
+constexpr int BN = 256;
+constexpr int BK = 64;
+constexpr int NWAVE = 8;
+#ifndef RNNT_NSTAGE
+#define RNNT_NSTAGE 4
+#endif
+constexpr int NSTAGE = RNNT_NSTAGE;          // LDS ring depth: NSTAGE-1 stages in flight
+constexpr int A_BYTES = BM * BK;             // 16 KiB
+constexpr int STAGE_BYTES = (BM + BN) * BK;  // 32 KiB
+constexpr int GLDS_PER_STAGE = 4;            // per wave: 2 x 1 KiB pieces of A, 2 of B
+static_assert(BM / 16 == 2 * NWAVE && BN / 16 == 2 * NWAVE, "two 16-row pieces per wave per operand");
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(1))) void glb_void;
 
-// LDS image of a [128][64 B] tile: 16-byte column c of row r is stored at column
+// LDS image of a [rows][64 B] tile: 16-byte column c of row r is stored at column
 // c ^ h[(r >> 2) & 3] with h = {0, 2, 3, 1}.  A fragment read (lane l: row l&15, column l>>4)
 // is a ds_read_b128 whose four 16-lane groups each touch rows {0-3,12-15} at one column and
 // rows 4-11 at the next; with this h every group lands on 16 distinct 16-byte bank slots.
@@ -49,133 +61,129 @@ __device__ __forceinline__ int swz(int row, int col16) { return row * BK + ((col
 
 // Retire this wave's LDS-DMA down to N outstanding, drain LDS ops, then barrier: after it,
 // every wave's DMA of the retired stage has landed (each wave waited for its own) and every
-// wave's reads of the previous stage are done.  One asm statement so the "memory" clobber
-// orders it against the compiler's LDS accesses on both sides.
+// wave's reads of the stage about to be refilled are done.  One asm statement, so its
+// "memory" clobber orders it against the compiler's LDS accesses on both sides.
 template <int N>
 __device__ __forceinline__ void stage_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-__device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int tile, int8_t* smem) {
+__device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int m0 = blockIdx.x * BM;  // packed gate row base
-  const int n0 = tile * BN;        // batch row base
+  const int wm = wave & 3, wn = wave >> 2;
+  const int m0 = mt * BM;  // packed gate row base
+  const int n0 = nt * BN;  // batch row base
   const int K = a.I + H;
   const int nK = K / BK;
 
   // ---- epilogue operands, prefetched so their latency hides under the main loop
   const int q = lane >> 4, col = lane & 15;
   const int u0 = (m0 >> 2) + wm * 16 + q * 4;  // this lane's 4 consecutive units
-  int nrow[4];
-  uint2 cpre[4];
-  int lpre[4];
+  const int nb = n0 + wn * 128 + col;          // batch row of j = 0 (row j: nb + 16 j)
+  uint2 cpre[8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    nrow[j] = n0 + wn * 64 + j * 16 + col;
-    cpre[j] = *(const uint2*)(a.c + (size_t)nrow[j] * H + u0);
-    lpre[j] = a.lens ? a.lens[nrow[j]] : 0;
-  }
-  float4 bq[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) bq[i] = *(const float4*)(a.bq + m0 + wm * 64 + i * 16 + q * 4);
-
+  for (int j = 0; j < 8; ++j) cpre[j] = *(const uint2*)(a.c + (size_t)(nb + 16 * j) * H + u0);
   // ---- LDS-DMA staging: wave w moves pieces 2w, 2w+1 (16 rows x 64 B each) of A and of B;
-  // lane l of a piece lands at LDS slot 64p + l = row*4 + (col16 ^ h(row)), so it fetches
-  // row 16p + (l>>2), column (l&3) ^ h (h depends on l>>4 only).
-  const int hx = (0x1320 >> ((lane >> 4) * 4)) & 3;  // h(row): (row>>2)&3 == lane>>4
+  // lane l of piece p lands at LDS slot 64p + l = row*4 + (col16 ^ h(row)), so it fetches
+  // row 16p + (l>>2), 16-byte column (l&3) ^ h, where h(row) depends on l>>4 only.
+  const int hx = (0x1320 >> ((lane >> 4) * 4)) & 3;
   const int gcol = ((lane & 3) ^ hx) * 16;
-  const int ra = wave * 32 + (lane >> 2), rb = ra + 16;  // rows of this wave's two pieces
-  const int8_t* wa0 = a.W + (size_t)(m0 + ra) * K + gcol;
-  const int8_t* wa1 = a.W + (size_t)(m0 + rb) * K + gcol;
-  const int8_t* xb0 = a.x + (size_t)(n0 + ra) * a.I + gcol;
-  const int8_t* xb1 = a.x + (size_t)(n0 + rb) * a.I + gcol;
-  const int8_t* hb0 = a.h_in + (size_t)(n0 + ra) * H + gcol - a.I;
-  const int8_t* hb1 = a.h_in + (size_t)(n0 + rb) * H + gcol - a.I;
-  lds_void* lds_base = (lds_void*)smem;
+  const int ra = wave * 32 + (lane >> 2), rb = ra + 16;
+#ifdef RNNT_DEV_SAME_TILE  // development ablation: every workgroup stages tile (0, 0) (L2-resident)
+  const int lm0 = 0, ln0 = 0;
+#else
+  const int lm0 = m0, ln0 = n0;
+#endif
+  const int8_t* wa0 = a.W + (size_t)(lm0 + ra) * K + gcol;
+  const int8_t* wa1 = a.W + (size_t)(lm0 + rb) * K + gcol;
+  const int8_t* xb0 = a.x + (size_t)(ln0 + ra) * a.I + gcol;
+  const int8_t* xb1 = a.x + (size_t)(ln0 + rb) * a.I + gcol;
+  const int8_t* hb0 = a.h_in + (size_t)(ln0 + ra) * H + gcol - a.I;
+  const int8_t* hb1 = a.h_in + (size_t)(ln0 + rb) * H + gcol - a.I;
+  lds_char* lds = (lds_char*)(lds_void*)smem;
+  const int pa = wave * 2 * 1024;
 
   auto issue = [&](int ks) __attribute__((always_inline)) {
+#ifdef RNNT_DEV_NO_LOAD  // development ablation: no staging (MFMA on stale LDS)
+    return;
+#endif
     const int k = ks * BK;
-    char __attribute__((address_space(3)))* st = (char __attribute__((address_space(3)))*)lds_base + (ks % NSTAGE) * STAGE_BYTES;
-    __builtin_amdgcn_global_load_lds((glb_void*)(wa0 + k), (lds_void*)(st + (wave * 2) * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((glb_void*)(wa1 + k), (lds_void*)(st + (wave * 2 + 1) * 1024), 16, 0, 0);
+    lds_char* st = lds + (ks % NSTAGE) * STAGE_BYTES + pa;
+    __builtin_amdgcn_global_load_lds((glb_void*)(wa0 + k), (lds_void*)st, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)(wa1 + k), (lds_void*)(st + 1024), 16, 0, 0);
     const int8_t* b0 = k < a.I ? xb0 + k : hb0 + k;
     const int8_t* b1 = k < a.I ? xb1 + k : hb1 + k;
-    __builtin_amdgcn_global_load_lds((glb_void*)b0, (lds_void*)(st + BM * BK + (wave * 2) * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((glb_void*)b1, (lds_void*)(st + BM * BK + (wave * 2 + 1) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)b0, (lds_void*)(st + A_BYTES), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)b1, (lds_void*)(st + A_BYTES + 1024), 16, 0, 0);
   };
 
-  v4i acc[4][4];
+  v4i acc[4][8];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+    for (int j = 0; j < 8; ++j) acc[i][j] = v4i{0, 0, 0, 0};
 
-  // fragment read offsets (rows wm*64 + i*16 + (lane&15), 16-byte column lane>>4)
-  int fa_off[4], fb_off[4];
+  // fragment reads: A rows wm*64 + i*16 + (lane&15), B rows wn*128 + j*16 + (lane&15), 16-byte
+  // column lane>>4; +16 rows is +1 KiB in the image (the swizzle repeats every 16 rows)
+  const int fa = swz(wm * 64 + col, q), fb = A_BYTES + swz(wn * 128 + col, q);
+
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    fa_off[i] = swz(wm * 64 + i * 16 + col, q);
-    fb_off[i] = BM * BK + swz(wn * 64 + i * 16 + col, q);
-  }
-
-  issue(0);
-  issue(1);  // nK >= 20 for every layer
+  for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
   for (int ks = 0; ks < nK; ++ks) {
-    if (ks + 1 < nK) stage_barrier<GLDS_PER_STAGE>();
+    // stages issued after ks that may stay in flight: min(NSTAGE - 2, nK - 1 - ks)
+    const int rem = nK - 1 - ks;
+    if (NSTAGE >= 5 && rem >= 3) stage_barrier<3 * GLDS_PER_STAGE>();
+    else if (NSTAGE >= 4 && rem >= 2) stage_barrier<2 * GLDS_PER_STAGE>();
+    else if (rem >= 1) stage_barrier<GLDS_PER_STAGE>();
     else stage_barrier<0>();
-    if (ks + 2 < nK) issue(ks + 2);
+    if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
     const int8_t* st = smem + (ks % NSTAGE) * STAGE_BYTES;
-    v4i fa[4], fb[4];
+    v4i fra[4], frb[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = *(const v4i*)(st + fa_off[i]);
+    for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa + i * 1024);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = *(const v4i*)(st + fb_off[j]);
+    for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb + j * 1024);
 #ifdef RNNT_DEV_NO_MFMA  // development ablation: staging + LDS reads only
 #pragma unroll
-    for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fa[i]), "v"(fb[i]));
+    for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fra[i]), "v"(frb[i]), "v"(frb[i + 4]));
 #else
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
 #endif
   }
 #ifdef RNNT_DEV_NO_EPI  // development ablation: main loop only
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-  asm volatile("" ::"v"(cpre[0].x), "v"(cpre[3].y), "v"(bq[0].x), "v"(bq[3].w), "v"(lpre[0]));
+    for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(acc[i][j]));
+  asm volatile("" ::"v"(cpre[0].x), "v"(cpre[7].y));
   return;
 #endif
 
-  // ---- fused LSTM cell epilogue (quant_lstm.py:162-183 semantics; see oracle_lstm_i8_layer)
+  // ---- fused LSTM cell epilogue (quant_lstm.py:162-183 semantics; oracle_enc_cell)
   const float rbs = a.rb, ins = a.in_s, outs = a.out_s;
+  float4 bq[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = nrow[j];
-    const uint16_t cin[4] = {(uint16_t)(cpre[j].x & 0xffff), (uint16_t)(cpre[j].x >> 16),
-                             (uint16_t)(cpre[j].y & 0xffff), (uint16_t)(cpre[j].y >> 16)};
-    uint16_t cout[4];
-    uint32_t hq = 0, yq = 0;
+  for (int i = 0; i < 4; ++i) bq[i] = *(const float4*)(a.bq + m0 + wm * 64 + i * 16 + q * 4);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = nb + 16 * j;
+    const float cin[4] = {h2f((uint16_t)(cpre[j].x & 0xffff)), h2f((uint16_t)(cpre[j].x >> 16)),
+                          h2f((uint16_t)(cpre[j].y & 0xffff)), h2f((uint16_t)(cpre[j].y >> 16))};
+    uint32_t cw[2] = {0u, 0u}, hq = 0, yq = 0;
     float hv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float pi = ((float)acc[i][j][0] + bq[i].x) * rbs;
-      const float pf = ((float)acc[i][j][1] + bq[i].y) * rbs;
-      const float pg = ((float)acc[i][j][2] + bq[i].z) * rbs;
-      const float po = ((float)acc[i][j][3] + bq[i].w) * rbs;
-      const float ig = det_sigmoid(pi), fg = det_sigmoid(pf), gg = det_tanh(pg), og = det_sigmoid(po);
-      const float cn = fg * h2f(cin[i]) + ig * gg;
-      cout[i] = f2h(cn);
-      const float hh = og * det_tanh(cn);
+      float cn, hh;
+      enc_cell(acc[i][j], bq[i], rbs, cin[i], cn, hh);
+      cw[i >> 1] |= (uint32_t)f2h(cn) << (16 * (i & 1));
       hv[i] = hh;
       hq |= (uint32_t)(uint8_t)q8(hh * ins) << (8 * i);
       yq |= (uint32_t)(uint8_t)q8(hh * outs) << (8 * i);
     }
-    *(uint2*)(a.c + (size_t)n * H + u0) =
-        uint2{(uint32_t)cout[0] | ((uint32_t)cout[1] << 16), (uint32_t)cout[2] | ((uint32_t)cout[3] << 16)};
+    *(uint2*)(a.c + (size_t)n * H + u0) = uint2{cw[0], cw[1]};
     *(uint32_t*)(a.h_out + (size_t)n * H + u0) = hq;
     if (a.mode == ENC_OUT_I8) {
       *(uint32_t*)(a.y8 + (size_t)n * H + u0) = yq;
@@ -183,7 +191,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int tile, int
       // StackTime (modeling_rnnt.py:314-324): frame t -> stacked frame t/2, half t%2;
       // frames t >= x_lens[n] are zeroed; the odd-T pad frame is zero too.
       int8_t* dst = a.y8 + (size_t)n * (2 * H) + u0;
-      *(uint32_t*)(dst + a.half * H) = (a.t < lpre[j]) ? yq : 0u;
+      *(uint32_t*)(dst + a.half * H) = (a.t < a.lens[n]) ? yq : 0u;
       if (a.zero_next) *(uint32_t*)(dst + H) = 0u;
     } else {
       if (a.y32) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1], hv[2], hv[3]};
@@ -193,22 +201,30 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int tile, int
   }
 }
 
-__global__ void __launch_bounds__(256, 2) lstm_i8_tick_kernel(EncTickArgs args) {
-  __shared__ __attribute__((aligned(16))) int8_t smem[NSTAGE * STAGE_BYTES];
-  const int y = blockIdx.y;
-  // wave-uniform job lookup; each case inlines the body with a constant job index so the
-  // job's arguments stay in the kernarg segment (scalar loads, no private copy)
-  if (y < args.tile_start[1]) {
-    lstm_i8_step(args.job[0], y, smem);
-  } else if (y < args.tile_start[2]) {
-    lstm_i8_step(args.job[1], y - args.tile_start[1], smem);
-  } else if (y < args.tile_start[3]) {
-    lstm_i8_step(args.job[2], y - args.tile_start[2], smem);
-  } else if (y < args.tile_start[4]) {
-    lstm_i8_step(args.job[3], y - args.tile_start[3], smem);
-  } else {
-    lstm_i8_step(args.job[4], y - args.tile_start[4], smem);
+// One launch = one wavefront tick: up to 5 independent layer-steps (jobs, longest K first).
+// XCD-aware tile order: workgroup id -> XCD id % 8 (round-robin dispatch).  XCD x takes gate
+// tiles 4(x&3)..4(x&3)+3 and the (x>>2)-th half of each job's active batch tiles, so the 32
+// workgroups resident on an XCD share 4 weight tiles and ~8 activation tiles through its L2
+// (weights fetched from HBM/MALL 2x, activations 4x per tick, instead of 1x / 8x).
+__global__ void __launch_bounds__(512, 1) lstm_i8_tick_kernel(EncTickArgs args) {
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  const int xcd = blockIdx.x & 7, gg = xcd & 3, bg = xcd >> 2;
+  int k = blockIdx.x >> 3, jsel = -1, mt = 0, nt = 0;
+  for (int j = 0; j < args.njobs; ++j) {
+    const int nbt = args.nbt[j], h0 = (nbt + 1) >> 1;
+    const int cnt = 4 * (bg ? nbt - h0 : h0);
+    if (k < cnt) {
+      jsel = j;
+      mt = gg * 4 + (k & 3);
+      nt = (bg ? h0 : 0) + (k >> 2);
+      break;
+    }
+    k -= cnt;
   }
+  if (jsel < 0) return;
+  // wave-uniform runtime index into the kernarg segment: the job's fields stay scalar loads
+  lstm_i8_step(args.job[__builtin_amdgcn_readfirstlane(jsel)], __builtin_amdgcn_readfirstlane(mt),
+               __builtin_amdgcn_readfirstlane(nt), smem);
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -222,9 +238,17 @@ int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStrea
 }
 
 int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
-  const int tiles = a.tile_start[a.njobs];
-  if (tiles <= 0) return 0;
-  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(G4 / BM, tiles), dim3(256), 0, st, a);
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)lstm_i8_tick_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            NSTAGE * STAGE_BYTES) != hipSuccess)
+      return -1;
+    attr = true;
+  }
+  int per_xcd = 0;  // the batch-half-0 XCDs carry the larger half
+  for (int j = 0; j < a.njobs; ++j) per_xcd += 4 * ((a.nbt[j] + 1) >> 1);
+  if (per_xcd <= 0) return 0;
+  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(8 * per_xcd), dim3(NWAVE * 64), NSTAGE * STAGE_BYTES, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -5,22 +5,22 @@
 
 namespace rnnt {
 
-constexpr int ENC_BATCH_TILE = 128;  // batch rows per encoder workgroup (buffers padded to it)
+constexpr int ENC_BATCH_TILE = 256;  // batch rows per encoder workgroup (buffers padded to it)
 
-// Packed row of (unit u, gate g) in the encoder weight image.  A 128-row workgroup tile
-// holds 32 units; inside it, wave half wm = (u>>4)&1, MFMA tile i = u&3, lane group
-// q = (u>>2)&3 and accumulator register g: row = 128*(u>>5) + 64*wm + 16*i + 4*q + g.  One
-// lane then owns the four gates of units u0..u0+3 (u0 = 32*(u>>5) + 16*wm + 4*q) for its
-// batch row, so the cell epilogue reads/writes 4 consecutive units per access.
+// Packed row of (unit u, gate g) in the encoder weight image.  Each wave's 64 gate rows hold
+// 16 units: MFMA tile i = u&3, lane group q = (u>>2)&3 and accumulator register g, i.e.
+// row = 64*(u>>4) + 16*i + 4*q + g.  One lane then owns the four gates of units u0..u0+3
+// (u0 = 16*(u>>4) + 4*q) for its batch row, so the cell epilogue reads/writes 4 consecutive
+// units per access.
 __host__ __device__ __forceinline__ int enc_packed_row(int u, int g) {
-  return ((u >> 5) << 7) + (((u >> 4) & 1) << 6) + ((u & 3) << 4) + (((u >> 2) & 3) << 2) + g;
+  return ((u >> 4) << 6) + ((u & 3) << 4) + (((u >> 2) & 3) << 2) + g;
 }
 
 enum EncOutMode { ENC_OUT_I8 = 0, ENC_OUT_STACKED = 1, ENC_OUT_FINAL = 2 };
 
 struct EncStepArgs {
   const int8_t* W;     // packed [4096][I+1024], gate-interleaved rows
-  const float* bq;     // packed [4096]
+  const float* bq;     // packed [4096], pre-scaled by rb (bqr = bq * rb)
   const int8_t* x;     // this frame's input rows: [Npad][I]
   const int8_t* h_in;  // [Npad][1024] h_{t-1} (quantised with in_s)
   int8_t* h_out;       // [Npad][1024] h_t
@@ -38,11 +38,11 @@ struct EncStepArgs {
 };
 
 // One launch runs up to ENC_MAX_JOBS independent layer-steps (the wavefront schedule of
-// engine.hip: layer l at its own frame); grid.y enumerates (job, batch tile) pairs.
+// engine.hip: layer l at its own frame), each over its leading nbt active batch tiles.
 constexpr int ENC_MAX_JOBS = 5;
 struct EncTickArgs {
   EncStepArgs job[ENC_MAX_JOBS];
-  int tile_start[ENC_MAX_JOBS + 1];  // prefix sums of each job's active batch tiles
+  int nbt[ENC_MAX_JOBS];  // active 256-row batch tiles per job
   int njobs;
 };
 

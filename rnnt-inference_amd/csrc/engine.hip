@@ -100,7 +100,7 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
       for (int u = 0; u < H; ++u) {
         const int pr = enc_packed_row(u, g);
         memcpy(&w[(size_t)pr * K], m->enc_w[l] + (size_t)(g * H + u) * K, K);
-        b[pr] = m->enc_bq[l][g * H + u];
+        b[pr] = m->enc_bq[l][g * H + u] * m->enc_rb[l];  // bqr (fp32 multiply, as oracle_lstm_i8_layer)
       }
     int r = upload(e, &e->enc_w[l], w);
     if (!r) r = upload(e, &e->enc_bq[l], b);
@@ -247,7 +247,7 @@ __global__ void stack_time_kernel(const int8_t* x, const int32_t* lens, int T, i
 // default stream is; the engine's own stream is only used by rnnt_engine_create.
 static hipStream_t pick(rnnt_engine*, void* s) { return (hipStream_t)s; }
 
-// number of leading 128-row tiles that hold a row with len > thr
+// number of leading 256-row tiles that hold a row with len > thr
 static int active_tiles(const std::vector<int>& tile_max, int thr) {
   int last = -1;
   for (int i = 0; i < (int)tile_max.size(); ++i)
@@ -291,14 +291,19 @@ struct TickBuilder {
   int n = 0;
   void add(const EncStepArgs& a, int tiles) {
     if (tiles <= 0) return;
-    args.job[n] = a;
-    args.tile_start[n + 1] = args.tile_start[n] + tiles;
-    ++n;
+    // keep jobs ordered by K descending (longest workgroups dispatched first)
+    int p = n++;
+    while (p > 0 && args.job[p - 1].I < a.I) {
+      args.job[p] = args.job[p - 1];
+      args.nbt[p] = args.nbt[p - 1];
+      --p;
+    }
+    args.job[p] = a;
+    args.nbt[p] = tiles;
   }
   int launch(rnnt_engine* e, hipStream_t st) {
     if (n == 0) return 0;
     args.njobs = n;
-    for (int j = n + 1; j <= ENC_MAX_JOBS; ++j) args.tile_start[j] = args.tile_start[n];
     e->step_launches++;
     return launch_lstm_i8_tick(args, st) ? fail(RNNT_EDEVICE, "lstm tick launch failed") : 0;
   }
@@ -319,7 +324,7 @@ static int run_layer(rnnt_engine* e, int l, int T, int n_pad, const int8_t* x, i
 static int check_batch(rnnt_engine* e, int T, int n, int n_pad) {
   if (T <= 0 || T > e->opts.max_frames) return fail(RNNT_EINVAL, "T out of range");
   if (n <= 0 || n_pad < n || n_pad % ENC_BATCH_TILE || n_pad > e->np_max)
-    return fail(RNNT_EINVAL, "n / n_pad out of range (n_pad must be a multiple of 128 <= max_batch)");
+    return fail(RNNT_EINVAL, "n / n_pad out of range (n_pad must be a multiple of 256 <= max_batch)");
   return 0;
 }
 

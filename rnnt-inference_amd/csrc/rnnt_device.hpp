@@ -54,6 +54,40 @@ __device__ __forceinline__ float det_tanh(float x) {
   return __builtin_copysignf(t, x);
 }
 
+// ---- int8 encoder cell (bit-identical to oracle_e2 / oracle_enc_cell; the division-light
+// form is documented there): 2^z with z clamped to [-40, 40], degree-5 minimax polynomial
+// and an exact ldexp; two IEEE divisions per cell.
+__device__ __forceinline__ float enc_e2(float z) {
+  z = __builtin_fminf(__builtin_fmaxf(z, -40.0f), 40.0f);
+  const float n = __builtin_rintf(z);
+  const float f = z - n;
+  float p = 1.327606732957065e-3f;
+  p = __builtin_fmaf(p, f, 9.675402194261551e-3f);
+  p = __builtin_fmaf(p, f, 5.550713464617729e-2f);
+  p = __builtin_fmaf(p, f, 2.4022123217582703e-1f);
+  p = __builtin_fmaf(p, f, 6.931469440460205e-1f);
+  p = __builtin_fmaf(p, f, 1.0000001192092896f);
+  return __builtin_ldexpf(p, (int)n);
+}
+constexpr float ENC_NL2E = -1.44269504088896341f;
+constexpr float ENC_NL2E2 = -2.88539008177792682f;
+// acc: int32 gate sums (i, f, g, o); bqr: bias pre-scaled by rb; returns c (fp32) and h.
+__device__ __forceinline__ void enc_cell(const v4i acc, const float4 bqr, float rb, float c_prev, float& c_out,
+                                         float& h_out) {
+  const float pi = __builtin_fmaf((float)acc[0], rb, bqr.x);
+  const float pf = __builtin_fmaf((float)acc[1], rb, bqr.y);
+  const float pg = __builtin_fmaf((float)acc[2], rb, bqr.z);
+  const float po = __builtin_fmaf((float)acc[3], rb, bqr.w);
+  const float ei = enc_e2(pi * ENC_NL2E), ef = enc_e2(pf * ENC_NL2E);
+  const float eg = enc_e2(pg * ENC_NL2E2), eo = enc_e2(po * ENC_NL2E);
+  const float A = 1.0f + ef, B = (1.0f + ei) * (1.0f + eg);
+  const float num = __builtin_fmaf(c_prev, B, (1.0f - eg) * A);
+  const float c = num / (A * B);
+  const float ec = enc_e2(c * ENC_NL2E2);
+  c_out = c;
+  h_out = (1.0f - ec) / ((1.0f + eo) * (1.0f + ec));
+}
+
 // f32 -> f16 round-half-even and f16 -> f32 on the hardware converters (v_cvt_f16_f32 /
 // v_cvt_f32_f16, default RNE, f16 denormals preserved): bit-identical to oracle_f2h/h2f.
 __device__ __forceinline__ uint16_t f2h(float f) {

@@ -14,7 +14,7 @@ from . import _lib
 from .config import RNNTParam as R
 from .weights import PreparedModel, f32_to_bf16_bits
 
-BATCH_TILE = 128
+BATCH_TILE = 256
 
 
 def pad_batch(n):

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 from rnnt_amd import synthetic, weights
+from rnnt_amd.engine import pad_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -36,7 +37,7 @@ def _valid(f, lens):
 
 
 def test_pre_rnn_layers_bitexact(engine, model, oracle):
-    T, n, n_pad = 7, 5, 128
+    T, n, n_pad = 7, 5, 256
     rng = np.random.default_rng(5)
     x = synthetic.make_features(T, n_pad, seed=3)
     hx = rng.integers(-128, 128, (2, n_pad, 1024)).astype(np.int8)
@@ -56,7 +57,7 @@ def test_pre_rnn_layers_bitexact(engine, model, oracle):
 
 
 def test_post_rnn_layers_bitexact(engine, model, oracle):
-    T, n_pad = 5, 128
+    T, n_pad = 5, 256
     rng = np.random.default_rng(6)
     x = rng.integers(-128, 128, (T, n_pad, 2048)).astype(np.int8)
     hx = np.zeros((3, n_pad, 1024), np.int8)
@@ -75,7 +76,7 @@ def test_post_rnn_layers_bitexact(engine, model, oracle):
 
 
 def test_stack_time_op(engine, oracle):
-    T, n_pad = 9, 128
+    T, n_pad = 9, 256
     x = np.random.default_rng(7).integers(-128, 128, (T, n_pad, 1024)).astype(np.int8)
     lens = np.zeros(n_pad, np.int32)
     lens[:4] = [9, 4, 1, 0]
@@ -87,7 +88,7 @@ def test_stack_time_op(engine, oracle):
 
 def _run(engine, model, oracle, T, lens, seed):
     n = len(lens)
-    n_pad = (n + 127) // 128 * 128
+    n_pad = pad_batch(n)
     lens_pad = np.zeros(n_pad, np.int32)
     lens_pad[:n] = lens
     x = synthetic.make_features(T, n_pad, seed=seed, lens=lens_pad)

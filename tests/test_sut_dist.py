@@ -28,7 +28,7 @@ def test_assemble_layout():
     lengths = np.array([3, 7, 2], np.int32)
     qsl = _qsl(lengths)
     x, lens = qsl.assemble([1, 0, 2])
-    assert x.shape == (7, 128, 256) and lens.shape == (128,)
+    assert x.shape == (7, 256, 256) and lens.shape == (256,)
     assert list(lens[:4]) == [7, 3, 2, 0]
     assert np.all(x[:7, 0, :240] == 1) and np.all(x[:3, 1, :240] == 0) and np.all(x[:2, 2, :240] == 2)
     assert np.all(x[3:, 1] == 0) and np.all(x[:, :, 240:] == 0) and np.all(x[:, 3:] == 0)

@@ -12,6 +12,14 @@ for v in "$@"; do
     noepi) build noepi -DRNNT_DEV_NO_EPI ;;
     nomfma) build nomfma -DRNNT_DEV_NO_MFMA ;;
     nomfma_noepi) build nomfma_noepi -DRNNT_DEV_NO_MFMA -DRNNT_DEV_NO_EPI ;;
+    same_nomfma_noepi) build same_nomfma_noepi -DRNNT_DEV_SAME_TILE -DRNNT_DEV_NO_MFMA -DRNNT_DEV_NO_EPI ;;
+    noload_noepi) build noload_noepi -DRNNT_DEV_NO_LOAD -DRNNT_DEV_NO_EPI ;;
+    noload) build noload -DRNNT_DEV_NO_LOAD ;;
+    ns3) build ns3 -DRNNT_NSTAGE=3 ;;
+    ns5) build ns5 -DRNNT_NSTAGE=5 ;;
+    ns3_noepi) build ns3_noepi -DRNNT_NSTAGE=3 -DRNNT_DEV_NO_EPI ;;
+    ns5_noepi) build ns5_noepi -DRNNT_NSTAGE=5 -DRNNT_DEV_NO_EPI ;;
+    same_noepi) build same_noepi -DRNNT_DEV_SAME_TILE -DRNNT_DEV_NO_EPI ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
