@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--qsl", type=int, default=2513, help="QSL utterances per GPU (mlperf.conf:13)")
     ap.add_argument("--query", type=int, default=24576, help="samples per Offline query per GPU (mlperf.conf:63)")
     ap.add_argument("--batch", type=int, default=8192, help="utterances per encode+decode call")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="batches in flight per GPU: one engine + HIP stream + host thread each, so one "
+                         "batch's latency-bound greedy decode overlaps the next batch's encoder")
     ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
@@ -114,17 +117,36 @@ def make_batches(qsl, query, batch):
     return out
 
 
-def run_step(engine, batches):
-    outs = []
-    for b in batches:
-        res = torch.empty((b["n"], engine.max_res), dtype=torch.int32, device="cuda")
-        rl = torch.empty(b["n"], dtype=torch.int32, device="cuda")
-        engine.infer(b["x"], b["lens"], b["lens_host"], res, rl, n=b["n"])
-        outs.append((res, rl))
+def run_step(engines, streams, batches):
+    """One Offline query.  Batch i runs on engine i % inflight, each engine with its own HIP
+    stream and host thread (ctypes releases the GIL).  Encoders take turns (a lock held until
+    the encode has finished on the GPU), so each batch's latency-bound greedy decode overlaps
+    the next batch's encoder instead of competing with another encoder.  Then the responses
+    are gathered to the host."""
+    import threading
+    k = len(engines)
+    enc_lock = threading.Lock()
+
+    def worker(j):
+        for b in batches[j::k]:
+            with enc_lock:
+                engines[j].encode(b["x"], b["lens"], b["lens_host"], n=b["n"], stream=streams[j])
+                streams[j].synchronize()
+            engines[j].decode(b["res"], b["rl"], stream=streams[j])
+
+    if k == 1:
+        worker(0)
+    else:
+        ths = [threading.Thread(target=worker, args=(j,)) for j in range(k)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    for s in streams:
+        s.synchronize()
     # host gather of the responses: lengths, then each batch's used token columns
-    lens = [rl.to("cpu", non_blocking=True) for _, rl in outs]
-    torch.cuda.synchronize()
-    toks = [res[:, : max(1, int(l.max()))].cpu() for (res, _), l in zip(outs, lens)]
+    lens = [b["rl"].cpu() for b in batches]
+    toks = [b["res"][:, : max(1, int(l.max()))].cpu() for b, l in zip(batches, lens)]
     return lens, toks
 
 
@@ -154,32 +176,40 @@ def main():
     pm, _ = weights.build_model()
     qsl = build_qsl(args.qsl, seed=4 + 1000 * rank)
     lens = qsl["lens"]
-    engine = Engine(pm, device=local, max_batch=min(args.batch, args.query), max_frames=500)
+    engines = [Engine(pm, device=local, max_batch=min(args.batch, args.query), max_frames=500)
+               for _ in range(args.inflight)]
+    engine = engines[0]
+    streams = [torch.cuda.Stream() for _ in engines]
     batches = make_batches(qsl, args.query, args.batch)
+    for b in batches:  # response buffers, allocated once (the engine fills them every call)
+        b["res"] = torch.empty((b["n"], engine.max_res), dtype=torch.int32, device="cuda")
+        b["rl"] = torch.empty(b["n"], dtype=torch.int32, device="cuda")
 
     for _ in range(args.warmup):
-        run_step(engine, batches)
-    torch.cuda.synchronize()
-    barrier(world)
-    engine.set_profiling(True)
-    engine.stats(reset=True)
+        run_step(engines, streams, batches)
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lens_out, _ = run_step(engine, batches)
+        lens_out, _ = run_step(engines, streams, batches)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
-    st = engine.stats(reset=True)
     elapsed_max = all_max(elapsed, world)
+    # roofline pass (untimed): the same query once more, batches back to back on one engine so
+    # the encoder kernel's event time is not shared with an overlapping decode
+    engine.set_profiling(True)
+    engine.stats(reset=True)
+    run_step([engine], [streams[0]], batches)
+    st = engine.stats(reset=True)
+    engine.set_profiling(False)
 
     utts = args.query * world * args.steps
     value = utts / elapsed_max
     emitted = int(sum(int(l.sum()) for l in lens_out))
     qlens = np.concatenate([b["lens_host"] for b in batches])
     enc_frames = int(sum(encoder_frames(l) for l in qlens))
-    enc_ops = float(sum(encoder_ops(int(l)) for l in qlens)) * args.steps  # SURVEY 8d E(T), valid frames
+    enc_ops = float(sum(encoder_ops(int(l)) for l in qlens))  # SURVEY 8d E(T), valid frames, one query
     achieved = enc_ops / (st["encode_ms"] * 1e-3) / 1e12 if st["encode_ms"] > 0 else 0.0
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -191,10 +221,11 @@ def main():
         "bound": "mfma", "kernel": "lstm_i8_step_kernel (int8 encoder, all 5 layers)",
         "achieved": round(achieved, 2), "peak": INT8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
         "frac": round(achieved / INT8_DENSE_PEAK_TOPS, 4), "traffic": traffic,
-        "encode_ms_per_step": round(st["encode_ms"] / args.steps, 3),
-        "joint_trans_ms_per_step": round(st["joint_trans_ms"] / args.steps, 3),
-        "greedy_ms_per_step": round(st["greedy_ms"] / args.steps, 3),
-        "step_launches_per_step": int(st["step_launches"] // max(1, args.steps)),
+        "measured_on": "untimed pass of the same query, batches back to back on one engine",
+        "encode_ms_per_query": round(st["encode_ms"], 3),
+        "joint_trans_ms_per_query": round(st["joint_trans_ms"], 3),
+        "greedy_ms_per_query": round(st["greedy_ms"], 3),
+        "tick_launches_per_query": int(st["step_launches"]),
     }
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "utterances/s", "n_gpus": world,
@@ -203,6 +234,7 @@ def main():
         "data": "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)",
         "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
                    "qsl_per_gpu": args.qsl, "query_samples_per_gpu": args.query, "batch_size": args.batch,
+                   "batches_in_flight": args.inflight,
                    "encoder": "int8 (lstm_amx_int8)",
                    "decoder": "bf16 prediction/joint, fp32 accumulate, greedy (device loop)",
                    "parallelism": f"dp{world} (one process per GPU, sharded queries)",
@@ -225,7 +257,8 @@ def main():
         out["parity_spot_check"] = {"utterances": cb["n"], "tokens_identical": same}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    engine.close()
+    for e in engines:
+        e.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -9,9 +9,9 @@
 //
 // The greedy loop runs lock-step over the batch like the reference's (rnnt_model.hpp:92-124):
 // per step, weight-stationary kernels run the prediction network for the rows that emitted,
-// then one kernel does joint + argmax + greedy_decode_update for every live row; the host
-// only enqueues steps and polls a live-row counter one 32-step chunk behind (no per-step
-// round trip).  Two algebraic shortcuts, both exact:
+// then one kernel does joint + argmax + greedy_decode_update for every live row, walking each
+// row through its blank frames until it emits; the host only enqueues steps and polls a
+// live-row counter one 32-step chunk behind (no per-step round trip).  Two algebraic shortcuts, both exact:
 //   * the joint's encoder half F[t] = b_t + bf16(f_t).W1t^T depends only on the frame, so it is
 //     one batched GEMM over all frames before the loop (launch_joint_trans);
 //   * prediction(pre_g, pre_hg, pre_cg) depends only on state that changes on an emit, so it
@@ -105,19 +105,20 @@ __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
 }
 
 // One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates = (b_ih+b_hh) +
-// chain over [x | h_prev]; c fp32, h bf16.  Grid: x = 8-gate-tile group (128 gate rows),
-// y = 16-row tile of the emit list.
-__global__ void __launch_bounds__(256) dec_pred_kernel(DecArgs a, int layer, int parity) {
+// chain over [x | h_prev]; c fp32, h bf16.  Grid: x = 8-gate-tile group (128 gate rows, the
+// weights held in registers for the whole launch), y = DEC_ROW_GROUPS workgroups striding over
+// the emit list's 16-row tiles, so each weight fetch is amortised over every tile it serves.
+__global__ void __launch_bounds__(256, 2) dec_pred_kernel(DecArgs a, int layer, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][XP];
   __shared__ int rows[16], slots[16], pregs[16];
   const DecState& s = a.s;
   const int cnt = s.count[parity];
-  const int rt = blockIdx.y;
-  if (rt * 16 >= cnt) return;
+  const int ntiles = (cnt + 15) >> 4;
+  if ((int)blockIdx.y >= ntiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   const int* list = s.list + parity * a.Npad;
   // this wave's weight fragments (2 gate tiles x 20 k-blocks = 160 VGPRs) in one burst, issued
-  // before the operand staging so the L2 round trip overlaps it
+  // before the first operand staging so the L2 round trip overlaps it
   const int gt = blockIdx.x * 8 + wave * 2;
   const uint16_t* w0 = a.w.wp[layer] + (size_t)(gt * 16 + c) * 640 + 8 * q;
   const uint16_t* w1 = w0 + 16 * 640;
@@ -127,138 +128,147 @@ __global__ void __launch_bounds__(256) dec_pred_kernel(DecArgs a, int layer, int
     wa[b] = *(const uint4*)(w0 + 32 * b);
     wb[b] = *(const uint4*)(w1 + 32 * b);
   }
-  if (tid < 16) {
-    const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
-    rows[tid] = row;
-    slots[tid] = row >= 0 ? s.slot[row] : 0;
-    pregs[tid] = row >= 0 ? s.preg[row] : SOS;
-  }
-  __syncthreads();
-  // stage [x | h_prev] for the 16 listed rows: 16 x 160 float4 groups, 10 per thread
-  for (int i = tid; i < 16 * 160; i += 256) {
-    const int mi = i / 160, k = (i % 160) * 4, row = rows[mi];
-    float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (row >= 0) {
-      const int sl = slots[mi];
-      if (layer == 0) {
-        if (k < P) {
-          const int g = pregs[mi];
-          if (g != SOS) {  // SOS -> zero embedding (modeling_rnnt.py:195-200)
-            const uint2 e2 = *(const uint2*)(a.w.embed + g * P + k);
-            v = float4{bits2f(e2.x << 16), bits2f(e2.x & 0xffff0000u), bits2f(e2.y << 16), bits2f(e2.y & 0xffff0000u)};
+  const float* bias = a.w.bp_lstm[layer];
+  const float4 b0 = *(const float4*)(bias + gt * 16 + 4 * q);
+  const float4 b1 = *(const float4*)(bias + (gt + 1) * 16 + 4 * q);
+  for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
+    if (tid < 16) {
+      const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
+      rows[tid] = row;
+      slots[tid] = row >= 0 ? s.slot[row] : 0;
+      pregs[tid] = row >= 0 ? s.preg[row] : SOS;
+    }
+    __syncthreads();
+    // stage [x | h_prev] for the 16 listed rows: 16 x 160 float4 groups, 10 per thread
+    for (int i = tid; i < 16 * 160; i += 256) {
+      const int mi = i / 160, k = (i % 160) * 4, row = rows[mi];
+      float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (row >= 0) {
+        const int sl = slots[mi];
+        if (layer == 0) {
+          if (k < P) {
+            const int g = pregs[mi];
+            if (g != SOS) {  // SOS -> zero embedding (modeling_rnnt.py:195-200)
+              const uint2 e2 = *(const uint2*)(a.w.embed + g * P + k);
+              v = float4{bits2f(e2.x << 16), bits2f(e2.x & 0xffff0000u), bits2f(e2.y << 16), bits2f(e2.y & 0xffff0000u)};
+            }
+          } else {
+            v = *(const float4*)(hc_part(a.hc, row, sl, 0) + k - P);
           }
         } else {
-          v = *(const float4*)(hc_part(a.hc, row, sl, 0) + k - P);
+          v = (k < P) ? *(const float4*)(hc_part(a.hc, row, sl ^ 1, 0) + k) : *(const float4*)(hc_part(a.hc, row, sl, 1) + k - P);
         }
-      } else {
-        v = (k < P) ? *(const float4*)(hc_part(a.hc, row, sl ^ 1, 0) + k) : *(const float4*)(hc_part(a.hc, row, sl, 1) + k - P);
+      }
+      X[mi][chain_pos(k)] = v.x;
+      X[mi][chain_pos(k + 1)] = v.y;
+      X[mi][chain_pos(k + 2)] = v.z;
+      X[mi][chain_pos(k + 3)] = v.w;
+    }
+    __syncthreads();
+    if (rt == (int)blockIdx.y) {
+#pragma unroll
+      for (int b = 0; b < 20; ++b)  // weights are live (waited for) here, behind the first staging
+        asm volatile("" ::"v"(wa[b].x), "v"(wa[b].y), "v"(wa[b].z), "v"(wa[b].w), "v"(wb[b].x), "v"(wb[b].y),
+                     "v"(wb[b].z), "v"(wb[b].w));
+    }
+    const float* xrow = &X[c][8 * q];
+    v4f acc0 = v4f{b0.x, b0.y, b0.z, b0.w}, acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int b = 0; b < 640 / 32; ++b) {
+      float x[8];
+      *(float4*)&x[0] = *(const float4*)(xrow + 32 * b);
+      *(float4*)&x[4] = *(const float4*)(xrow + 32 * b + 4);
+      acc0 = chain8(wa[b], x, acc0);
+      acc1 = chain8(wb[b], x, acc1);
+    }
+    const int row = rows[c];
+    if (row >= 0) {
+      const int sl = slots[c];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const v4f g = half ? acc1 : acc0;
+        const int u = (gt + half) * 4 + q;
+        const float ig = det_sigmoid(g[0]), fg = det_sigmoid(g[1]), gg = det_tanh(g[2]), og = det_sigmoid(g[3]);
+        const float cp = hc_part(a.hc, row, sl, 2 + layer)[u];
+        const float cn = fg * cp + ig * gg;
+        const float hh = bf_round(og * det_tanh(cn));
+        hc_part(a.hc, row, sl ^ 1, 2 + layer)[u] = cn;
+        hc_part(a.hc, row, sl ^ 1, layer)[u] = hh;
       }
     }
-    X[mi][chain_pos(k)] = v.x;
-    X[mi][chain_pos(k + 1)] = v.y;
-    X[mi][chain_pos(k + 2)] = v.z;
-    X[mi][chain_pos(k + 3)] = v.w;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < 20; ++b)  // weights are live (waited for) here, behind the staging
-    asm volatile("" ::"v"(wa[b].x), "v"(wa[b].y), "v"(wa[b].z), "v"(wa[b].w), "v"(wb[b].x), "v"(wb[b].y),
-                 "v"(wb[b].z), "v"(wb[b].w));
-  const float* bias = a.w.bp_lstm[layer];
-  const float* xrow = &X[c][8 * q];
-  v4f acc0, acc1;
-  {
-    const float4 b0 = *(const float4*)(bias + gt * 16 + 4 * q);
-    const float4 b1 = *(const float4*)(bias + (gt + 1) * 16 + 4 * q);
-    acc0 = v4f{b0.x, b0.y, b0.z, b0.w};
-    acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
-  }
-#pragma unroll
-  for (int b = 0; b < 640 / 32; ++b) {
-    float x[8];
-    *(float4*)&x[0] = *(const float4*)(xrow + 32 * b);
-    *(float4*)&x[4] = *(const float4*)(xrow + 32 * b + 4);
-    acc0 = chain8(wa[b], x, acc0);
-    acc1 = chain8(wb[b], x, acc1);
-  }
-  const int row = rows[c];
-  if (row >= 0) {
-    const int sl = slots[c];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const v4f g = half ? acc1 : acc0;
-      const int u = (gt + half) * 4 + q;
-      const float ig = det_sigmoid(g[0]), fg = det_sigmoid(g[1]), gg = det_tanh(g[2]), og = det_sigmoid(g[3]);
-      const float cp = hc_part(a.hc, row, sl, 2 + layer)[u];
-      const float cn = fg * cp + ig * gg;
-      const float hh = bf_round(og * det_tanh(cn));
-      hc_part(a.hc, row, sl ^ 1, 2 + layer)[u] = cn;
-      hc_part(a.hc, row, sl ^ 1, layer)[u] = hh;
-    }
+    __syncthreads();  // X / rows are restaged by the next tile
   }
 }
 
-// G = b_p + g . W1p^T for the listed rows' new candidates.  Grid: x = 128-column group,
-// y = 16-row tile.  Also clears the other parity's emit list for the joint that follows.
-__global__ void __launch_bounds__(256) dec_g_kernel(DecArgs a, int parity) {
+// G = b_p + g . W1p^T for the listed rows' new candidates.  Grid: x = 128-column group
+// (weights in registers), y = DEC_ROW_GROUPS workgroups striding over 16-row tiles.  Also
+// clears the other parity's emit list for the joint that follows.
+__global__ void __launch_bounds__(256, 2) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][GP];
   __shared__ int rows[16], slots[16];
   DecState& s = a.s;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) s.count[parity ^ 1] = 0;
   const int cnt = s.count[parity];
-  const int rt = blockIdx.y;
-  if (rt * 16 >= cnt) return;
+  const int ntiles = (cnt + 15) >> 4;
+  if ((int)blockIdx.y >= ntiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   const int* list = s.list + parity * a.Npad;
-  if (tid < 16) {
-    const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
-    rows[tid] = row;
-    slots[tid] = row >= 0 ? s.slot[row] : 0;
-  }
-  __syncthreads();
-  for (int i = tid; i < 16 * (P / 4); i += 256) {
-    const int mi = i / (P / 4), k = (i % (P / 4)) * 4, row = rows[mi];
-    const float4 v = row >= 0 ? *(const float4*)(hc_part(a.hc, row, slots[mi] ^ 1, 1) + k) : float4{0.0f, 0.0f, 0.0f, 0.0f};
-    X[mi][chain_pos(k)] = v.x;
-    X[mi][chain_pos(k + 1)] = v.y;
-    X[mi][chain_pos(k + 2)] = v.z;
-    X[mi][chain_pos(k + 3)] = v.w;
-  }
-  __syncthreads();
   const int jt = blockIdx.x * 8 + wave * 2;
-  v4f acc0, acc1;
-  {
-    const float4 b0 = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
-    const float4 b1 = *(const float4*)(a.w.bp + (jt + 1) * 16 + 4 * q);
-    acc0 = v4f{b0.x, b0.y, b0.z, b0.w};
-    acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
-  }
   const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
   const uint16_t* w1 = w0 + 16 * P;
-  const float* xr = &X[c][8 * q];
   uint4 wa[P / 32], wb[P / 32];
 #pragma unroll
   for (int b = 0; b < P / 32; ++b) {
     wa[b] = *(const uint4*)(w0 + 32 * b);
     wb[b] = *(const uint4*)(w1 + 32 * b);
   }
+  const float4 b0 = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
+  const float4 b1 = *(const float4*)(a.w.bp + (jt + 1) * 16 + 4 * q);
+  for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
+    if (tid < 16) {
+      const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
+      rows[tid] = row;
+      slots[tid] = row >= 0 ? s.slot[row] : 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < 16 * (P / 4); i += 256) {
+      const int mi = i / (P / 4), k = (i % (P / 4)) * 4, row = rows[mi];
+      const float4 v = row >= 0 ? *(const float4*)(hc_part(a.hc, row, slots[mi] ^ 1, 1) + k) : float4{0.0f, 0.0f, 0.0f, 0.0f};
+      X[mi][chain_pos(k)] = v.x;
+      X[mi][chain_pos(k + 1)] = v.y;
+      X[mi][chain_pos(k + 2)] = v.z;
+      X[mi][chain_pos(k + 3)] = v.w;
+    }
+    __syncthreads();
+    v4f acc0 = v4f{b0.x, b0.y, b0.z, b0.w}, acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
+    const float* xr = &X[c][8 * q];
 #pragma unroll
-  for (int b = 0; b < P / 32; ++b) {
-    float x[8];
-    *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
-    *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-    acc0 = chain8(wa[b], x, acc0);
-    acc1 = chain8(wb[b], x, acc1);
-  }
-  const int row = rows[c];
-  if (row >= 0) {
-    *(float4*)(a.G + (size_t)row * J + jt * 16 + 4 * q) = float4{acc0[0], acc0[1], acc0[2], acc0[3]};
-    *(float4*)(a.G + (size_t)row * J + (jt + 1) * 16 + 4 * q) = float4{acc1[0], acc1[1], acc1[2], acc1[3]};
+    for (int b = 0; b < P / 32; ++b) {
+      float x[8];
+      *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
+      *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
+      acc0 = chain8(wa[b], x, acc0);
+      acc1 = chain8(wb[b], x, acc1);
+    }
+    const int row = rows[c];
+    if (row >= 0) {
+      *(float4*)(a.G + (size_t)row * J + jt * 16 + 4 * q) = float4{acc0[0], acc0[1], acc0[2], acc0[3]};
+      *(float4*)(a.G + (size_t)row * J + (jt + 1) * 16 + 4 * q) = float4{acc1[0], acc1[1], acc1[2], acc1[3]};
+    }
+    __syncthreads();
   }
 }
 
 // joint (y1 = bf16(relu(F[t] + G)), logits = b2 + y1.W2^T) + argmax + greedy_decode_update
-// (decoder.py:137-167) for 16 rows per workgroup; emitting rows go to the next emit list.
+// (decoder.py:137-167) for 16 rows per workgroup.  A blank (or a forced advance after
+// max_symbols_per_step) moves the row to its next frame with the SAME prediction, so the
+// workgroup evaluates up to RNNT_JOINT_ITERS frames per launch, stopping a row at its first
+// emission (it then needs a new prediction: next step's emit list) or at its last frame; rows
+// still in a blank run stay live for the next step.  Identical results for any cap; the cap
+// trades lock-step steps against the length of each step.
+#ifndef RNNT_JOINT_ITERS
+#define RNNT_JOINT_ITERS 2
+#endif
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][YP];
   __shared__ float L[16][NLAB_PAD + 1];
@@ -273,69 +283,75 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     tidx[tid] = lv ? s.time[row] : 0;
   }
   __syncthreads();
-  bool any = false;
+  for (int it = 0; it < RNNT_JOINT_ITERS; ++it) {
+    bool any = false;
 #pragma unroll
-  for (int m = 0; m < 16; ++m) any |= live[m] != 0;
-  if (!any) return;
-  for (int i = tid; i < 16 * (J / 4); i += 256) {
-    const int m = i / (J / 4), k = (i % (J / 4)) * 4, row = r0 + m;
-    float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (live[m]) {
-      const float4 f4 = *(const float4*)(a.F + ((size_t)tidx[m] * a.Npad + row) * J + k);
-      const float4 g4 = *(const float4*)(a.G + (size_t)row * J + k);
-      const float s0 = f4.x + g4.x, s1 = f4.y + g4.y, s2 = f4.z + g4.z, s3 = f4.w + g4.w;
-      v = float4{bf_round(s0 > 0.0f ? s0 : 0.0f), bf_round(s1 > 0.0f ? s1 : 0.0f), bf_round(s2 > 0.0f ? s2 : 0.0f),
-                 bf_round(s3 > 0.0f ? s3 : 0.0f)};
-    }
-    X[m][chain_pos(k)] = v.x;
-    X[m][chain_pos(k + 1)] = v.y;
-    X[m][chain_pos(k + 2)] = v.z;
-    X[m][chain_pos(k + 3)] = v.w;
-  }
-  __syncthreads();
-  if (wave < 2) {
-    const float4 b0 = *(const float4*)(a.w.b2 + wave * 16 + 4 * q);
-    v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
-    const uint16_t* wr = a.w.w2 + (size_t)(wave * 16 + c) * J + 8 * q;
-    const float* xr = &X[c][8 * q];
-    uint4 wv[J / 32];
-#pragma unroll
-    for (int b = 0; b < J / 32; ++b) wv[b] = *(const uint4*)(wr + 32 * b);
-#pragma unroll
-    for (int b = 0; b < J / 32; ++b) {
-      float x[8];
-      *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
-      *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-      acc = chain8(wv[b], x, acc);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) L[c][wave * 16 + 4 * q + r] = acc[r];
-  }
-  __syncthreads();
-  if (tid < 16 && live[tid]) {
-    const int m = tid, row = r0 + m;
-    int best = 0;
-    float bv = L[m][0];
-    for (int j = 1; j < NLAB; ++j)
-      if (L[m][j] > bv) { bv = L[m][j]; best = j; }  // torch.argmax: first maximum
-    if (best != BLANK && s.added[row] != MAXSYM) {
-      const int id = ++s.idx[row];
-      if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
-      s.added[row]++;
-      s.preg[row] = best;
-      s.slot[row] ^= 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
-      s.list[(parity ^ 1) * a.Npad + atomicAdd(&s.count[parity ^ 1], 1)] = row;
-    } else {
-      const int fl = a.f_lens[row];
-      int t = tidx[m] + 1;
-      if (t >= fl) {
-        s.fin[row] = 1;
-        atomicSub(s.unfinished, 1);
+    for (int m = 0; m < 16; ++m) any |= live[m] != 0;
+    if (!any) return;
+    for (int i = tid; i < 16 * (J / 4); i += 256) {
+      const int m = i / (J / 4), k = (i % (J / 4)) * 4, row = r0 + m;
+      float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (live[m]) {
+        const float4 f4 = *(const float4*)(a.F + ((size_t)tidx[m] * a.Npad + row) * J + k);
+        const float4 g4 = *(const float4*)(a.G + (size_t)row * J + k);
+        const float s0 = f4.x + g4.x, s1 = f4.y + g4.y, s2 = f4.z + g4.z, s3 = f4.w + g4.w;
+        v = float4{bf_round(s0 > 0.0f ? s0 : 0.0f), bf_round(s1 > 0.0f ? s1 : 0.0f), bf_round(s2 > 0.0f ? s2 : 0.0f),
+                   bf_round(s3 > 0.0f ? s3 : 0.0f)};
       }
-      if (t > fl - 1) t = fl - 1;
-      s.time[row] = t;
-      s.added[row] = 0;
+      X[m][chain_pos(k)] = v.x;
+      X[m][chain_pos(k + 1)] = v.y;
+      X[m][chain_pos(k + 2)] = v.z;
+      X[m][chain_pos(k + 3)] = v.w;
     }
+    __syncthreads();
+    if (wave < 2) {
+      const float4 b0 = *(const float4*)(a.w.b2 + wave * 16 + 4 * q);
+      v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
+      const uint16_t* wr = a.w.w2 + (size_t)(wave * 16 + c) * J + 8 * q;
+      const float* xr = &X[c][8 * q];
+      uint4 wv[J / 32];
+#pragma unroll
+      for (int b = 0; b < J / 32; ++b) wv[b] = *(const uint4*)(wr + 32 * b);
+#pragma unroll
+      for (int b = 0; b < J / 32; ++b) {
+        float x[8];
+        *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
+        *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
+        acc = chain8(wv[b], x, acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) L[c][wave * 16 + 4 * q + r] = acc[r];
+    }
+    __syncthreads();
+    if (tid < 16 && live[tid]) {
+      const int m = tid, row = r0 + m;
+      int best = 0;
+      float bv = L[m][0];
+      for (int j = 1; j < NLAB; ++j)
+        if (L[m][j] > bv) { bv = L[m][j]; best = j; }  // torch.argmax: first maximum
+      if (best != BLANK && s.added[row] != MAXSYM) {
+        const int id = ++s.idx[row];
+        if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
+        s.added[row]++;
+        s.preg[row] = best;
+        s.slot[row] ^= 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+        s.list[(parity ^ 1) * a.Npad + atomicAdd(&s.count[parity ^ 1], 1)] = row;
+        live[m] = 0;
+      } else {
+        const int fl = a.f_lens[row];
+        int t = tidx[m] + 1;
+        if (t >= fl) {
+          s.fin[row] = 1;
+          atomicSub(s.unfinished, 1);
+          live[m] = 0;
+          t = fl - 1;
+        }
+        tidx[m] = t;
+        s.time[row] = t;
+        s.added[row] = 0;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -346,6 +362,9 @@ __global__ void dec_finish_kernel(DecArgs a) {
 
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st) {
   const int rt = a.Npad / 16;
+  // row-tile workgroups per column group, sized so each launch is ONE resident round (2
+  // workgroups per CU x 256 CUs): 10 x 51 for the prediction layers, 4 x 128 for G
+  const int rg_pred = rt < 51 ? rt : 51, rg_g = rt < 128 ? rt : 128;
   if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.s.unfinished, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
@@ -356,9 +375,9 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   while (!done && step < a.max_iter) {
     for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rt), dim3(256), 0, st, a, 0, p);
-      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rt), dim3(256), 0, st, a, 1, p);
-      hipLaunchKernelGGL(dec_g_kernel, dim3(J / 128, rt), dim3(256), 0, st, a, p);
+      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rg_pred), dim3(256), 0, st, a, 0, p);
+      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rg_pred), dim3(256), 0, st, a, 1, p);
+      hipLaunchKernelGGL(dec_g_kernel, dim3(J / 128, rg_g), dim3(256), 0, st, a, p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rt), dim3(256), 0, st, a, p);
     }
     // poll the live-row counter one chunk behind, so the host never drains the queue

@@ -77,8 +77,14 @@ def main():
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         st = eng.stats(reset=True)
+        U = rl.cpu().numpy().astype(np.int64)
+        Tp = (lens.astype(np.int64) + 1) // 2
         out["infer_batch"] = {"n": args.n, "wall_ms": round(wall * 1e3, 2), **{k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()},
-                              "emitted": int(rl.sum().item())}
+                              "emitted": int(U.sum()),
+                              "U_pct": [int(np.percentile(U, p)) for p in (50, 90, 99, 100)],
+                              "Tp_pct": [int(np.percentile(Tp, p)) for p in (50, 90, 99, 100)],
+                              "TpU_max": int((Tp + U).max()), "U_over_Tp_max": round(float((U / Tp).max()), 2),
+                              "top_U_rows": [[int(U[i]), int(Tp[i])] for i in np.argsort(-U)[:8]]}
     print(json.dumps(out))
     eng.close()
 

@@ -15,6 +15,10 @@ for v in "$@"; do
     same_nomfma_noepi) build same_nomfma_noepi -DRNNT_DEV_SAME_TILE -DRNNT_DEV_NO_MFMA -DRNNT_DEV_NO_EPI ;;
     noload_noepi) build noload_noepi -DRNNT_DEV_NO_LOAD -DRNNT_DEV_NO_EPI ;;
     noload) build noload -DRNNT_DEV_NO_LOAD ;;
+    ji1) build ji1 -DRNNT_JOINT_ITERS=1 ;;
+    ji2) build ji2 -DRNNT_JOINT_ITERS=2 ;;
+    ji4) build ji4 -DRNNT_JOINT_ITERS=4 ;;
+    ji8) build ji8 -DRNNT_JOINT_ITERS=8 ;;
     ns3) build ns3 -DRNNT_NSTAGE=3 ;;
     ns5) build ns5 -DRNNT_NSTAGE=5 ;;
     ns3_noepi) build ns3_noepi -DRNNT_NSTAGE=3 -DRNNT_DEV_NO_EPI ;;
