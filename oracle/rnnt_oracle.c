@@ -56,45 +56,45 @@ float oracle_tanh(float x) {
 }
 
 /* ---------------------------------------------------------------- int8 LSTM cell ----
- * The quantised encoder's cell (quant_lstm.py:162-183 semantics), in the division-light
- * form the HIP epilogue evaluates (rnnt-inference_amd/csrc/rnnt_device.hpp enc_cell):
- *   e2(z) = 2^z: z clamped to [-40, 40], n = rint(z), degree-5 minimax polynomial in
- *           z - n (max rel. error 2.2e-7), scaled by ldexp (exact);
- *   sigma(x) = 1 / (1 + e2(-x log2 e)), tanh(x) = (1 - e2(-2x log2 e)) / (1 + e2(-2x log2 e));
- *   c = f c_prev + i g = (c_prev (1+ei)(1+eg) + (1-eg)(1+ef)) / ((1+ef)(1+ei)(1+eg))
- *   h = o tanh(c)      = (1 - ec) / ((1+eo)(1+ec))
- * i.e. two IEEE divisions per cell instead of five.  The clamp is exact in fp32 (sigma and
- * tanh round to +-1 / 0 long before it) and keeps every product below 2^121. */
-float oracle_e2(float z) {
-  z = fminf(fmaxf(z, -40.0f), 40.0f);
-  const float n = rintf(z);
-  const float f = z - n;
-  float p = 1.327606732957065e-3f;
-  p = fmaf(p, f, 9.675402194261551e-3f);
-  p = fmaf(p, f, 5.550713464617729e-2f);
-  p = fmaf(p, f, 2.4022123217582703e-1f);
-  p = fmaf(p, f, 6.931469440460205e-1f);
-  p = fmaf(p, f, 1.0000001192092896f);
-  return ldexpf(p, (int)n);
+ * The quantised encoder's cell (quant_lstm.py:162-183 semantics) exactly as the HIP epilogue
+ * evaluates it (rnnt-inference_amd/csrc/rnnt_device.hpp enc_cell):
+ *   sigma(x) from a 128-interval piecewise-cubic table on [-16, 16) (act_table.inc, generated
+ *   by tools/gen_act_table.py; max abs error 4e-7), indexed by t = 4x + 64:
+ *       t = clamp(t, 0, 127.99998); k = (int)t; fr = t - floor(t); Horner in fr with fmaf;
+ *   tanh(x) = 2 sigma(2x) - 1 (t = 8x + 64);
+ *   the dequantisation is folded into the index: t = fma((float)acc, A, B) with A = 4 rb
+ *   (8 rb for the g gate) and B = 4 (bq rb) + 64 (8 (bq rb) + 64 for g), B precomputed per
+ *   gate row in fp32 (oracle_enc_bias);
+ *   c = fma(f, c_prev, i g),  h = o (2 sigma(2c) - 1).
+ * No exp, no division: ~60 VALU instructions per cell on the GPU. */
+static const float ACT_TAB[128][4] = {
+#include "act_table.inc"
+};
+
+float oracle_act_sig_t(float t) {
+  t = fminf(fmaxf(t, 0.0f), 127.99998f);
+  const int k = (int)t;
+  const float fr = t - floorf(t);
+  const float* c = ACT_TAB[k];
+  return fmaf(fmaf(fmaf(c[3], fr, c[2]), fr, c[1]), fr, c[0]);
 }
 
-#define NL2E (-1.44269504088896341f)
-#define NL2E2 (-2.88539008177792682f)
+float oracle_enc_bias(float bq, float rb, int gate) {
+  const float b = bq * rb;
+  return gate == 2 ? b * 8.0f + 64.0f : b * 4.0f + 64.0f;
+}
 
-void oracle_enc_cell(const int32_t acc[4], const float bqr[4], float rb, float c_prev,
-                     float* c_out, float* h_out) {
-  const float pi = fmaf((float)acc[0], rb, bqr[0]);
-  const float pf = fmaf((float)acc[1], rb, bqr[1]);
-  const float pg = fmaf((float)acc[2], rb, bqr[2]);
-  const float po = fmaf((float)acc[3], rb, bqr[3]);
-  const float ei = oracle_e2(pi * NL2E), ef = oracle_e2(pf * NL2E);
-  const float eg = oracle_e2(pg * NL2E2), eo = oracle_e2(po * NL2E);
-  const float A = 1.0f + ef, B = (1.0f + ei) * (1.0f + eg);
-  const float num = fmaf(c_prev, B, (1.0f - eg) * A);
-  const float c = num / (A * B);
-  const float ec = oracle_e2(c * NL2E2);
+void oracle_enc_cell(const int32_t acc[4], const float B[4], float rb, float c_prev, float* c_out,
+                     float* h_out) {
+  const float As = rb * 4.0f, Ag = rb * 8.0f;
+  const float ig = oracle_act_sig_t(fmaf((float)acc[0], As, B[0]));
+  const float fg = oracle_act_sig_t(fmaf((float)acc[1], As, B[1]));
+  const float gg = fmaf(2.0f, oracle_act_sig_t(fmaf((float)acc[2], Ag, B[2])), -1.0f);
+  const float og = oracle_act_sig_t(fmaf((float)acc[3], As, B[3]));
+  const float c = fmaf(fg, c_prev, ig * gg);
+  const float tc = fmaf(2.0f, oracle_act_sig_t(fmaf(c, 8.0f, 64.0f)), -1.0f);
   *c_out = c;
-  *h_out = (1.0f - ec) / ((1.0f + eo) * (1.0f + ec));
+  *h_out = og * tc;
 }
 
 /* ---------------------------------------------------------------- conversions ---- */
@@ -193,9 +193,9 @@ void oracle_lstm_i8_layer(int T, int N, int I, int H, const int8_t* x, const int
       const int32_t* a = acc + (size_t)n * 4 * H;
       uint16_t* cv = c + (size_t)n * H;
       for (int j = 0; j < H; ++j) {
-        /* bias pre-scaled once: bqr = bq * rb (fp32), pre = fma(acc, rb, bqr) */
         const int32_t ag[4] = {a[j], a[H + j], a[2 * H + j], a[3 * H + j]};
-        const float br[4] = {bq[j] * rb, bq[H + j] * rb, bq[2 * H + j] * rb, bq[3 * H + j] * rb};
+        const float br[4] = {oracle_enc_bias(bq[j], rb, 0), oracle_enc_bias(bq[H + j], rb, 1),
+                             oracle_enc_bias(bq[2 * H + j], rb, 2), oracle_enc_bias(bq[3 * H + j], rb, 3)};
         float cn, hh;
         oracle_enc_cell(ag, br, rb, oracle_h2f(cv[j]), &cn, &hh);
         cv[j] = oracle_f2h(cn);

@@ -25,8 +25,9 @@ extern "C" {
 float oracle_exp(float x);
 float oracle_sigmoid(float x);
 float oracle_tanh(float x);
-float oracle_e2(float z);         /* 2^z of the int8 cell (see rnnt_oracle.c) */
-void oracle_enc_cell(const int32_t acc[4], const float bqr[4], float rb, float c_prev,
+float oracle_act_sig_t(float t);  /* table sigma at t = 4x + 64 (int8 cell, see rnnt_oracle.c) */
+float oracle_enc_bias(float bq, float rb, int gate);
+void oracle_enc_cell(const int32_t acc[4], const float B[4], float rb, float c_prev,
                      float* c_out, float* h_out);
 uint16_t oracle_f2h(float x);      /* f32 -> f16 bits, round-half-even */
 float oracle_h2f(uint16_t h);

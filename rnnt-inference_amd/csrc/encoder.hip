@@ -16,6 +16,11 @@
 
 namespace rnnt {
 
+// sigma table of the cell (tools/gen_act_table.py), copied to LDS by every workgroup
+__device__ const float4 g_act_tab[128] = {
+#include "act_table.inc"
+};
+
 // ---------------------------------------------------------------- feature quantisation
 // x_q = q8(x * in_scale[0]) over [T][Npad][256] (layer-0 input quantizer, calibrated on
 // cat([x, h]); quant_modules.py:118-121).
@@ -46,6 +51,8 @@ constexpr int NSTAGE = RNNT_NSTAGE;          // LDS ring depth: NSTAGE-1 stages 
 constexpr int A_BYTES = BM * BK;             // 16 KiB
 constexpr int STAGE_BYTES = (BM + BN) * BK;  // 32 KiB
 constexpr int GLDS_PER_STAGE = 4;            // per wave: 2 x 1 KiB pieces of A, 2 of B
+constexpr int TAB_OFF = NSTAGE * STAGE_BYTES;   // LDS: sigma table after the ring
+constexpr int SMEM_BYTES = TAB_OFF + 128 * 16;
 static_assert(BM / 16 == 2 * NWAVE && BN / 16 == 2 * NWAVE, "two 16-row pieces per wave per operand");
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -163,7 +170,8 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #endif
 
   // ---- fused LSTM cell epilogue (quant_lstm.py:162-183 semantics; oracle_enc_cell)
-  const float rbs = a.rb, ins = a.in_s, outs = a.out_s;
+  const float As = a.rb * 4.0f, Ag = a.rb * 8.0f, ins = a.in_s, outs = a.out_s;
+  const float4* tab = (const float4*)(smem + TAB_OFF);
   float4 bq[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) bq[i] = *(const float4*)(a.bq + m0 + wm * 64 + i * 16 + q * 4);
@@ -177,7 +185,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float cn, hh;
-      enc_cell(acc[i][j], bq[i], rbs, cin[i], cn, hh);
+      enc_cell(tab, acc[i][j], bq[i], As, Ag, cin[i], cn, hh);
       cw[i >> 1] |= (uint32_t)f2h(cn) << (16 * (i & 1));
       hv[i] = hh;
       hq |= (uint32_t)(uint8_t)q8(hh * ins) << (8 * i);
@@ -222,6 +230,8 @@ __global__ void __launch_bounds__(512, 1) lstm_i8_tick_kernel(EncTickArgs args) 
     k -= cnt;
   }
   if (jsel < 0) return;
+  if (threadIdx.x < 128) ((float4*)(smem + TAB_OFF))[threadIdx.x] = g_act_tab[threadIdx.x];  // read after the
+  // first stage barrier of the main loop (lgkmcnt(0) + s_barrier)
   // wave-uniform runtime index into the kernarg segment: the job's fields stay scalar loads
   lstm_i8_step(args.job[__builtin_amdgcn_readfirstlane(jsel)], __builtin_amdgcn_readfirstlane(mt),
                __builtin_amdgcn_readfirstlane(nt), smem);
@@ -241,14 +251,14 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute((const void*)lstm_i8_tick_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            NSTAGE * STAGE_BYTES) != hipSuccess)
+                            SMEM_BYTES) != hipSuccess)
       return -1;
     attr = true;
   }
   int per_xcd = 0;  // the batch-half-0 XCDs carry the larger half
   for (int j = 0; j < a.njobs; ++j) per_xcd += 4 * ((a.nbt[j] + 1) >> 1);
   if (per_xcd <= 0) return 0;
-  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(8 * per_xcd), dim3(NWAVE * 64), NSTAGE * STAGE_BYTES, st, a);
+  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(8 * per_xcd), dim3(NWAVE * 64), SMEM_BYTES, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -20,7 +20,7 @@ enum EncOutMode { ENC_OUT_I8 = 0, ENC_OUT_STACKED = 1, ENC_OUT_FINAL = 2 };
 
 struct EncStepArgs {
   const int8_t* W;     // packed [4096][I+1024], gate-interleaved rows
-  const float* bq;     // packed [4096], pre-scaled by rb (bqr = bq * rb)
+  const float* bq;     // packed [4096] cell bias terms B = (bq rb) * (4 | 8 for g) + 64
   const int8_t* x;     // this frame's input rows: [Npad][I]
   const int8_t* h_in;  // [Npad][1024] h_{t-1} (quantised with in_s)
   int8_t* h_out;       // [Npad][1024] h_t

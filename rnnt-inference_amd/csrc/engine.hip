@@ -100,7 +100,10 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
       for (int u = 0; u < H; ++u) {
         const int pr = enc_packed_row(u, g);
         memcpy(&w[(size_t)pr * K], m->enc_w[l] + (size_t)(g * H + u) * K, K);
-        b[pr] = m->enc_bq[l][g * H + u] * m->enc_rb[l];  // bqr (fp32 multiply, as oracle_lstm_i8_layer)
+        {  // the cell's folded bias term, as oracle_enc_bias: (bq rb) * (g == 2 ? 8 : 4) + 64
+          const float bqr = m->enc_bq[l][g * H + u] * m->enc_rb[l];
+          b[pr] = g == 2 ? bqr * 8.0f + 64.0f : bqr * 4.0f + 64.0f;
+        }
       }
     int r = upload(e, &e->enc_w[l], w);
     if (!r) r = upload(e, &e->enc_bq[l], b);

@@ -54,38 +54,33 @@ __device__ __forceinline__ float det_tanh(float x) {
   return __builtin_copysignf(t, x);
 }
 
-// ---- int8 encoder cell (bit-identical to oracle_e2 / oracle_enc_cell; the division-light
-// form is documented there): 2^z with z clamped to [-40, 40], degree-5 minimax polynomial
-// and an exact ldexp; two IEEE divisions per cell.
-__device__ __forceinline__ float enc_e2(float z) {
-  z = __builtin_fminf(__builtin_fmaxf(z, -40.0f), 40.0f);
-  const float n = __builtin_rintf(z);
-  const float f = z - n;
-  float p = 1.327606732957065e-3f;
-  p = __builtin_fmaf(p, f, 9.675402194261551e-3f);
-  p = __builtin_fmaf(p, f, 5.550713464617729e-2f);
-  p = __builtin_fmaf(p, f, 2.4022123217582703e-1f);
-  p = __builtin_fmaf(p, f, 6.931469440460205e-1f);
-  p = __builtin_fmaf(p, f, 1.0000001192092896f);
-  return __builtin_ldexpf(p, (int)n);
+// ---- int8 encoder cell (bit-identical to oracle_act_sig_t / oracle_enc_cell, where the
+// contract is documented): sigma from a 128-interval piecewise-cubic table held in LDS
+// (float4 per interval), indexed by t = 4x + 64; tanh(x) = 2 sigma(2x) - 1; the
+// dequantisation folded into the index, t = fma((float)acc, A, B).
+__device__ __forceinline__ float act_sig_t(const float4* __restrict__ tab, float t) {
+  t = __builtin_fminf(__builtin_fmaxf(t, 0.0f), 127.99998f);
+  const int k = (int)t;
+  const float fr = __builtin_amdgcn_fractf(t);  // v_fract_f32: t - floor(t), exact for t >= 0
+  const float4 c = tab[k];
+  return __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c.w, fr, c.z), fr, c.y), fr, c.x);
 }
-constexpr float ENC_NL2E = -1.44269504088896341f;
-constexpr float ENC_NL2E2 = -2.88539008177792682f;
-// acc: int32 gate sums (i, f, g, o); bqr: bias pre-scaled by rb; returns c (fp32) and h.
-__device__ __forceinline__ void enc_cell(const v4i acc, const float4 bqr, float rb, float c_prev, float& c_out,
-                                         float& h_out) {
-  const float pi = __builtin_fmaf((float)acc[0], rb, bqr.x);
-  const float pf = __builtin_fmaf((float)acc[1], rb, bqr.y);
-  const float pg = __builtin_fmaf((float)acc[2], rb, bqr.z);
-  const float po = __builtin_fmaf((float)acc[3], rb, bqr.w);
-  const float ei = enc_e2(pi * ENC_NL2E), ef = enc_e2(pf * ENC_NL2E);
-  const float eg = enc_e2(pg * ENC_NL2E2), eo = enc_e2(po * ENC_NL2E);
-  const float A = 1.0f + ef, B = (1.0f + ei) * (1.0f + eg);
-  const float num = __builtin_fmaf(c_prev, B, (1.0f - eg) * A);
-  const float c = num / (A * B);
-  const float ec = enc_e2(c * ENC_NL2E2);
+// acc: int32 gate sums (i, f, g, o); B: packed per-gate bias terms (oracle_enc_bias);
+// As = 4 rb, Ag = 8 rb.  Returns c (fp32) and h.
+__device__ __forceinline__ void enc_cell(const float4* __restrict__ tab, const v4i acc, const float4 B, float As,
+                                         float Ag, float c_prev, float& c_out, float& h_out) {
+  const float ig = act_sig_t(tab, __builtin_fmaf((float)acc[0], As, B.x));
+  const float fg = act_sig_t(tab, __builtin_fmaf((float)acc[1], As, B.y));
+  const float gg = __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf((float)acc[2], Ag, B.z)), -1.0f);
+  const float og = act_sig_t(tab, __builtin_fmaf((float)acc[3], As, B.w));
+  float c = __builtin_fmaf(fg, c_prev, ig * gg);
+  // opaque here: otherwise the backend folds fma + the later f32->f16 store conversion into
+  // v_fma_mixlo_f16 (one rounding straight to f16), which is not the contract's fp32 c
+  // rounded to fp16
+  asm volatile("" : "+v"(c));
+  const float tc = __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf(c, 8.0f, 64.0f)), -1.0f);
   c_out = c;
-  h_out = (1.0f - ec) / ((1.0f + eo) * (1.0f + ec));
+  h_out = og * tc;
 }
 
 // f32 -> f16 round-half-even and f16 -> f32 on the hardware converters (v_cvt_f16_f32 /
