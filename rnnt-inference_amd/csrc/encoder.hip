@@ -87,9 +87,6 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   const int q = lane >> 4, col = lane & 15;
   const int u0 = (m0 >> 2) + wm * 16 + q * 4;  // this lane's 4 consecutive units
   const int nb = n0 + wn * 128 + col;          // batch row of j = 0 (row j: nb + 16 j)
-  uint2 cpre[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) cpre[j] = *(const uint2*)(a.c + (size_t)(nb + 16 * j) * H + u0);
   // ---- LDS-DMA staging: wave w moves pieces 2w, 2w+1 (16 rows x 64 B each) of A and of B;
   // lane l of piece p lands at LDS slot 64p + l = row*4 + (col16 ^ h(row)), so it fetches
   // row 16p + (l>>2), 16-byte column (l&3) ^ h, where h(row) depends on l>>4 only.
@@ -101,12 +98,14 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #else
   const int lm0 = m0, ln0 = n0;
 #endif
-  const int8_t* wa0 = a.W + (size_t)(lm0 + ra) * K + gcol;
-  const int8_t* wa1 = a.W + (size_t)(lm0 + rb) * K + gcol;
-  const int8_t* xb0 = a.x + (size_t)(ln0 + ra) * a.I + gcol;
-  const int8_t* xb1 = a.x + (size_t)(ln0 + rb) * a.I + gcol;
-  const int8_t* hb0 = a.h_in + (size_t)(ln0 + ra) * H + gcol - a.I;
-  const int8_t* hb1 = a.h_in + (size_t)(ln0 + rb) * H + gcol - a.I;
+  // per-lane 32-bit offsets from wave-uniform (SGPR) tile bases: global_load_lds with saddr
+  const uint32_t oA = (uint32_t)(ra * K + gcol), oX = (uint32_t)(ra * a.I + gcol), oH = (uint32_t)(ra * H + gcol);
+  const int8_t* wbase0 = a.W + (size_t)lm0 * K;
+  const int8_t* wbase1 = wbase0 + (size_t)16 * K;
+  const int8_t* xbase0 = a.x + (size_t)ln0 * a.I;
+  const int8_t* xbase1 = xbase0 + (size_t)16 * a.I;
+  const int8_t* hbase0 = a.h_in + (size_t)ln0 * H - a.I;
+  const int8_t* hbase1 = hbase0 + (size_t)16 * H;
   lds_char* lds = (lds_char*)(lds_void*)smem;
   const int pa = wave * 2 * 1024;
 
@@ -116,12 +115,28 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #endif
     const int k = ks * BK;
     lds_char* st = lds + (ks % NSTAGE) * STAGE_BYTES + pa;
-    __builtin_amdgcn_global_load_lds((glb_void*)(wa0 + k), (lds_void*)st, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((glb_void*)(wa1 + k), (lds_void*)(st + 1024), 16, 0, 0);
-    const int8_t* b0 = k < a.I ? xb0 + k : hb0 + k;
-    const int8_t* b1 = k < a.I ? xb1 + k : hb1 + k;
-    __builtin_amdgcn_global_load_lds((glb_void*)b0, (lds_void*)(st + A_BYTES), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((glb_void*)b1, (lds_void*)(st + A_BYTES + 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)(wbase0 + k + oA), (lds_void*)st, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((glb_void*)(wbase1 + k + oA), (lds_void*)(st + 1024), 16, 0, 0);
+    if (k < a.I) {
+      __builtin_amdgcn_global_load_lds((glb_void*)(xbase0 + k + oX), (lds_void*)(st + A_BYTES), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void*)(xbase1 + k + oX), (lds_void*)(st + A_BYTES + 1024), 16, 0, 0);
+    } else {
+      __builtin_amdgcn_global_load_lds((glb_void*)(hbase0 + k + oH), (lds_void*)(st + A_BYTES), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void*)(hbase1 + k + oH), (lds_void*)(st + A_BYTES + 1024), 16, 0, 0);
+    }
+  };
+
+  // the tile's fp16 cell state (256 rows x 64 units x 2 B = 32 KiB) DMA'd into the ring buffer
+  // of stage nK-4 once it has been read; piece p, lane l: row 8p + (l>>3), 16-B chunk l&7
+  const int cbuf = ((nK - 4) % NSTAGE) * STAGE_BYTES;
+  auto issue_c = [&]() __attribute__((always_inline)) {
+    const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + (lane & 7) * 8;
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) {
+      const int p = wave * 4 + pc;
+      __builtin_amdgcn_global_load_lds((glb_void*)(cb + (size_t)(8 * p + (lane >> 3)) * H), (lds_void*)(lds + cbuf + p * 1024),
+                                       16, 0, 0);
+    }
   };
 
   v4i acc[4][8];
@@ -134,16 +149,18 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // column lane>>4; +16 rows is +1 KiB in the image (the swizzle repeats every 16 rows)
   const int fa = swz(wm * 64 + col, q), fb = A_BYTES + swz(wn * 128 + col, q);
 
+  static_assert(NSTAGE == 4, "cell-state DMA placement assumes a 4-deep ring");
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
   for (int ks = 0; ks < nK; ++ks) {
-    // stages issued after ks that may stay in flight: min(NSTAGE - 2, nK - 1 - ks)
-    const int rem = nK - 1 - ks;
-    if (NSTAGE >= 5 && rem >= 3) stage_barrier<3 * GLDS_PER_STAGE>();
-    else if (NSTAGE >= 4 && rem >= 2) stage_barrier<2 * GLDS_PER_STAGE>();
+    // stages issued after ks that may stay in flight: min(NSTAGE - 2, nK - 1 - ks), plus the
+    // cell-state DMA issued at step nK-3 into stage nK-4's buffer (read at step nK-4)
+    const int rem = (nK - 1 - ks < 2 ? nK - 1 - ks : 2) + (ks >= nK - 2 ? 1 : 0);
+    if (rem >= 2) stage_barrier<2 * GLDS_PER_STAGE>();
     else if (rem >= 1) stage_barrier<GLDS_PER_STAGE>();
     else stage_barrier<0>();
     if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
+    else if (ks + NSTAGE - 1 == nK) issue_c();
     const int8_t* st = smem + (ks % NSTAGE) * STAGE_BYTES;
     v4i fra[4], frb[8];
 #pragma unroll
@@ -154,18 +171,20 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #pragma unroll
     for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fra[i]), "v"(frb[i]), "v"(frb[i + 4]));
 #else
+    __builtin_amdgcn_s_setprio(1);  // MFMA cluster at raised priority (guide T5)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
 #endif
   }
+  stage_barrier<0>();  // the cell-state DMA has landed for every wave
 #ifdef RNNT_DEV_NO_EPI  // development ablation: main loop only
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" ::"v"(acc[i][j]));
-  asm volatile("" ::"v"(cpre[0].x), "v"(cpre[7].y));
   return;
 #endif
 
@@ -178,8 +197,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int n = nb + 16 * j;
-    const float cin[4] = {h2f((uint16_t)(cpre[j].x & 0xffff)), h2f((uint16_t)(cpre[j].x >> 16)),
-                          h2f((uint16_t)(cpre[j].y & 0xffff)), h2f((uint16_t)(cpre[j].y >> 16))};
+    const uint2 cv = *(const uint2*)(smem + cbuf + (n - n0) * 128 + (u0 - (m0 >> 2)) * 2);
+    const float cin[4] = {h2f((uint16_t)(cv.x & 0xffff)), h2f((uint16_t)(cv.x >> 16)), h2f((uint16_t)(cv.y & 0xffff)),
+                          h2f((uint16_t)(cv.y >> 16))};
     uint32_t cw[2] = {0u, 0u}, hq = 0, yq = 0;
     float hv[4];
 #pragma unroll

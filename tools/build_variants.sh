@@ -5,7 +5,12 @@ set -e
 cd "$(dirname "$0")/../rnnt-inference_amd/csrc"
 OUTD=../../build_dev
 mkdir -p $OUTD
-build() { /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -w "${@:2}" engine.hip encoder.hip decoder.hip -o $OUTD/lib_$1.so; }
+build() {
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -w "${@:2}" -c encoder.hip -o $OUTD/enc_$1.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c engine.hip -o $OUTD/eng_$1.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c decoder.hip -o $OUTD/dec_$1.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUTD/eng_$1.o $OUTD/dec_$1.o $OUTD/enc_$1.o -o $OUTD/lib_$1.so
+}
 for v in "$@"; do
   case $v in
     base) build base ;;
