@@ -10,9 +10,12 @@ offline, so the query / response types are plain Python):
                   sorts, takes <= batch_size samples per batch, runs encode+decode on its GPU
                   and completes each sample with its int32 token row (res_len*4 bytes,
                   QuerySamplesComplete, torch_sut.cpp:221-236).
-Multi-GPU: one process per GPU, each with its own engine; a query's sorted samples are dealt
-to ranks in batch-sized chunks (snake order, so every rank gets the same length mix).  There
-is no data-path collective: results are completed per rank.
+Multi-GPU: one process per GPU, each with its own engine(s); a query's sorted samples are
+dealt to ranks in batch-sized chunks (snake order, so every rank gets the same length mix).
+There is no data-path collective: results are completed per rank.  Within a GPU, several
+engines (each with its own HIP stream and host thread, like the reference's INTER worker
+threads, torch_sut.cpp:143-182) keep batches in flight; encoders take turns so one batch's
+latency-bound greedy decode overlaps the next batch's encoder.
 """
 from dataclasses import dataclass
 
@@ -83,23 +86,51 @@ def deal_batches(sorted_samples, batch_size, rank=0, world=1):
 
 class OfflineSUT:
     def __init__(self, engine, qsl, batch_size=1024, rank=0, world=1, on_complete=None):
-        self.engine, self.qsl, self.batch_size = engine, qsl, batch_size
+        """engine: one Engine, or a list of Engines on this GPU (one batch in flight each)."""
+        self.engines = list(engine) if isinstance(engine, (list, tuple)) else [engine]
+        self.engine = self.engines[0]
+        self.qsl, self.batch_size = qsl, batch_size
         self.rank, self.world = rank, world
         self.on_complete = on_complete
         self.responses = {}
 
     def issue_queries(self, samples):
+        import threading
         import torch
         batches = deal_batches(self.qsl.sort(samples), self.batch_size, self.rank, self.world)
-        pending = []
-        for batch in batches:
-            x, lens = self.qsl.assemble([s.index for s in batch])
-            n = len(batch)
-            res = torch.empty((n, self.engine.max_res), dtype=torch.int32, device="cuda")
-            rl = torch.empty(n, dtype=torch.int32, device="cuda")
-            self.engine.infer(torch.from_numpy(x).cuda(), torch.from_numpy(lens).cuda(), lens[:n], res, rl, n=n)
-            pending.append((batch, res, rl))
-        for batch, res, rl in pending:
+        k = len(self.engines)
+        streams = [torch.cuda.Stream() for _ in range(k)] if k > 1 else [torch.cuda.current_stream()]
+        done = [None] * len(batches)
+        enc_lock = threading.Lock()
+
+        def worker(j):
+            eng, st = self.engines[j], streams[j]
+            for bi in range(j, len(batches), k):
+                batch = batches[bi]
+                x, lens = self.qsl.assemble([s.index for s in batch])
+                n = len(batch)
+                with torch.cuda.stream(st):
+                    xd = torch.from_numpy(x).cuda()
+                    ld = torch.from_numpy(lens).cuda()
+                    res = torch.empty((n, eng.max_res), dtype=torch.int32, device="cuda")
+                    rl = torch.empty(n, dtype=torch.int32, device="cuda")
+                with enc_lock:
+                    eng.encode(xd, ld, lens[:n], n=n, stream=st)
+                    st.synchronize()
+                eng.decode(res, rl, stream=st)
+                done[bi] = (batch, res, rl, xd, ld)
+
+        if k == 1:
+            worker(0)
+        else:
+            ths = [threading.Thread(target=worker, args=(j,)) for j in range(k)]
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+        for st in streams:
+            st.synchronize()
+        for batch, res, rl, _, _ in done:
             self.query_samples_complete(batch, res, rl)
 
     def query_samples_complete(self, batch, res, res_len):

@@ -89,3 +89,24 @@ def test_offline_sut_end_to_end(dec, model, oracle):
         fo = oracle.encoder_i8(model, x, np.array([L], np.int32))
         ro, rlo, _ = oracle.greedy_decode(model, fo, np.array([(L + 1) // 2], np.int32))
         np.testing.assert_array_equal(sut.responses[s.id], ro[0, : rlo[0]])
+
+
+def test_offline_sut_batches_in_flight(dec, model):
+    """Two engines on one GPU (own stream + host thread each, encoders taking turns) give the
+    same responses as one engine: the pipelining is pure scheduling."""
+    from rnnt_amd.engine import Engine
+    from rnnt_amd.sut import OfflineSUT, QuerySample, RNNTQSL
+    lengths = np.minimum(synthetic.devclean_lengths(53, seed=41), 128)
+    qsl = RNNTQSL.synthetic(lengths, seed=42)
+    samples = [QuerySample(id=i, index=i) for i in range(len(lengths))]
+    one = OfflineSUT(dec.engine, qsl, batch_size=12)
+    one.issue_queries(samples)
+    e2 = Engine(model, device=0, max_batch=64, max_frames=128)
+    try:
+        two = OfflineSUT([dec.engine, e2], qsl, batch_size=12)
+        two.issue_queries(samples)
+    finally:
+        e2.close()
+    assert sorted(two.responses) == sorted(one.responses)
+    for k in one.responses:
+        np.testing.assert_array_equal(two.responses[k], one.responses[k])

@@ -16,3 +16,8 @@ for P in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_I
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/pmc$i -o pmc -- $BENCH > $OUT/pmc$i.log 2>&1
 done
+# condense on the box (the raw per-dispatch CSVs are far larger than what gpurun copies back)
+PREFIX=${PREFIX:-$OUT/summary/r}
+python3 tools/summarize_profile.py $OUT $PREFIX
+find $OUT -name "*_kernel_trace.csv" -delete
+find $OUT -name "*_counter_collection.csv" -size +8M -delete
