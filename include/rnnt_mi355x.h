@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RNNT_ABI_VERSION 1
+#define RNNT_ABI_VERSION 2
 
 #define RNNT_OK 0
 #define RNNT_EINVAL (-22)
@@ -79,7 +79,7 @@ void rnnt_engine_destroy(rnnt_engine* e);
  * the same lengths on the host (drive the active-tile schedule; may be NULL = all T frames).
  * Keeps the encoder output (f, f_lens = ceil(lens/2)) in the engine for rnnt_engine_decode; if
  * f_out != NULL also writes f there, device fp32 [ceil(T/2)][n_pad][1024].
- * n_pad must be >= n, a multiple of 128, <= max_batch rounded up to 128. */
+ * n_pad must be >= n, a multiple of 256, <= max_batch rounded up to 256. */
 int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
                        int T, int n, int n_pad, float* f_out, void* stream);
 
@@ -90,6 +90,19 @@ int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
 /* encode + decode. */
 int rnnt_engine_infer(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host, int T,
                       int n, int n_pad, int32_t* res, int32_t* res_len, int max_res, void* stream);
+
+/* ---- fp32 transcription (BASELINE config 2; the reference's run_mode="f32" encoder,
+ * models/modeling_rnnt.py:116-144 with torch LSTM layers).  Weights in the checkpoint's natural
+ * layouts: wih[l] fp32 [4096][I_l] (I = 240, 1024, 2048, 1024, 1024), whh[l] fp32 [4096][1024],
+ * bih[l] / bhh[l] fp32 [4096] (gate order i,f,g,o).  Optional; loaded once per engine. */
+int rnnt_engine_load_f32_encoder(rnnt_engine* e, const float* const* wih, const float* const* whh,
+                                 const float* const* bih, const float* const* bhh);
+/* feats device fp32 [T][n_pad][256] (channels 240..255 ignored), lens device int32 [n_pad];
+ * f_out device fp32 [ceil(T/2)][n_pad][1024].  n_pad a multiple of 64.  Arithmetic: k-ordered fp32
+ * fma chains (b_ih + x.W_ih^T, b_hh + h.W_hh^T) on v_mfma_f32_16x16x4_f32, exact vs the CPU
+ * restatement (oracle_encoder_f32). */
+int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const int32_t* lens, int T, int n, int n_pad,
+                           float* f_out, void* stream);
 
 /* ---- in-run measurement (bench.py's roofline leg): HIP events recorded on the launch stream
  * around each call's encoder kernels and decoder kernels; rnnt_engine_get_stats synchronises

@@ -92,7 +92,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // row 16p + (l>>2), 16-byte column (l&3) ^ h, where h(row) depends on l>>4 only.
   const int hx = (0x1320 >> ((lane >> 4) * 4)) & 3;
   const int gcol = ((lane & 3) ^ hx) * 16;
-  const int ra = wave * 32 + (lane >> 2), rb = ra + 16;
+  const int ra = wave * 32 + (lane >> 2);  // first row of this wave's two 16-row pieces (second: +16)
 #ifdef RNNT_DEV_SAME_TILE  // development ablation: every workgroup stages tile (0, 0) (L2-resident)
   const int lm0 = 0, ln0 = 0;
 #else

@@ -1,0 +1,130 @@
+// encoder_f32.hip -- fp32 transcription (BASELINE config 2: the encoder LSTM stack in fp32).
+//
+// The reference's run_mode="f32" encoder (models/modeling_rnnt.py:116-144 with torch LSTM
+// layers, the `P.lstm` op of the f32 graph) with the fp32 restatement's arithmetic
+// (oracle_lstm_f32_layer): per gate row, ax = b_ih + x.W_ih^T and ah = b_hh + h.W_hh^T as two
+// k-ordered fp32 fma chains, gate = ax + ah, Cephes-exp sigmoid / tanh, c = f*c + i*g,
+// h = o*tanh(c).  The chains run on v_mfma_f32_16x16x4_f32, which is bit-identical to a
+// k-ordered fmaf chain on gfx950 (tools/probe), so the output is bit-exact with the CPU
+// restatement (and within the reference's fp32 tolerance through it).
+//
+// Layouts: gate rows interleaved (packed row 4u+g), every k axis chain-permuted inside 32-wide
+// blocks (chain_pos), so one lane's 8 consecutive floats feed 8 chained MFMAs.  One launch =
+// one layer x one timestep; workgroup = 4 waves x (16 gate rows) x 64 batch rows.
+#include "rnnt_device.hpp"
+#include "encoder_f32.hpp"
+
+namespace rnnt {
+
+#define MFMA4(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+
+// acc[j] += chain over k in [0, K) of A(row) . B_j, K a multiple of 16; a/b point at this
+// lane's first element (row base + 8q); blocks of 32 feed 8 MFMAs, a final half block 4.
+__device__ __forceinline__ void chain_rows(const float* __restrict__ a, const float* const* b, int K, v4f* acc) {
+  const int nb = K >> 5;
+  for (int blk = 0; blk < nb; ++blk) {
+    const float4 a0 = *(const float4*)(a + 32 * blk), a1 = *(const float4*)(a + 32 * blk + 4);
+    float4 b0[4], b1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      b0[j] = *(const float4*)(b[j] + 32 * blk);
+      b1[j] = *(const float4*)(b[j] + 32 * blk + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] = MFMA4(a0.x, b0[j].x, acc[j]);
+      acc[j] = MFMA4(a0.y, b0[j].y, acc[j]);
+      acc[j] = MFMA4(a0.z, b0[j].z, acc[j]);
+      acc[j] = MFMA4(a0.w, b0[j].w, acc[j]);
+      acc[j] = MFMA4(a1.x, b1[j].x, acc[j]);
+      acc[j] = MFMA4(a1.y, b1[j].y, acc[j]);
+      acc[j] = MFMA4(a1.z, b1[j].z, acc[j]);
+      acc[j] = MFMA4(a1.w, b1[j].w, acc[j]);
+    }
+  }
+  if (K & 16) {  // half block: instructions i = 0..3 (k = 32 nb + 4i + q)
+    const float4 a0 = *(const float4*)(a + 32 * nb);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 b0 = *(const float4*)(b[j] + 32 * nb);
+      acc[j] = MFMA4(a0.x, b0.x, acc[j]);
+      acc[j] = MFMA4(a0.y, b0.y, acc[j]);
+      acc[j] = MFMA4(a0.z, b0.z, acc[j]);
+      acc[j] = MFMA4(a0.w, b0.w, acc[j]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) lstm_f32_step_kernel(EncF32StepArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+  const int gt = blockIdx.x * 4 + wave;  // 16-row gate tile = units 4gt .. 4gt+3
+  const int n0 = blockIdx.y * 64;
+  const int row = gt * 16 + c;           // packed gate row fed by this lane (A operand)
+  const float* bx[4];
+  const float* bh[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bx[j] = a.x + (size_t)(n0 + j * 16 + c) * a.Ip + 8 * q;
+    bh[j] = a.h_in + (size_t)(n0 + j * 16 + c) * H + 8 * q;
+  }
+  v4f ax[4], ah[4];
+  const float4 bi = *(const float4*)(a.bih + gt * 16 + 4 * q), bhv = *(const float4*)(a.bhh + gt * 16 + 4 * q);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ax[j] = v4f{bi.x, bi.y, bi.z, bi.w};
+    ah[j] = v4f{bhv.x, bhv.y, bhv.z, bhv.w};
+  }
+  chain_rows(a.wih + (size_t)row * a.Ip + 8 * q, bx, a.I, ax);
+  chain_rows(a.whh + (size_t)row * H + 8 * q, bh, H, ah);
+  // C/D: lane (q, c) holds rows 4q..4q+3 of the tile = gates i,f,g,o of unit 4gt+q, batch row c
+  const int u = gt * 4 + q;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + j * 16 + c;
+    if (n >= a.n) continue;
+    const float ig = det_sigmoid(ax[j][0] + ah[j][0]);
+    const float fg = det_sigmoid(ax[j][1] + ah[j][1]);
+    const float gg = det_tanh(ax[j][2] + ah[j][2]);
+    const float og = det_sigmoid(ax[j][3] + ah[j][3]);
+    float* cp = a.c + (size_t)n * H + u;
+    const float cn = fg * *cp + ig * gg;
+    *cp = cn;
+    const float hh = og * det_tanh(cn);
+    a.h_out[(size_t)n * H + chain_pos(u)] = hh;
+    if (a.mode == ENC_F32_NEXT) {
+      a.y[(size_t)n * H + chain_pos(u)] = hh;
+    } else if (a.mode == ENC_F32_STACKED) {
+      // StackTime.forward_f32 (modeling_rnnt.py:314-324): frame t -> stacked frame t/2, half
+      // t%2, frames t >= x_lens[n] zeroed, odd-T pad frame zero
+      float* dst = a.y + (size_t)n * 2 * H + chain_pos(u);
+      dst[a.half * H] = a.t < a.lens[n] ? hh : 0.0f;
+      if (a.zero_next) dst[H] = 0.0f;
+    } else {
+      a.y[(size_t)n * H + u] = hh;
+    }
+  }
+}
+
+// features [T][n_pad][256] natural -> [T][n_pad][256] chain-permuted (channels >= 240 are 0)
+__global__ void permute_feats_kernel(const float* __restrict__ x, int64_t rows, float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * FEAT) return;
+  const int64_t r = i / FEAT;
+  const int k = (int)(i % FEAT);
+  y[r * FEAT + chain_pos(k)] = x[i];
+}
+
+int launch_lstm_f32_step(const EncF32StepArgs& a, hipStream_t st) {
+  if (a.n <= 0) return 0;
+  if (a.I % 16 || a.Ip % 32 || a.Ip < a.I) return -1;
+  hipLaunchKernelGGL(lstm_f32_step_kernel, dim3(G4 / 64, (a.n + 63) / 64), dim3(256), 0, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_permute_feats(const float* x, int64_t rows, float* y, hipStream_t st) {
+  const int64_t total = rows * FEAT;
+  hipLaunchKernelGGL(permute_feats_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, rows, y);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace rnnt

@@ -1,0 +1,30 @@
+// encoder_f32.hpp -- launch interface of the fp32 encoder kernels (engine-internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rnnt {
+
+enum EncF32Mode { ENC_F32_NEXT = 0, ENC_F32_STACKED = 1, ENC_F32_FINAL = 2 };
+
+struct EncF32StepArgs {
+  const float* wih;     // [4096][Ip] packed rows (4u+g), chain-permuted k, zero past I
+  const float* whh;     // [4096][1024] packed rows, chain-permuted k
+  const float* bih;     // [4096] packed
+  const float* bhh;     // [4096] packed
+  const float* x;       // this frame's input rows [n_pad][Ip], chain-permuted
+  const float* h_in;    // [n_pad][1024] chain-permuted
+  float* h_out;         // [n_pad][1024] chain-permuted
+  float* c;             // [n_pad][1024] natural
+  float* y;             // NEXT: [n_pad][1024] chain-permuted; STACKED: [n_pad][2048] chain-permuted;
+                        // FINAL: [n_pad][1024] natural (f)
+  const int32_t* lens;  // STACKED masking
+  int I, Ip;            // real / padded input width (240/256, 1024/1024, 2048/2048)
+  int n;                // rows to compute (multiple-of-64 tiles launched; rows >= n skipped)
+  int mode, t, half, zero_next;
+};
+
+int launch_lstm_f32_step(const EncF32StepArgs& a, hipStream_t st);
+int launch_permute_feats(const float* x, int64_t rows, float* y, hipStream_t st);
+
+}  // namespace rnnt

@@ -16,6 +16,7 @@
 #include "../../include/rnnt_mi355x.h"
 #include "decoder.hpp"
 #include "encoder.hpp"
+#include "encoder_f32.hpp"
 #include "rnnt_device.hpp"
 
 using namespace rnnt;
@@ -62,6 +63,12 @@ struct rnnt_engine {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_enc;
   std::vector<std::array<hipEvent_t, 3>> ev_dec;
   int64_t step_launches = 0, decode_steps = 0, encode_calls = 0, decode_calls = 0;
+  // optional fp32 encoder (rnnt_engine_load_f32_encoder) and its lazily sized workspace
+  bool f32_loaded = false;
+  float *f32_wih[5] = {}, *f32_whh[5] = {}, *f32_bih[5] = {}, *f32_bhh[5] = {};
+  std::vector<void*> f32_ws;
+  size_t f32_ws_T = 0, f32_ws_np = 0;
+  float *f32_x = nullptr, *f32_ya = nullptr, *f32_xs = nullptr, *f32_yb = nullptr, *f32_h[2] = {}, *f32_c = nullptr;
 };
 
 static hipEvent_t new_event(hipStream_t st) {
@@ -196,6 +203,7 @@ extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   for (void* p : e->allocs) (void)hipFree(p);
+  for (void* p : e->f32_ws) (void)hipFree(p);
   if (e->host_flags) (void)hipHostFree(e->host_flags);
   for (auto ev : e->poll_ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -509,5 +517,118 @@ extern "C" int rnnt_op_stack_time(rnnt_engine* e, const int8_t* x, const int32_t
   hipLaunchKernelGGL(stack_time_kernel, dim3(n_pad, (T + 1) / 2), dim3(64), 0, pick(e, stream), x, x_lens, T, n_pad,
                      C, y);
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------- fp32 encoder (config 2)
+static const int F32_I[5] = {240, 1024, 2048, 1024, 1024};   // real input widths
+static const int F32_IP[5] = {256, 1024, 2048, 1024, 1024};  // padded to 32 (chain blocks)
+
+extern "C" int rnnt_engine_load_f32_encoder(rnnt_engine* e, const float* const* wih, const float* const* whh,
+                                            const float* const* bih, const float* const* bhh) {
+  if (!e || !wih || !whh || !bih || !bhh) return fail(RNNT_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(e->device));
+  for (int l = 0; l < 5; ++l) {
+    if (!wih[l] || !whh[l] || !bih[l] || !bhh[l]) return fail(RNNT_EINVAL, "null fp32 encoder weight");
+    const int I = F32_I[l], Ip = F32_IP[l];
+    std::vector<float> wi((size_t)G4 * Ip, 0.0f), wh((size_t)G4 * H), bi(G4), bh(G4);
+    for (int g = 0; g < 4; ++g)
+      for (int u = 0; u < H; ++u) {
+        const int src = g * H + u, dst = 4 * u + g;  // gate-interleaved rows
+        for (int k = 0; k < I; ++k) wi[(size_t)dst * Ip + chain_pos(k)] = wih[l][(size_t)src * I + k];
+        for (int k = 0; k < H; ++k) wh[(size_t)dst * H + chain_pos(k)] = whh[l][(size_t)src * H + k];
+        bi[dst] = bih[l][src];
+        bh[dst] = bhh[l][src];
+      }
+    int r = upload(e, &e->f32_wih[l], wi);
+    if (!r) r = upload(e, &e->f32_whh[l], wh);
+    if (!r) r = upload(e, &e->f32_bih[l], bi);
+    if (!r) r = upload(e, &e->f32_bhh[l], bh);
+    if (r) return r;
+  }
+  e->f32_loaded = true;
+  return 0;
+}
+
+static int f32_workspace(rnnt_engine* e, int T, int n_pad) {
+  if ((size_t)T <= e->f32_ws_T && (size_t)n_pad <= e->f32_ws_np) return 0;
+  for (void* p : e->f32_ws) (void)hipFree(p);
+  e->f32_ws.clear();
+  const size_t Tp = (T + 1) / 2, NH = (size_t)n_pad * H;
+  auto al = [&](float** p, size_t count) -> int {
+    void* q = nullptr;
+    if (hipMalloc(&q, count * sizeof(float) + 256) != hipSuccess) return fail(RNNT_ENOMEM, "hipMalloc failed (f32)");
+    e->f32_ws.push_back(q);
+    *p = (float*)q;
+    return 0;
+  };
+  int r = al(&e->f32_x, (size_t)T * n_pad * FEAT);
+  if (!r) r = al(&e->f32_ya, (size_t)T * NH);
+  if (!r) r = al(&e->f32_xs, Tp * NH * 2);
+  if (!r) r = al(&e->f32_yb, Tp * NH);
+  if (!r) r = al(&e->f32_h[0], NH);
+  if (!r) r = al(&e->f32_h[1], NH);
+  if (!r) r = al(&e->f32_c, NH);
+  if (r) {
+    e->f32_ws_T = e->f32_ws_np = 0;
+    return r;
+  }
+  e->f32_ws_T = T;
+  e->f32_ws_np = n_pad;
+  return 0;
+}
+
+// one fp32 layer over T steps; x / y advance by their per-frame strides
+static int run_f32_layer(rnnt_engine* e, int l, int T, int n, int n_pad, const float* x, int mode, float* y,
+                         const int32_t* lens, int stacked_T, hipStream_t st) {
+  const size_t NH = (size_t)n_pad * H;
+  HIPCHK(hipMemsetAsync(e->f32_h[0], 0, NH * sizeof(float), st));
+  HIPCHK(hipMemsetAsync(e->f32_c, 0, NH * sizeof(float), st));
+  for (int t = 0; t < T; ++t) {
+    EncF32StepArgs a{};
+    a.wih = e->f32_wih[l];
+    a.whh = e->f32_whh[l];
+    a.bih = e->f32_bih[l];
+    a.bhh = e->f32_bhh[l];
+    a.I = F32_I[l];
+    a.Ip = F32_IP[l];
+    a.x = x + (size_t)t * n_pad * a.Ip;
+    a.h_in = e->f32_h[t & 1];
+    a.h_out = e->f32_h[(t + 1) & 1];
+    a.c = e->f32_c;
+    a.n = n;
+    a.mode = mode;
+    a.lens = lens;
+    if (mode == ENC_F32_STACKED) {
+      a.y = y + (size_t)(t / 2) * NH * 2;
+      a.t = t;
+      a.half = t & 1;
+      a.zero_next = ((t & 1) == 0 && t + 1 == stacked_T);
+    } else {
+      a.y = y + (size_t)t * NH;
+    }
+    if (launch_lstm_f32_step(a, st)) return fail(RNNT_EDEVICE, "fp32 lstm step launch failed");
+  }
+  return 0;
+}
+
+extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const int32_t* lens, int T, int n, int n_pad,
+                                      float* f_out, void* stream) {
+  if (!e || !feats || !lens || !f_out) return fail(RNNT_EINVAL, "null argument");
+  if (!e->f32_loaded) return fail(RNNT_EINVAL, "fp32 encoder weights not loaded (rnnt_engine_load_f32_encoder)");
+  if (T <= 0 || T > e->opts.max_frames || n <= 0 || n_pad < n || n_pad % 64)
+    return fail(RNNT_EINVAL, "T / n / n_pad out of range (n_pad a multiple of 64)");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = pick(e, stream);
+  int r = f32_workspace(e, T, n_pad);
+  if (r) return r;
+  const int Tp = (T + 1) / 2;
+  if (launch_permute_feats(feats, (int64_t)T * n_pad, e->f32_x, st)) return fail(RNNT_EDEVICE, "permute launch failed");
+  // Transcription.forward (modeling_rnnt.py:116-144): pre_rnn 2 layers -> StackTime -> post_rnn 3 layers
+  if ((r = run_f32_layer(e, 0, T, n, n_pad, e->f32_x, ENC_F32_NEXT, e->f32_ya, lens, T, st))) return r;
+  if ((r = run_f32_layer(e, 1, T, n, n_pad, e->f32_ya, ENC_F32_STACKED, e->f32_xs, lens, T, st))) return r;
+  if ((r = run_f32_layer(e, 2, Tp, n, n_pad, e->f32_xs, ENC_F32_NEXT, e->f32_yb, lens, Tp, st))) return r;
+  if ((r = run_f32_layer(e, 3, Tp, n, n_pad, e->f32_yb, ENC_F32_NEXT, e->f32_ya, lens, Tp, st))) return r;
+  if ((r = run_f32_layer(e, 4, Tp, n, n_pad, e->f32_ya, ENC_F32_FINAL, f_out, lens, Tp, st))) return r;
   return 0;
 }

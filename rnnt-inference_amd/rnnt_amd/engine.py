@@ -102,6 +102,23 @@ class Engine:
                                          _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))
         _lib.check(rc, "rnnt_engine_infer")
 
+    # ---------------------------------------------------------------- fp32 transcription
+    def load_f32_encoder(self, layers):
+        """layers: 5 x (W_ih [4096, I], W_hh [4096, 1024], b_ih, b_hh) fp32 in the checkpoint's
+        natural layout (weights.enc_layer_params), I = 240, 1024, 2048, 1024, 1024."""
+        keep = [[np.ascontiguousarray(l[i], np.float32) for l in layers] for i in range(4)]
+        arrs = [(C.c_void_p * 5)(*[a.ctypes.data for a in col]) for col in keep]
+        _lib.check(self._lib.rnnt_engine_load_f32_encoder(self._h, *arrs), "rnnt_engine_load_f32_encoder")
+
+    def encode_f32(self, feats, lens, n, f_out, stream=None):
+        """Transcription in fp32 (config 2): feats cuda fp32 [T, n_pad, 256], lens cuda int32
+        [n_pad] -> f_out cuda fp32 [ceil(T/2), n_pad, 1024]."""
+        T, n_pad, ch = feats.shape
+        assert ch == R.PADDED_INPUT_SIZE and feats.is_contiguous() and f_out.is_contiguous()
+        rc = self._lib.rnnt_engine_encode_f32(self._h, _ptr(feats), _ptr(lens), T, n, n_pad, _ptr(f_out),
+                                              _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_encode_f32")
+
     # ---------------------------------------------------------------- measurement
     def set_profiling(self, on=True):
         _lib.check(self._lib.rnnt_engine_set_profiling(self._h, int(bool(on))), "rnnt_engine_set_profiling")
