@@ -382,8 +382,9 @@ static void dec_w_free(dec_w* d) {
 }
 
 /* Prediction.forward (modeling_rnnt.py:183-205): SOS -> zero embedding; 2-layer LSTM.
- * bf16: gates = b_ih+b_hh then chain over x then h (lstm_amx_bf16 fused bias, :170-172);
- * fp32: (b_ih + x.W_ih) + (b_hh + h.W_hh).  h stored bf16 in bf16 mode, c fp32. */
+ * gates = (b_ih + x.W_ih) + (b_hh + h.W_hh), each a k-ordered fmaf chain (torch.nn.LSTM's
+ * ax + ah form; the two chains run side by side on the GPU).  h stored bf16 in bf16 mode
+ * (lstm_amx_bf16), c fp32. */
 static void pred_row(const dec_w* d, int pre_g, const float* ph, const float* pc, float* gh,
                      float* gc) {
   float x[P], ax[4 * P], ah[4 * P];
@@ -394,20 +395,13 @@ static void pred_row(const dec_w* d, int pre_g, const float* ph, const float* pc
   for (int l = 0; l < 2; ++l) {
     const float* hp = ph + l * P;
     const float* cp = pc + l * P;
-    if (d->bf16) {
-      for (int r = 0; r < 4 * P; ++r) ax[r] = d->bih[l][r] + d->bhh[l][r];
-      chain_acc(ax, x, d->WihT[l], P, 4 * P);
-      chain_acc(ax, hp, d->WhhT[l], P, 4 * P);
-      memset(ah, 0, sizeof(ah));
-    } else {
-      memcpy(ax, d->bih[l], sizeof(ax));
-      memcpy(ah, d->bhh[l], sizeof(ah));
-      chain_acc(ax, x, d->WihT[l], P, 4 * P);
-      chain_acc(ah, hp, d->WhhT[l], P, 4 * P);
-    }
+    memcpy(ax, d->bih[l], sizeof(ax));
+    memcpy(ah, d->bhh[l], sizeof(ah));
+    chain_acc(ax, x, d->WihT[l], P, 4 * P);
+    chain_acc(ah, hp, d->WhhT[l], P, 4 * P);
     for (int j = 0; j < P; ++j) {
-      float pi = ax[j], pf = ax[P + j], pg = ax[2 * P + j], po = ax[3 * P + j];
-      if (!d->bf16) { pi = pi + ah[j]; pf = pf + ah[P + j]; pg = pg + ah[2 * P + j]; po = po + ah[3 * P + j]; }
+      const float pi = ax[j] + ah[j], pf = ax[P + j] + ah[P + j];
+      const float pg = ax[2 * P + j] + ah[2 * P + j], po = ax[3 * P + j] + ah[3 * P + j];
       const float ig = oracle_sigmoid(pi), fg = oracle_sigmoid(pf);
       const float gg = oracle_tanh(pg), og = oracle_sigmoid(po);
       const float cn = fg * cp[j] + ig * gg;
@@ -422,7 +416,9 @@ static void pred_row(const dec_w* d, int pre_g, const float* ph, const float* pc
 
 /* Joint (modeling_rnnt.py:259-289): F = b_t + f.W1t^T, G = b_p + g.W1p^T (fp32 path:
  * linear1_trans(f) += linear1_pred(g)); y1 = relu(F+G) (bf16 in bf16 mode); logits =
- * b2 + y1.W2^T over the 29 real labels. */
+ * b2 + y1.W2^T over the 29 real labels.  bf16 mode sums y1.W2^T in 4 blocks of 128 k (chain
+ * 0 from b2, chains 1-3 from 0, combined in order): four short chains on four waves of the
+ * GPU's per-step joint instead of one 512-long dependent chain. */
 static void joint_F(const dec_w* d, const float* f, float* F) {
   float fin[H_ENC];
   for (int k = 0; k < H_ENC; ++k) fin[k] = d->bf16 ? bfr(f[k]) : f[k];
@@ -441,7 +437,16 @@ static void joint_logits(const dec_w* d, const float* F, const float* G, float* 
     y1[j] = d->bf16 ? bfr(r) : r;
   }
   memcpy(logits, d->b2, sizeof(float) * NLAB);
-  chain_acc(logits, y1, d->W2T, J, NLAB);
+  if (!d->bf16) {
+    chain_acc(logits, y1, d->W2T, J, NLAB);
+    return;
+  }
+  chain_acc(logits, y1, d->W2T, J / 4, NLAB);
+  for (int b = 1; b < 4; ++b) {
+    float part[NLAB] = {0};
+    chain_acc(part, y1 + b * (J / 4), d->W2T + (size_t)b * (J / 4) * NLAB, J / 4, NLAB);
+    for (int j = 0; j < NLAB; ++j) logits[j] = logits[j] + part[j];
+  }
 }
 static int argmax29(const float* v) {  /* torch.argmax: first maximal index */
   int best = 0;

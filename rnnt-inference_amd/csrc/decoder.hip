@@ -104,33 +104,40 @@ __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
   }
 }
 
-// One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates = (b_ih+b_hh) +
-// chain over [x | h_prev]; c fp32, h bf16.  Grid: x = 8-gate-tile group (128 gate rows, the
-// weights held in registers for the whole launch), y = DEC_ROW_GROUPS workgroups striding over
-// the emit list's 16-row tiles, so each weight fetch is amortised over every tile it serves.
-__global__ void __launch_bounds__(256, 2) dec_pred_kernel(DecArgs a, int layer, int parity) {
+// One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates =
+// (b_ih + chain over x) + (b_hh + chain over h_prev); c fp32, h bf16.  A workgroup (8 waves)
+// owns PRED_TILES gate tiles; wave w runs tile w % PRED_TILES's x chain (first half of the
+// waves) or h chain (second half) -- 80 chained MFMAs and 10 KB of weights per wave, held in
+// registers for the launch -- and the h-chain partials meet the x chains in LDS.  Grid: x =
+// 1280 / (16 PRED_TILES) gate groups, y = row groups striding over the emit list's 16-row
+// tiles (one resident round).
+constexpr int PRED_TILES = 4;
+constexpr int PRED_THREADS = PRED_TILES * 2 * 64;
+constexpr int PRED_ROW_GROUPS = 25;
+__global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int layer, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][XP];
+  __shared__ v4f Hp[PRED_TILES][64];
   __shared__ int rows[16], slots[16], pregs[16];
   const DecState& s = a.s;
   const int cnt = s.count[parity];
   const int ntiles = (cnt + 15) >> 4;
   if ((int)blockIdx.y >= ntiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  const int tile = wave % PRED_TILES, part = wave / PRED_TILES;  // part 0: x chain from b_ih, 1: h from b_hh
   const int* list = s.list + parity * a.Npad;
-  // this wave's weight fragments (2 gate tiles x 20 k-blocks = 160 VGPRs) in one burst, issued
-  // before the first operand staging so the L2 round trip overlaps it
-  const int gt = blockIdx.x * 8 + wave * 2;
-  const uint16_t* w0 = a.w.wp[layer] + (size_t)(gt * 16 + c) * 640 + 8 * q;
-  const uint16_t* w1 = w0 + 16 * 640;
-  uint4 wa[20], wb[20];
+  const int gt = blockIdx.x * PRED_TILES + tile;
+  // k blocks of [W_ih | W_hh]: part p reads blocks 10p .. 10p+9 (offset p*320 in the row)
+  const uint16_t* w0 = a.w.wp[layer] + (size_t)(gt * 16 + c) * 640 + part * P + 8 * q;
+  uint4 wv[P / 32];
 #pragma unroll
-  for (int b = 0; b < 20; ++b) {
-    wa[b] = *(const uint4*)(w0 + 32 * b);
-    wb[b] = *(const uint4*)(w1 + 32 * b);
+  for (int b = 0; b < P / 32; ++b) {
+#ifdef RNNT_DEV_PRED_NOWLOAD
+    wv[b] = uint4{(uint32_t)b, 0u, 0u, 0u};
+#else
+    wv[b] = *(const uint4*)(w0 + 32 * b);
+#endif
   }
-  const float* bias = a.w.bp_lstm[layer];
-  const float4 b0 = *(const float4*)(bias + gt * 16 + 4 * q);
-  const float4 b1 = *(const float4*)(bias + (gt + 1) * 16 + 4 * q);
+  const float4 bias = *(const float4*)((part ? a.w.bhh_p[layer] : a.w.bih_p[layer]) + gt * 16 + 4 * q);
   for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
     if (tid < 16) {
       const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
@@ -139,8 +146,12 @@ __global__ void __launch_bounds__(256, 2) dec_pred_kernel(DecArgs a, int layer, 
       pregs[tid] = row >= 0 ? s.preg[row] : SOS;
     }
     __syncthreads();
-    // stage [x | h_prev] for the 16 listed rows: 16 x 160 float4 groups, 10 per thread
-    for (int i = tid; i < 16 * 160; i += 256) {
+    // stage [x | h_prev] for the 16 listed rows: 16 x 160 float4 groups
+#ifdef RNNT_DEV_PRED_NOSTAGE
+    for (int i = tid; i < 0; i += PRED_THREADS) {
+#else
+    for (int i = tid; i < 16 * 160; i += PRED_THREADS) {
+#endif
       const int mi = i / 160, k = (i % 160) * 4, row = rows[mi];
       float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
       if (row >= 0) {
@@ -165,45 +176,43 @@ __global__ void __launch_bounds__(256, 2) dec_pred_kernel(DecArgs a, int layer, 
       X[mi][chain_pos(k + 3)] = v.w;
     }
     __syncthreads();
-    if (rt == (int)blockIdx.y) {
+    const float* xr = &X[c][part * P + 8 * q];
+    v4f acc = v4f{bias.x, bias.y, bias.z, bias.w};
+#ifndef RNNT_DEV_PRED_NOMFMA
 #pragma unroll
-      for (int b = 0; b < 20; ++b)  // weights are live (waited for) here, behind the first staging
-        asm volatile("" ::"v"(wa[b].x), "v"(wa[b].y), "v"(wa[b].z), "v"(wa[b].w), "v"(wb[b].x), "v"(wb[b].y),
-                     "v"(wb[b].z), "v"(wb[b].w));
-    }
-    const float* xrow = &X[c][8 * q];
-    v4f acc0 = v4f{b0.x, b0.y, b0.z, b0.w}, acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-    for (int b = 0; b < 640 / 32; ++b) {
+    for (int b = 0; b < P / 32; ++b) {
       float x[8];
-      *(float4*)&x[0] = *(const float4*)(xrow + 32 * b);
-      *(float4*)&x[4] = *(const float4*)(xrow + 32 * b + 4);
-      acc0 = chain8(wa[b], x, acc0);
-      acc1 = chain8(wb[b], x, acc1);
+      *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
+      *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
+      acc = chain8(wv[b], x, acc);
     }
+#else
+    asm volatile("" ::"v"(wv[0].x), "v"(wv[9].w), "v"(xr[0]));
+#endif
+    if (part) Hp[tile][lane] = acc;
+    __syncthreads();
     const int row = rows[c];
-    if (row >= 0) {
+    if (!part && row >= 0) {
+      const v4f g = acc + Hp[tile][lane];
       const int sl = slots[c];
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const v4f g = half ? acc1 : acc0;
-        const int u = (gt + half) * 4 + q;
-        const float ig = det_sigmoid(g[0]), fg = det_sigmoid(g[1]), gg = det_tanh(g[2]), og = det_sigmoid(g[3]);
-        const float cp = hc_part(a.hc, row, sl, 2 + layer)[u];
-        const float cn = fg * cp + ig * gg;
-        const float hh = bf_round(og * det_tanh(cn));
-        hc_part(a.hc, row, sl ^ 1, 2 + layer)[u] = cn;
-        hc_part(a.hc, row, sl ^ 1, layer)[u] = hh;
-      }
+      const int u = gt * 4 + q;
+      const float ig = det_sigmoid(g[0]), fg = det_sigmoid(g[1]), gg = det_tanh(g[2]), og = det_sigmoid(g[3]);
+      const float cp = hc_part(a.hc, row, sl, 2 + layer)[u];
+      const float cn = fg * cp + ig * gg;
+      const float hh = bf_round(og * det_tanh(cn));
+      hc_part(a.hc, row, sl ^ 1, 2 + layer)[u] = cn;
+      hc_part(a.hc, row, sl ^ 1, layer)[u] = hh;
     }
-    __syncthreads();  // X / rows are restaged by the next tile
+    __syncthreads();  // X / rows / Hp are restaged by the next tile
   }
 }
 
-// G = b_p + g . W1p^T for the listed rows' new candidates.  Grid: x = 128-column group
-// (weights in registers), y = DEC_ROW_GROUPS workgroups striding over 16-row tiles.  Also
-// clears the other parity's emit list for the joint that follows.
-__global__ void __launch_bounds__(256, 2) dec_g_kernel(DecArgs a, int parity) {
+// G = b_p + g . W1p^T for the listed rows' new candidates.  Grid: x = 64-column group (one
+// 16-column tile per wave, its weights in registers), y = row groups striding over 16-row
+// tiles (one resident round: 8 x 96).  Also clears the other parity's emit list for the
+// joint that follows.
+constexpr int G_ROW_GROUPS = 96;
+__global__ void __launch_bounds__(256) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][GP];
   __shared__ int rows[16], slots[16];
   DecState& s = a.s;
@@ -213,17 +222,12 @@ __global__ void __launch_bounds__(256, 2) dec_g_kernel(DecArgs a, int parity) {
   if ((int)blockIdx.y >= ntiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   const int* list = s.list + parity * a.Npad;
-  const int jt = blockIdx.x * 8 + wave * 2;
+  const int jt = blockIdx.x * 4 + wave;
   const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
-  const uint16_t* w1 = w0 + 16 * P;
-  uint4 wa[P / 32], wb[P / 32];
+  uint4 wv[P / 32];
 #pragma unroll
-  for (int b = 0; b < P / 32; ++b) {
-    wa[b] = *(const uint4*)(w0 + 32 * b);
-    wb[b] = *(const uint4*)(w1 + 32 * b);
-  }
+  for (int b = 0; b < P / 32; ++b) wv[b] = *(const uint4*)(w0 + 32 * b);
   const float4 b0 = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
-  const float4 b1 = *(const float4*)(a.w.bp + (jt + 1) * 16 + 4 * q);
   for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
     if (tid < 16) {
       const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
@@ -240,21 +244,17 @@ __global__ void __launch_bounds__(256, 2) dec_g_kernel(DecArgs a, int parity) {
       X[mi][chain_pos(k + 3)] = v.w;
     }
     __syncthreads();
-    v4f acc0 = v4f{b0.x, b0.y, b0.z, b0.w}, acc1 = v4f{b1.x, b1.y, b1.z, b1.w};
+    v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
     const float* xr = &X[c][8 * q];
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) {
       float x[8];
       *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
       *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-      acc0 = chain8(wa[b], x, acc0);
-      acc1 = chain8(wb[b], x, acc1);
+      acc = chain8(wv[b], x, acc);
     }
     const int row = rows[c];
-    if (row >= 0) {
-      *(float4*)(a.G + (size_t)row * J + jt * 16 + 4 * q) = float4{acc0[0], acc0[1], acc0[2], acc0[3]};
-      *(float4*)(a.G + (size_t)row * J + (jt + 1) * 16 + 4 * q) = float4{acc1[0], acc1[1], acc1[2], acc1[3]};
-    }
+    if (row >= 0) *(float4*)(a.G + (size_t)row * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
     __syncthreads();
   }
 }
@@ -272,6 +272,7 @@ __global__ void __launch_bounds__(256, 2) dec_g_kernel(DecArgs a, int parity) {
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][YP];
   __shared__ float L[16][NLAB_PAD + 1];
+  __shared__ float Lp[4][16][NLAB_PAD + 1];
   __shared__ int live[16], tidx[16];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
@@ -304,23 +305,42 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       X[m][chain_pos(k + 3)] = v.w;
     }
     __syncthreads();
-    if (wave < 2) {
-      const float4 b0 = *(const float4*)(a.w.b2 + wave * 16 + 4 * q);
-      v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
-      const uint16_t* wr = a.w.w2 + (size_t)(wave * 16 + c) * J + 8 * q;
+    {  // logits = ((s0 + s1) + s2) + s3, s_b = y1[128b : 128b+128] . W2^T (s0 from b2): wave w
+       // runs label half w&1 over k blocks 2(w>>1) and 2(w>>1)+1 as two independent chains
+      const int lh = wave & 1, kb0 = 2 * (wave >> 1);
+      const uint16_t* wr = a.w.w2 + (size_t)(lh * 16 + c) * J + 8 * q;
       const float* xr = &X[c][8 * q];
-      uint4 wv[J / 32];
+      uint4 wv[8];
 #pragma unroll
-      for (int b = 0; b < J / 32; ++b) wv[b] = *(const uint4*)(wr + 32 * b);
-#pragma unroll
-      for (int b = 0; b < J / 32; ++b) {
-        float x[8];
-        *(float4*)&x[0] = *(const float4*)(xr + 32 * b);
-        *(float4*)&x[4] = *(const float4*)(xr + 32 * b + 4);
-        acc = chain8(wv[b], x, acc);
+      for (int b = 0; b < 4; ++b) {
+        wv[b] = *(const uint4*)(wr + 128 * kb0 + 32 * b);
+        wv[4 + b] = *(const uint4*)(wr + 128 * (kb0 + 1) + 32 * b);
+      }
+      v4f s0 = v4f{0.0f, 0.0f, 0.0f, 0.0f}, s1 = s0;
+      if (kb0 == 0) {
+        const float4 b0 = *(const float4*)(a.w.b2 + lh * 16 + 4 * q);
+        s0 = v4f{b0.x, b0.y, b0.z, b0.w};
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) L[c][wave * 16 + 4 * q + r] = acc[r];
+      for (int b = 0; b < 4; ++b) {
+        float x0[8], x1[8];
+        *(float4*)&x0[0] = *(const float4*)(xr + 128 * kb0 + 32 * b);
+        *(float4*)&x0[4] = *(const float4*)(xr + 128 * kb0 + 32 * b + 4);
+        *(float4*)&x1[0] = *(const float4*)(xr + 128 * (kb0 + 1) + 32 * b);
+        *(float4*)&x1[4] = *(const float4*)(xr + 128 * (kb0 + 1) + 32 * b + 4);
+        s0 = chain8(wv[b], x0, s0);
+        s1 = chain8(wv[4 + b], x1, s1);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Lp[kb0][c][lh * 16 + 4 * q + r] = s0[r];
+        Lp[kb0 + 1][c][lh * 16 + 4 * q + r] = s1[r];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < 16 * NLAB_PAD; i += 256) {
+      const int m = i / NLAB_PAD, j = i % NLAB_PAD;
+      L[m][j] = ((Lp[0][m][j] + Lp[1][m][j]) + Lp[2][m][j]) + Lp[3][m][j];
     }
     __syncthreads();
     if (tid < 16 && live[tid]) {
@@ -362,9 +382,9 @@ __global__ void dec_finish_kernel(DecArgs a) {
 
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st) {
   const int rt = a.Npad / 16;
-  // row-tile workgroups per column group, sized so each launch is ONE resident round (2
-  // workgroups per CU x 256 CUs): 10 x 51 for the prediction layers, 4 x 128 for G
-  const int rg_pred = rt < 51 ? rt : 51, rg_g = rt < 128 ? rt : 128;
+  // row-tile workgroups per column group, sized so each launch is ONE resident round:
+  // 20 x 25 for the prediction layers (2 x 8 waves per CU), 8 x 96 for G (3 per CU)
+  const int rg_pred = rt < PRED_ROW_GROUPS ? rt : PRED_ROW_GROUPS, rg_g = rt < G_ROW_GROUPS ? rt : G_ROW_GROUPS;
   if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.s.unfinished, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
@@ -375,9 +395,9 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   while (!done && step < a.max_iter) {
     for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rg_pred), dim3(256), 0, st, a, 0, p);
-      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / 128, rg_pred), dim3(256), 0, st, a, 1, p);
-      hipLaunchKernelGGL(dec_g_kernel, dim3(J / 128, rg_g), dim3(256), 0, st, a, p);
+      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / (16 * PRED_TILES), rg_pred), dim3(PRED_THREADS), 0, st, a, 0, p);
+      hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / (16 * PRED_TILES), rg_pred), dim3(PRED_THREADS), 0, st, a, 1, p);
+      hipLaunchKernelGGL(dec_g_kernel, dim3(J / 64, rg_g), dim3(256), 0, st, a, p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rt), dim3(256), 0, st, a, p);
     }
     // poll the live-row counter one chunk behind, so the host never drains the queue

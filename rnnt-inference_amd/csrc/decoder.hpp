@@ -9,7 +9,8 @@ namespace rnnt {
 struct DecWeights {
   const uint16_t* embed;   // bf16 [28][320] natural
   const uint16_t* wp[2];   // bf16 [1280][640] gate-interleaved rows, chain-permuted k ([W_ih | W_hh])
-  const float* bp_lstm[2]; // fp32 [1280] b_ih + b_hh, gate-interleaved
+  const float* bih_p[2];   // fp32 [1280] b_ih, gate-interleaved
+  const float* bhh_p[2];   // fp32 [1280] b_hh, gate-interleaved
   const uint16_t* w1t;     // bf16 [512][1024] chain-permuted k
   const uint16_t* w1p;     // bf16 [512][320]  chain-permuted k
   const float* bt;         // [512]

@@ -119,19 +119,21 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
     e->in_s[l] = m->enc_in_s[l];
     e->out_s[l] = m->enc_out_s[l];
   }
-  // prediction LSTM: rows gate-interleaved, k = [W_ih | W_hh] chain-permuted, fused bias
+  // prediction LSTM: rows gate-interleaved, k = [W_ih | W_hh] chain-permuted, biases separate
+  // (the two chains b_ih + x.W_ih and b_hh + h.W_hh are summed after, oracle pred_row)
   for (int l = 0; l < 2; ++l) {
     if (!m->pred_w_ih[l] || !m->pred_w_hh[l] || !m->pred_b_ih[l] || !m->pred_b_hh[l])
       return fail(RNNT_EINVAL, "null prediction weight");
     std::vector<uint16_t> w((size_t)PG4 * 640);
-    std::vector<float> b(PG4);
+    std::vector<float> b(2 * PG4);
     for (int g = 0; g < 4; ++g)
       for (int u = 0; u < P; ++u) {
         const int src = g * P + u, dst = 4 * u + g;
         for (int k = 0; k < 640; ++k)
           w[(size_t)dst * 640 + chain_pos(k)] =
               k < P ? m->pred_w_ih[l][(size_t)src * P + k] : m->pred_w_hh[l][(size_t)src * P + k - P];
-        b[dst] = m->pred_b_ih[l][src] + m->pred_b_hh[l][src];  // fp32 add, as the oracle
+        b[dst] = m->pred_b_ih[l][src];
+        b[PG4 + dst] = m->pred_b_hh[l][src];
       }
     uint16_t* dwp;
     float* dbp;
@@ -139,7 +141,8 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
     if (!r) r = upload(e, &dbp, b);
     if (r) return r;
     e->dw.wp[l] = dwp;
-    e->dw.bp_lstm[l] = dbp;
+    e->dw.bih_p[l] = dbp;
+    e->dw.bhh_p[l] = dbp + PG4;
   }
   auto permute_rows = [](const uint16_t* src, int rows, int rows_pad, int K) {
     std::vector<uint16_t> w((size_t)rows_pad * K, 0);

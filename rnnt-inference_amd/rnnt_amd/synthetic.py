@@ -72,7 +72,7 @@ def _plant_anti_repeat(sd, gamma, noise):
     gram = (phi[:, :, None] * phi[:, None, :]).sum(0)         # [28, 28]
     pinv = np.linalg.solve(gram + 1e-9 * np.eye(gram.shape[0]), phi.T)  # [28, P]
     u = sd["joint_net.3.weight"][: R.num_labels - 1].astype(np.float64).T  # [512, 28]
-    w1p = -gamma * (u[:, :, None] * pinv[None, :, :]).sum(1)  # [512, P]
+    w1p = -gamma * (u[:, :, None] * pinv[None, :, :]).sum(1)  # [512, P]: G_s ~ -gamma W2[s]
     w = sd["joint_net.0.weight"]
     w[:, H:] = (w1p + noise * w[:, H:].astype(np.float64)).astype(np.float32)
 

@@ -1,13 +1,22 @@
 set -e
-mkdir -p gpurun_out/c11
-for v in base p0 p0prio base p0 p0prio; do
-  echo -n "$v " >> gpurun_out/c11/abl.txt
-  RNNT_MI355X_LIB=build_dev/lib_$v.so timeout -k 10 300 python tools/bench_kernels.py --n 8192 --T 16 --layers 1,2,0 >> gpurun_out/c11/abl.txt 2>gpurun_out/c11/$v.err || echo FAIL >> gpurun_out/c11/abl.txt
-done
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { tail -20 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/t7
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/t7/tr -o kb -- python3 tools/bench_kernels.py --n 8192 --layers "" > gpurun_out/t7/kb.log 2>&1
 python3 - <<'P'
-import json
-for line in open('gpurun_out/c11/abl.txt'):
-    v, js = line.split(' ', 1)
-    d = json.loads(js)
-    print(v, d['step_K1280']['us_per_launch'], d['step_K2048']['us_per_launch'], d['step_K3072']['us_per_launch'], d['infer_batch']['encode_ms'])
+import csv, glob, sys, numpy as np
+f = glob.glob('gpurun_out/t7/tr/**/kb_kernel_trace.csv', recursive=True)[0]
+rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r['Start_Timestamp']))
+dec = [(r['Kernel_Name'].split('(')[0].replace('rnnt::', ''), int(r['Start_Timestamp']), int(r['End_Timestamp'])) for r in rows if 'dec_' in r['Kernel_Name']]
+dec = dec[len(dec)//2:]
+out = []
+for name in ('dec_pred_kernel', 'dec_g_kernel', 'dec_joint_kernel'):
+    d = np.array([(e - s) / 1e3 for n, s, e in dec if n == name])
+    out.append(f"{name}: n={len(d)} med={np.median(d):.2f} tail={np.median(d[-len(d)//3:]):.2f} max={d.max():.1f} sum={d.sum()/1e3:.1f}ms")
+print(" | ".join(out))
 P
+find gpurun_out/t7 -name "*.csv" -delete
+timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench_c16.json 2> gpurun_out/bench_c16.err
+python3 -c "
+import json; d=json.load(open('gpurun_out/bench_c16.json')); r=d['roofline']; print(d['value'], d['ms_per_step'], r['encode_ms_per_query'], r['greedy_ms_per_query'], r['isolated'])"

@@ -25,6 +25,9 @@ for v in "$@"; do
     ji2) build ji2 -DRNNT_JOINT_ITERS=2 ;;
     ji4) build ji4 -DRNNT_JOINT_ITERS=4 ;;
     ji8) build ji8 -DRNNT_JOINT_ITERS=8 ;;
+    pred_nomfma) build pred_nomfma -DRNNT_DEV_PRED_NOMFMA ;;
+    pred_nostage) build pred_nostage -DRNNT_DEV_PRED_NOSTAGE ;;
+    pred_nowload) build pred_nowload -DRNNT_DEV_PRED_NOWLOAD ;;
     ns3) build ns3 -DRNNT_NSTAGE=3 ;;
     ns5) build ns5 -DRNNT_NSTAGE=5 ;;
     ns3_noepi) build ns3_noepi -DRNNT_NSTAGE=3 -DRNNT_DEV_NO_EPI ;;
