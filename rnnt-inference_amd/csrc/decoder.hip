@@ -113,7 +113,20 @@ __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
 // tiles (one resident round).
 constexpr int PRED_TILES = 4;
 constexpr int PRED_THREADS = PRED_TILES * 2 * 64;
-constexpr int PRED_ROW_GROUPS = 25;
+#ifndef RNNT_PRED_RG
+#define RNNT_PRED_RG 25
+#endif
+#ifndef RNNT_G_RG
+#define RNNT_G_RG 96
+#endif
+#ifndef RNNT_JOINT_G
+#define RNNT_JOINT_G 512
+#endif
+// decode grids are kept small: every resident decode workgroup, even an idle one, keeps an
+// encoder tick workgroup (a whole CU) of the batch in flight beside it from starting
+constexpr int PRED_ROW_GROUPS = RNNT_PRED_RG;
+constexpr int G_ROW_GROUPS = RNNT_G_RG;
+constexpr int JOINT_GROUPS = RNNT_JOINT_G;
 __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int layer, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][XP];
   __shared__ v4f Hp[PRED_TILES][64];
@@ -211,7 +224,6 @@ __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int l
 // 16-column tile per wave, its weights in registers), y = row groups striding over 16-row
 // tiles (one resident round: 8 x 96).  Also clears the other parity's emit list for the
 // joint that follows.
-constexpr int G_ROW_GROUPS = 96;
 __global__ void __launch_bounds__(256) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) float X[16][GP];
   __shared__ int rows[16], slots[16];
@@ -276,7 +288,8 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ int live[16], tidx[16];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
-  const int r0 = blockIdx.x * 16;
+  for (int rtile = blockIdx.x; rtile < (a.N + 15) / 16; rtile += gridDim.x) {
+  const int r0 = rtile * 16;
   if (tid < 16) {
     const int row = r0 + tid;
     const int lv = (row < a.N) && !s.fin[row];
@@ -288,7 +301,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     bool any = false;
 #pragma unroll
     for (int m = 0; m < 16; ++m) any |= live[m] != 0;
-    if (!any) return;
+    if (!any) break;
     for (int i = tid; i < 16 * (J / 4); i += 256) {
       const int m = i / (J / 4), k = (i % (J / 4)) * 4, row = r0 + m;
       float4 v = float4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -373,6 +386,8 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     }
     __syncthreads();
   }
+  __syncthreads();  // live / tidx / X are reused by the next row tile
+  }
 }
 
 __global__ void dec_finish_kernel(DecArgs a) {
@@ -385,6 +400,7 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   // row-tile workgroups per column group, sized so each launch is ONE resident round:
   // 20 x 25 for the prediction layers (2 x 8 waves per CU), 8 x 96 for G (3 per CU)
   const int rg_pred = rt < PRED_ROW_GROUPS ? rt : PRED_ROW_GROUPS, rg_g = rt < G_ROW_GROUPS ? rt : G_ROW_GROUPS;
+  const int rg_joint = rt < JOINT_GROUPS ? rt : JOINT_GROUPS;
   if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.s.unfinished, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
@@ -398,7 +414,7 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
       hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / (16 * PRED_TILES), rg_pred), dim3(PRED_THREADS), 0, st, a, 0, p);
       hipLaunchKernelGGL(dec_pred_kernel, dim3(PG4 / (16 * PRED_TILES), rg_pred), dim3(PRED_THREADS), 0, st, a, 1, p);
       hipLaunchKernelGGL(dec_g_kernel, dim3(J / 64, rg_g), dim3(256), 0, st, a, p);
-      hipLaunchKernelGGL(dec_joint_kernel, dim3(rt), dim3(256), 0, st, a, p);
+      hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
     }
     // poll the live-row counter one chunk behind, so the host never drains the queue
     if (hipMemcpyAsync(host_flags + (chunk & 1), a.s.unfinished, sizeof(int32_t), hipMemcpyDeviceToHost, st) !=

@@ -41,19 +41,26 @@ __global__ void __launch_bounds__(256) quantize_kernel(const float4* __restrict_
 // tile: staging through the per-CU load path (~70 GB/s/CU from L2), not the MFMA, bounds this
 // GEMM (DESIGN.md "Encoder kernel").
 constexpr int BM = 256;
-constexpr int BN = 256;
+constexpr int BN = ENC_BATCH_TILE;           // 128 * ENC_WN
 constexpr int BK = 64;
-constexpr int NWAVE = 8;
+constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-column waves
 #ifndef RNNT_NSTAGE
-#define RNNT_NSTAGE 4
+#define RNNT_NSTAGE (ENC_WN == 2 ? 4 : 3)
+#endif
+#ifndef RNNT_INTERLEAVE
+#define RNNT_INTERLEAVE 0
 #endif
 constexpr int NSTAGE = RNNT_NSTAGE;          // LDS ring depth: NSTAGE-1 stages in flight
 constexpr int A_BYTES = BM * BK;             // 16 KiB
-constexpr int STAGE_BYTES = (BM + BN) * BK;  // 32 KiB
-constexpr int GLDS_PER_STAGE = 4;            // per wave: 2 x 1 KiB pieces of A, 2 of B
+constexpr int STAGE_BYTES = (BM + BN) * BK;  // 32 / 24 KiB
+constexpr int APW = (BM / 16) / NWAVE;       // 16-row A pieces (1 KiB LDS-DMA each) per wave: 2 | 4
+constexpr int BPW = (BN / 16) / NWAVE;       // B pieces per wave: 2
+constexpr int GLDS_PER_STAGE = APW + BPW;
+constexpr int C_GLDS = (BN * 128 / 1024) / NWAVE;  // cell-state DMA pieces per wave: 4
 constexpr int TAB_OFF = NSTAGE * STAGE_BYTES;   // LDS: sigma table after the ring
 constexpr int SMEM_BYTES = TAB_OFF + 128 * 16;
-static_assert(BM / 16 == 2 * NWAVE && BN / 16 == 2 * NWAVE, "two 16-row pieces per wave per operand");
+static_assert(BPW == 2 && (APW == 2 || APW == 4) && C_GLDS == 4, "staging split");
+static_assert(BN * 128 <= STAGE_BYTES, "the cell-state image fits one ring buffer");
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) char lds_char;
@@ -74,6 +81,17 @@ template <int N>
 __device__ __forceinline__ void stage_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
+// runtime-selected immediate (wave-uniform n in [0, 24])
+__device__ __forceinline__ void stage_barrier_n(int n) {
+  switch (n) {
+#define RNNT_SB(v) \
+  case v: stage_barrier<v>(); break;
+    RNNT_SB(0) RNNT_SB(2) RNNT_SB(4) RNNT_SB(6) RNNT_SB(8) RNNT_SB(10) RNNT_SB(12) RNNT_SB(14) RNNT_SB(16)
+    RNNT_SB(18) RNNT_SB(20) RNNT_SB(22) RNNT_SB(24)
+#undef RNNT_SB
+    default: stage_barrier<0>(); break;
+  }
+}
 
 __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -87,53 +105,59 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   const int q = lane >> 4, col = lane & 15;
   const int u0 = (m0 >> 2) + wm * 16 + q * 4;  // this lane's 4 consecutive units
   const int nb = n0 + wn * 128 + col;          // batch row of j = 0 (row j: nb + 16 j)
-  // ---- LDS-DMA staging: wave w moves pieces 2w, 2w+1 (16 rows x 64 B each) of A and of B;
-  // lane l of piece p lands at LDS slot 64p + l = row*4 + (col16 ^ h(row)), so it fetches
-  // row 16p + (l>>2), 16-byte column (l&3) ^ h, where h(row) depends on l>>4 only.
+  // ---- LDS-DMA staging: wave w moves A pieces APW*w .. +APW-1 and B pieces 2w, 2w+1 (16 rows x
+  // 64 B each); lane l of piece p lands at LDS slot 64p + l = row*4 + (col16 ^ h(row)), so it
+  // fetches row 16p + (l>>2), 16-byte column (l&3) ^ h, where h(row) depends on l>>4 only.
   const int hx = (0x1320 >> ((lane >> 4) * 4)) & 3;
   const int gcol = ((lane & 3) ^ hx) * 16;
-  const int ra = wave * 32 + (lane >> 2);  // first row of this wave's two 16-row pieces (second: +16)
+  const int rA = wave * APW * 16 + (lane >> 2);  // first row of this wave's A pieces (+16 each)
+  const int rB = wave * BPW * 16 + (lane >> 2);  // first row of its B pieces
 #ifdef RNNT_DEV_SAME_TILE  // development ablation: every workgroup stages tile (0, 0) (L2-resident)
   const int lm0 = 0, ln0 = 0;
 #else
   const int lm0 = m0, ln0 = n0;
 #endif
   // per-lane 32-bit offsets from wave-uniform (SGPR) tile bases: global_load_lds with saddr
-  const uint32_t oA = (uint32_t)(ra * K + gcol), oX = (uint32_t)(ra * a.I + gcol), oH = (uint32_t)(ra * H + gcol);
-  const int8_t* wbase0 = a.W + (size_t)lm0 * K;
-  const int8_t* wbase1 = wbase0 + (size_t)16 * K;
+  const uint32_t oA = (uint32_t)(rA * K + gcol), oX = (uint32_t)(rB * a.I + gcol), oH = (uint32_t)(rB * H + gcol);
+  const int8_t* wbase = a.W + (size_t)lm0 * K;
   const int8_t* xbase0 = a.x + (size_t)ln0 * a.I;
   const int8_t* xbase1 = xbase0 + (size_t)16 * a.I;
   const int8_t* hbase0 = a.h_in + (size_t)ln0 * H - a.I;
   const int8_t* hbase1 = hbase0 + (size_t)16 * H;
   lds_char* lds = (lds_char*)(lds_void*)smem;
-  const int pa = wave * 2 * 1024;
+  const int pa = wave * APW * 1024, pb = A_BYTES + wave * BPW * 1024;
 
-  auto issue = [&](int ks) __attribute__((always_inline)) {
+  // piece j (0..GLDS_PER_STAGE-1) of stage ks: A pieces first, then the two B pieces
+  auto issue_piece = [&](int ks, int j) __attribute__((always_inline)) {
 #ifdef RNNT_DEV_NO_LOAD  // development ablation: no staging (MFMA on stale LDS)
     return;
 #endif
     const int k = ks * BK;
-    lds_char* st = lds + (ks % NSTAGE) * STAGE_BYTES + pa;
-    __builtin_amdgcn_global_load_lds((glb_void*)(wbase0 + k + oA), (lds_void*)st, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((glb_void*)(wbase1 + k + oA), (lds_void*)(st + 1024), 16, 0, 0);
-    if (k < a.I) {
-      __builtin_amdgcn_global_load_lds((glb_void*)(xbase0 + k + oX), (lds_void*)(st + A_BYTES), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_void*)(xbase1 + k + oX), (lds_void*)(st + A_BYTES + 1024), 16, 0, 0);
+    lds_char* st = lds + (ks % NSTAGE) * STAGE_BYTES;
+    if (j < APW) {
+      __builtin_amdgcn_global_load_lds((glb_void*)(wbase + (size_t)(16 * j) * K + k + oA), (lds_void*)(st + pa + j * 1024), 16,
+                                       0, 0);
+    } else if (k < a.I) {
+      __builtin_amdgcn_global_load_lds((glb_void*)((j == APW ? xbase0 : xbase1) + k + oX),
+                                       (lds_void*)(st + pb + (j - APW) * 1024), 16, 0, 0);
     } else {
-      __builtin_amdgcn_global_load_lds((glb_void*)(hbase0 + k + oH), (lds_void*)(st + A_BYTES), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((glb_void*)(hbase1 + k + oH), (lds_void*)(st + A_BYTES + 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void*)((j == APW ? hbase0 : hbase1) + k + oH),
+                                       (lds_void*)(st + pb + (j - APW) * 1024), 16, 0, 0);
     }
   };
+  auto issue = [&](int ks) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < GLDS_PER_STAGE; ++j) issue_piece(ks, j);
+  };
 
-  // the tile's fp16 cell state (256 rows x 64 units x 2 B = 32 KiB) DMA'd into the ring buffer
-  // of stage nK-4 once it has been read; piece p, lane l: row 8p + (l>>3), 16-B chunk l&7
-  const int cbuf = ((nK - 4) % NSTAGE) * STAGE_BYTES;
+  // the tile's fp16 cell state (BN rows x 64 units x 2 B) DMA'd into the ring buffer of stage
+  // nK-NSTAGE once it has been read; piece p, lane l: row 8p + (l>>3), 16-B chunk l&7
+  const int cbuf = ((nK - NSTAGE) % NSTAGE) * STAGE_BYTES;
   auto issue_c = [&]() __attribute__((always_inline)) {
     const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + (lane & 7) * 8;
 #pragma unroll
-    for (int pc = 0; pc < 4; ++pc) {
-      const int p = wave * 4 + pc;
+    for (int pc = 0; pc < C_GLDS; ++pc) {
+      const int p = wave * C_GLDS + pc;
       __builtin_amdgcn_global_load_lds((glb_void*)(cb + (size_t)(8 * p + (lane >> 3)) * H), (lds_void*)(lds + cbuf + p * 1024),
                                        16, 0, 0);
     }
@@ -149,33 +173,56 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // column lane>>4; +16 rows is +1 KiB in the image (the swizzle repeats every 16 rows)
   const int fa = swz(wm * 64 + col, q), fb = A_BYTES + swz(wn * 128 + col, q);
 
-  static_assert(NSTAGE == 4, "cell-state DMA placement assumes a 4-deep ring");
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
   for (int ks = 0; ks < nK; ++ks) {
-    // stages issued after ks that may stay in flight: min(NSTAGE - 2, nK - 1 - ks), plus the
-    // cell-state DMA issued at step nK-3 into stage nK-4's buffer (read at step nK-4)
-    const int rem = (nK - 1 - ks < 2 ? nK - 1 - ks : 2) + (ks >= nK - 2 ? 1 : 0);
-    if (rem >= 2) stage_barrier<2 * GLDS_PER_STAGE>();
-    else if (rem >= 1) stage_barrier<GLDS_PER_STAGE>();
-    else stage_barrier<0>();
+    // LDS-DMA this wave may leave in flight: the stages issued after ks (min(NSTAGE - 2,
+    // nK - 1 - ks)) and, once issued (step nK-NSTAGE+1, into stage nK-NSTAGE's buffer), the
+    // cell-state pieces
+    const int later = nK - 1 - ks < NSTAGE - 2 ? nK - 1 - ks : NSTAGE - 2;
+    stage_barrier_n(later * GLDS_PER_STAGE + (ks > nK - NSTAGE + 1 ? C_GLDS : 0));
+#if !RNNT_INTERLEAVE
     if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
     else if (ks + NSTAGE - 1 == nK) issue_c();
+#else
+    const bool next = ks + NSTAGE - 1 < nK;
+    if (ks + NSTAGE - 1 == nK) issue_c();
+#endif
     const int8_t* st = smem + (ks % NSTAGE) * STAGE_BYTES;
     v4i fra[4], frb[8];
+#ifdef RNNT_DEV_NO_READ  // development ablation: MFMA on register-resident fragments
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fra[i] = v4i{ks, i, 1, 2};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) frb[j] = v4i{j, ks, 3, 4};
+    asm volatile("" : "+v"(fra[0]), "+v"(frb[0]));
+    (void)st;
+#else
 #pragma unroll
     for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa + i * 1024);
 #pragma unroll
     for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb + j * 1024);
+#endif
 #ifdef RNNT_DEV_NO_MFMA  // development ablation: staging + LDS reads only
 #pragma unroll
     for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fra[i]), "v"(frb[i]), "v"(frb[i + 4]));
 #else
     __builtin_amdgcn_s_setprio(1);  // MFMA cluster at raised priority (guide T5)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+#if RNNT_INTERLEAVE
+      // the next stage's LDS-DMA pieces spread between the MFMA groups
+#pragma unroll
+      for (int pj = i * GLDS_PER_STAGE / 4; pj < (i + 1) * GLDS_PER_STAGE / 4; ++pj)
+        if (next) issue_piece(ks + NSTAGE - 1, pj);
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+#if RNNT_INTERLEAVE
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
     __builtin_amdgcn_s_setprio(0);
 #endif
   }
@@ -234,7 +281,8 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 // tiles 4(x&3)..4(x&3)+3 and the (x>>2)-th half of each job's active batch tiles, so the 32
 // workgroups resident on an XCD share 4 weight tiles and ~8 activation tiles through its L2
 // (weights fetched from HBM/MALL 2x, activations 4x per tick, instead of 1x / 8x).
-__global__ void __launch_bounds__(512, 1) lstm_i8_tick_kernel(EncTickArgs args) {
+// 2 waves per SIMD either way: one 8-wave workgroup per CU (ENC_WN 2) or two 4-wave ones (1)
+__global__ void __launch_bounds__(NWAVE * 64, ENC_WN == 2 ? 1 : 2) lstm_i8_tick_kernel(EncTickArgs args) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   const int xcd = blockIdx.x & 7, gg = xcd & 3, bg = xcd >> 2;
   int k = blockIdx.x >> 3, jsel = -1, mt = 0, nt = 0;

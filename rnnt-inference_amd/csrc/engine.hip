@@ -226,7 +226,7 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   e->opts.max_batch = (opts && opts->max_batch > 0) ? opts->max_batch : 1024;
   e->opts.max_frames = (opts && opts->max_frames > 0) ? opts->max_frames : 500;
   e->opts.max_res = (opts && opts->max_res > 0) ? opts->max_res : (e->opts.max_frames / 2) * MAXSYM;
-  e->np_max = (e->opts.max_batch + ENC_BATCH_TILE - 1) / ENC_BATCH_TILE * ENC_BATCH_TILE;
+  e->np_max = (e->opts.max_batch + ENC_PAD - 1) / ENC_PAD * ENC_PAD;
   e->tp_max = (e->opts.max_frames + 1) / 2;
   int r = 0;
   if (hipSetDevice(device) != hipSuccess) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
@@ -337,7 +337,7 @@ static int run_layer(rnnt_engine* e, int l, int T, int n_pad, const int8_t* x, i
 
 static int check_batch(rnnt_engine* e, int T, int n, int n_pad) {
   if (T <= 0 || T > e->opts.max_frames) return fail(RNNT_EINVAL, "T out of range");
-  if (n <= 0 || n_pad < n || n_pad % ENC_BATCH_TILE || n_pad > e->np_max)
+  if (n <= 0 || n_pad < n || n_pad % ENC_PAD || n_pad > e->np_max)
     return fail(RNNT_EINVAL, "n / n_pad out of range (n_pad must be a multiple of 256 <= max_batch)");
   return 0;
 }
@@ -480,7 +480,7 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
                                  uint16_t* cx, void* y, void* stream) {
   if (!e || !x || !hx || !cx || !y) return fail(RNNT_EINVAL, "null argument");
   if (first < 0 || count <= 0 || first + count > 5) return fail(RNNT_EINVAL, "bad layer range");
-  if (T <= 0 || T > e->opts.max_frames || n_pad <= 0 || n_pad % ENC_BATCH_TILE || n_pad > e->np_max)
+  if (T <= 0 || T > e->opts.max_frames || n_pad <= 0 || n_pad % ENC_PAD || n_pad > e->np_max)
     return fail(RNNT_EINVAL, "T / n_pad out of range");
   if (first <= 1 && first + count > 2) return fail(RNNT_EINVAL, "a call covers pre_rnn or post_rnn, not both");
   if (first >= 2 && T > e->tp_max) return fail(RNNT_EINVAL, "post_rnn T exceeds ceil(max_frames/2)");

@@ -62,7 +62,11 @@ __device__ __forceinline__ float act_sig_t(const float4* __restrict__ tab, float
   t = __builtin_fminf(__builtin_fmaxf(t, 0.0f), 127.99998f);
   const int k = (int)t;
   const float fr = __builtin_amdgcn_fractf(t);  // v_fract_f32: t - floor(t), exact for t >= 0
+#ifdef RNNT_DEV_NO_TAB  // development ablation: no LDS lookup
+  const float4 c = float4{t * 0.001f, (float)k, 0.5f, 0.25f};
+#else
   const float4 c = tab[k];
+#endif
   return __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c.w, fr, c.z), fr, c.y), fr, c.x);
 }
 // acc: int32 gate sums (i, f, g, o); B: packed per-gate bias terms (oracle_enc_bias);

@@ -28,6 +28,18 @@ for v in "$@"; do
     pred_nomfma) build pred_nomfma -DRNNT_DEV_PRED_NOMFMA ;;
     pred_nostage) build pred_nostage -DRNNT_DEV_PRED_NOSTAGE ;;
     pred_nowload) build pred_nowload -DRNNT_DEV_PRED_NOWLOAD ;;
+    dg_a) build dg_a -DRNNT_PRED_RG=25 -DRNNT_G_RG=96 -DRNNT_JOINT_G=512 ;;
+    dg_b) build dg_b -DRNNT_PRED_RG=8 -DRNNT_G_RG=24 -DRNNT_JOINT_G=128 ;;
+    dg_c) build dg_c -DRNNT_PRED_RG=12 -DRNNT_G_RG=40 -DRNNT_JOINT_G=256 ;;
+    dg_d) build dg_d -DRNNT_PRED_RG=5 -DRNNT_G_RG=16 -DRNNT_JOINT_G=64 ;;
+    wn1) build wn1 -DENC_WN=1 ;;
+    wn1_ns4) build wn1_ns4 -DENC_WN=1 -DRNNT_NSTAGE=4 ;;
+    wn1_noepi) build wn1_noepi -DENC_WN=1 -DRNNT_DEV_NO_EPI ;;
+    noread_noload_noepi) build noread_noload_noepi -DRNNT_DEV_NO_READ -DRNNT_DEV_NO_LOAD -DRNNT_DEV_NO_EPI ;;
+    noread_noepi) build noread_noepi -DRNNT_DEV_NO_READ -DRNNT_DEV_NO_EPI ;;
+    il) build il -DRNNT_INTERLEAVE=1 ;;
+    il_noepi) build il_noepi -DRNNT_INTERLEAVE=1 -DRNNT_DEV_NO_EPI ;;
+    notab) build notab -DRNNT_DEV_NO_TAB ;;
     ns3) build ns3 -DRNNT_NSTAGE=3 ;;
     ns5) build ns5 -DRNNT_NSTAGE=5 ;;
     ns3_noepi) build ns3_noepi -DRNNT_NSTAGE=3 -DRNNT_DEV_NO_EPI ;;
