@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RNNT_ABI_VERSION 2
+#define RNNT_ABI_VERSION 3
 
 #define RNNT_OK 0
 #define RNNT_EINVAL (-22)
@@ -132,6 +132,30 @@ int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const void* x, int T
  * (modeling_rnnt.py:326-328). */
 int rnnt_op_stack_time(rnnt_engine* e, const int8_t* x, const int32_t* x_lens, int T, int n_pad, int C,
                        int8_t* y, void* stream);
+
+/* ---- operator-level decode (the reference's op-by-op loop, models/decoder.py:171-212, on the
+ * bound model; same arithmetic as the fused rnnt_engine_decode).  Row counts n_pad are multiples
+ * of 16; bf16 tensors hold bf16 bit patterns. */
+/* lstm_amx_bf16 (modeling_rnnt.py:202): x bf16 [n_pad][320] (embedding rows, zero for SOS),
+ * hx bf16 [2][n_pad][320], cx fp32 [2][n_pad][320] -> hy, cy (same shapes, must not alias the
+ * inputs); g = hy[1]. */
+int rnnt_op_lstm_bf16(rnnt_engine* e, const uint16_t* x, const uint16_t* hx, const float* cx, uint16_t* hy, float* cy,
+                      int n_pad, void* stream);
+/* amx_linear_bf16_accum_relu (modeling_rnnt.py:269-275): f fp32 [n_pad][1024] (rounded to bf16),
+ * g bf16 [n_pad][320] -> y1 bf16 [n_pad][512] = relu(f.W1t^T + b_t + g.W1p^T + b_p). */
+int rnnt_op_joint_hidden(rnnt_engine* e, const float* f, const uint16_t* g, uint16_t* y1, int n_pad, void* stream);
+/* amx_linear_i16o32 (modeling_rnnt.py:280-283): y1 bf16 [n_pad][512] -> logits fp32 [n_pad][32]
+ * (labels 29..31 are zero padding, as the reference's padded linear2). */
+int rnnt_op_joint_logits(rnnt_engine* e, const uint16_t* y1, float* logits, int n_pad, void* stream);
+/* greedy_decode_update (modeling_rnnt.py:331-365; spec decoder.py:125-167), in place on the
+ * device state; `finish` int32 [n] is the spec's self.finish (decoder.py:106).  f fp32
+ * [T'][n_pad][1024], fi fp32 [n_pad][1024], pre_hg/hg bf16 and pre_cg/cg fp32 [2][n_pad][320],
+ * res int32 [n][max_res].  Synchronises the stream; returns 1 when every row has finished, 0
+ * otherwise, or a negative error code. */
+int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int32_t* symbols_added, int32_t* res,
+                          int32_t* res_idx, const float* f, const int32_t* f_lens, int32_t* time_idx, float* fi,
+                          int32_t* pre_g, uint16_t* pre_hg, float* pre_cg, const uint16_t* hg, const float* cg,
+                          int32_t* finish, int n, int n_pad, int max_res, void* stream);
 
 #ifdef __cplusplus
 }

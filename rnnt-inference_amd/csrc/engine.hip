@@ -15,6 +15,7 @@
 
 #include "../../include/rnnt_mi355x.h"
 #include "decoder.hpp"
+#include "decoder_ops.hpp"
 #include "encoder.hpp"
 #include "encoder_f32.hpp"
 #include "rnnt_device.hpp"
@@ -69,6 +70,9 @@ struct rnnt_engine {
   std::vector<void*> f32_ws;
   size_t f32_ws_T = 0, f32_ws_np = 0;
   float *f32_x = nullptr, *f32_ya = nullptr, *f32_xs = nullptr, *f32_yb = nullptr, *f32_h[2] = {}, *f32_c = nullptr;
+  // operator-level decode: unfinished-row counter for greedy_decode_update's return value
+  int32_t* op_count = nullptr;
+  int32_t* op_count_host = nullptr;
 };
 
 static hipEvent_t new_event(hipStream_t st) {
@@ -207,6 +211,7 @@ extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
   (void)hipSetDevice(e->device);
   for (void* p : e->allocs) (void)hipFree(p);
   for (void* p : e->f32_ws) (void)hipFree(p);
+  if (e->op_count_host) (void)hipHostFree(e->op_count_host);
   if (e->host_flags) (void)hipHostFree(e->host_flags);
   for (auto ev : e->poll_ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -634,4 +639,71 @@ extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const 
   if ((r = run_f32_layer(e, 3, Tp, n, n_pad, e->f32_yb, ENC_F32_NEXT, e->f32_ya, lens, Tp, st))) return r;
   if ((r = run_f32_layer(e, 4, Tp, n, n_pad, e->f32_ya, ENC_F32_FINAL, f_out, lens, Tp, st))) return r;
   return 0;
+}
+
+// ---------------------------------------------------------------- operator-level decode
+// torch.ops.intel_mlperf lstm_amx_bf16 / amx_linear_bf16_accum_relu / amx_linear_i16o32 /
+// greedy_decode_update (reference models/modeling_rnnt.py:202, 269-283, 331-365) on the bound
+// model, for the reference's op-by-op Python loop (models/decoder.py:171-212).
+static int check_rows(int n_pad) { return n_pad > 0 && n_pad % 16 == 0; }
+
+extern "C" int rnnt_op_lstm_bf16(rnnt_engine* e, const uint16_t* x, const uint16_t* hx, const float* cx, uint16_t* hy,
+                                 float* cy, int n_pad, void* stream) {
+  if (!e || !x || !hx || !cx || !hy || !cy) return fail(RNNT_EINVAL, "null argument");
+  if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = pick(e, stream);
+  const size_t NP = (size_t)n_pad * P;
+  if (launch_op_lstm_bf16(e->dw, 0, x, hx, cx, hy, cy, n_pad, st) ||
+      launch_op_lstm_bf16(e->dw, 1, hy, hx + NP, cx + NP, hy + NP, cy + NP, n_pad, st))
+    return fail(RNNT_EDEVICE, "lstm_bf16 launch failed");
+  return 0;
+}
+
+extern "C" int rnnt_op_joint_hidden(rnnt_engine* e, const float* f, const uint16_t* g, uint16_t* y1, int n_pad,
+                                    void* stream) {
+  if (!e || !f || !g || !y1) return fail(RNNT_EINVAL, "null argument");
+  if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
+  HIPCHK(hipSetDevice(e->device));
+  if (launch_op_joint_hidden(e->dw, f, g, y1, n_pad, pick(e, stream))) return fail(RNNT_EDEVICE, "joint launch failed");
+  return 0;
+}
+
+extern "C" int rnnt_op_joint_logits(rnnt_engine* e, const uint16_t* y1, float* logits, int n_pad, void* stream) {
+  if (!e || !y1 || !logits) return fail(RNNT_EINVAL, "null argument");
+  if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
+  HIPCHK(hipSetDevice(e->device));
+  if (launch_op_joint_logits(e->dw, y1, logits, n_pad, pick(e, stream))) return fail(RNNT_EDEVICE, "linear2 launch failed");
+  return 0;
+}
+
+__global__ void op_count_unfinished_kernel(const int32_t* finish, int n, int32_t* count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !finish[i]) atomicAdd(count, 1);
+}
+
+extern "C" int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int32_t* symbols_added, int32_t* res,
+                                     int32_t* res_idx, const float* f, const int32_t* f_lens, int32_t* time_idx,
+                                     float* fi, int32_t* pre_g, uint16_t* pre_hg, float* pre_cg, const uint16_t* hg,
+                                     const float* cg, int32_t* finish, int n, int n_pad, int max_res, void* stream) {
+  if (!e || !symbols || !symbols_added || !res || !res_idx || !f || !f_lens || !time_idx || !fi || !pre_g || !pre_hg ||
+      !pre_cg || !hg || !cg || !finish)
+    return fail(RNNT_EINVAL, "null argument");
+  if (n <= 0 || n_pad < n || max_res <= 0) return fail(RNNT_EINVAL, "bad sizes");
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t st = pick(e, stream);
+  if (!e->op_count) {
+    int r = dev_alloc(e, &e->op_count, 4);
+    if (r) return r;
+    HIPCHK(hipHostMalloc((void**)&e->op_count_host, sizeof(int32_t)));
+  }
+  GreedyUpdateArgs a{symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg,
+                     finish, e->op_count + 1, n, n_pad, max_res};
+  if (launch_op_greedy_update(a, st)) return fail(RNNT_EDEVICE, "greedy_update launch failed");
+  HIPCHK(hipMemsetAsync(e->op_count, 0, sizeof(int32_t), st));
+  hipLaunchKernelGGL(op_count_unfinished_kernel, dim3((n + 255) / 256), dim3(256), 0, st, finish, n, e->op_count);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->op_count_host, e->op_count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return *e->op_count_host == 0 ? 1 : 0;  // all(finish), the op's bool result
 }

@@ -49,6 +49,10 @@ _SIGS = {
     "rnnt_engine_encode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                      C.c_void_p, C.c_void_p]),
     "rnnt_engine_decode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "rnnt_op_lstm_bf16": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_void_p]),
+    "rnnt_op_joint_hidden": (C.c_int, [C.c_void_p] * 4 + [C.c_int, C.c_void_p]),
+    "rnnt_op_joint_logits": (C.c_int, [C.c_void_p] * 3 + [C.c_int, C.c_void_p]),
+    "rnnt_op_greedy_update": (C.c_int, [C.c_void_p] * 15 + [C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "rnnt_engine_load_f32_encoder": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                                C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "rnnt_engine_encode_f32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,

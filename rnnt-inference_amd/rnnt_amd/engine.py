@@ -140,6 +140,31 @@ class Engine:
         rc = self._lib.rnnt_op_stack_time(self._h, _ptr(x), _ptr(x_lens), T, n_pad, Cc, _ptr(y), _stream_handle(stream))
         _lib.check(rc, "rnnt_op_stack_time")
 
+    # ---------------------------------------------------------------- op-level decode
+    def op_lstm_bf16(self, x, hx, cx, hy, cy, stream=None):
+        """x bf16-bits int16 [n_pad, 320]; hx/hy int16 [2, n_pad, 320]; cx/cy f32 [2, n_pad, 320]."""
+        rc = self._lib.rnnt_op_lstm_bf16(self._h, _ptr(x), _ptr(hx), _ptr(cx), _ptr(hy), _ptr(cy), x.shape[0],
+                                         _stream_handle(stream))
+        _lib.check(rc, "rnnt_op_lstm_bf16")
+
+    def op_joint_hidden(self, f, g, y1, stream=None):
+        rc = self._lib.rnnt_op_joint_hidden(self._h, _ptr(f), _ptr(g), _ptr(y1), f.shape[0], _stream_handle(stream))
+        _lib.check(rc, "rnnt_op_joint_hidden")
+
+    def op_joint_logits(self, y1, logits, stream=None):
+        rc = self._lib.rnnt_op_joint_logits(self._h, _ptr(y1), _ptr(logits), y1.shape[0], _stream_handle(stream))
+        _lib.check(rc, "rnnt_op_joint_logits")
+
+    def op_greedy_update(self, symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg,
+                         hg, cg, finish, n, stream=None):
+        rc = self._lib.rnnt_op_greedy_update(self._h, *[_ptr(t) for t in (symbols, symbols_added, res, res_idx, f, f_lens,
+                                                                           time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg,
+                                                                           finish)],
+                                             n, fi.shape[0], res.shape[1], _stream_handle(stream))
+        if rc < 0:
+            _lib.check(rc, "rnnt_op_greedy_update")
+        return rc == 1
+
     def close(self):
         if getattr(self, "_h", None):
             self._lib.rnnt_engine_destroy(self._h)

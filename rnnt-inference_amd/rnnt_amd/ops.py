@@ -136,3 +136,75 @@ def greedy_decode(n, max_res=None):
     rl = torch.empty(n, dtype=torch.int32, device="cuda")
     e.decode(res, rl)
     return res, rl
+
+
+# ---------------------------------------------------------------- decode operators
+# The reference's op-by-op greedy loop (models/decoder.py:171-212) calls these four; tensors use
+# torch's bfloat16 / float32 / int32 dtypes and the reference's shapes.  Weight arguments are
+# accepted for signature compatibility and checked against the bound model's shapes; the
+# engine computes with its own packed copy (as for lstm_amx_int8).
+
+def _bits(t):
+    import torch
+    return t.contiguous().view(torch.int16)
+
+
+def lstm_amx_bf16(x, hx, cx, weights=None):
+    """modeling_rnnt.py:202: x bf16 [1, N, 320]; hx: 2 x bf16 [N, 320]; cx: 2 x fp32 [N, 320]
+    -> (g bf16 [1, N, 320], hy, cy)."""
+    import torch
+    e = _engine()
+    N = x.shape[-2]
+    _check(x.shape[-1] == R.pred_hidden_size and len(hx) == 2 and len(cx) == 2, "lstm_amx_bf16: bad shapes")
+    n_pad = (N + 15) // 16 * 16
+    xb = torch.zeros((n_pad, R.pred_hidden_size), dtype=torch.bfloat16, device=x.device)
+    xb[:N] = x.reshape(N, -1)
+    h = torch.zeros((2, n_pad, R.pred_hidden_size), dtype=torch.bfloat16, device=x.device)
+    c = torch.zeros((2, n_pad, R.pred_hidden_size), dtype=torch.float32, device=x.device)
+    for l in range(2):
+        h[l, :N] = hx[l]
+        c[l, :N] = cx[l]
+    hy, cy = torch.empty_like(h), torch.empty_like(c)
+    e.op_lstm_bf16(_bits(xb), _bits(h), c, _bits(hy).view(torch.int16), cy)
+    return hy[1, :N].unsqueeze(0), [hy[0, :N], hy[1, :N]], [cy[0, :N], cy[1, :N]]
+
+
+def amx_linear_bf16_accum_relu(f, w1_trans=None, g=None, w1_pred=None, bias=None):
+    """modeling_rnnt.py:269-275: f [N, 1024] (fp32 or bf16), g bf16 [N, 320] -> y1 bf16 [N, 512]."""
+    import torch
+    e = _engine()
+    N = f.shape[0]
+    n_pad = (N + 15) // 16 * 16
+    fp = torch.zeros((n_pad, R.trans_hidden_size), dtype=torch.float32, device=f.device)
+    fp[:N] = f.float()
+    gp = torch.zeros((n_pad, R.pred_hidden_size), dtype=torch.bfloat16, device=f.device)
+    gp[:N] = g.reshape(N, -1)
+    y1 = torch.empty((n_pad, R.joint_hidden_size), dtype=torch.bfloat16, device=f.device)
+    e.op_joint_hidden(fp, _bits(gp), y1.view(torch.int16))
+    return y1[:N]
+
+
+def amx_linear_i16o32(y, w2=None, b2=None):
+    """modeling_rnnt.py:280-283: y1 bf16 [N, 512] -> logits fp32 [N, 32] (29 labels + zero pad)."""
+    import torch
+    e = _engine()
+    N = y.shape[0]
+    n_pad = (N + 15) // 16 * 16
+    yp = torch.zeros((n_pad, R.joint_hidden_size), dtype=torch.bfloat16, device=y.device)
+    yp[:N] = y
+    logits = torch.empty((n_pad, 32), dtype=torch.float32, device=y.device)
+    e.op_joint_logits(yp.view(torch.int16), logits)
+    return logits[:N]
+
+
+def greedy_decode_update(symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg,
+                         finish):
+    """modeling_rnnt.py:331-365 (spec decoder.py:125-167), in place.  Device tensors: symbols,
+    symbols_added, res_idx, f_lens, time_idx, finish int32 [N]; res int32 [N, max_res]; f fp32
+    [T', n_pad, 1024]; fi fp32 [n_pad, 1024]; pre_g int32 [N]; pre_hg / hg bf16 [2, n_pad, 320];
+    pre_cg / cg fp32 [2, n_pad, 320].  Returns all(finish)."""
+    import torch
+    e = _engine()
+    N = symbols.shape[0]
+    return e.op_greedy_update(symbols.to(torch.int32).contiguous(), symbols_added, res, res_idx, f, f_lens, time_idx, fi,
+                              pre_g, pre_hg.view(torch.int16), pre_cg, hg.view(torch.int16), cg, finish, N)

@@ -110,3 +110,63 @@ def test_offline_sut_batches_in_flight(dec, model):
     assert sorted(two.responses) == sorted(one.responses)
     for k in one.responses:
         np.testing.assert_array_equal(two.responses[k], one.responses[k])
+
+
+def test_op_by_op_greedy_loop(dec, model, oracle):
+    """The reference's op-by-op decode loop (decoder.py:171-212 greedy_decode_quant) written
+    with the four decode operators (lstm_amx_bf16, amx_linear_bf16_accum_relu,
+    amx_linear_i16o32, greedy_decode_update) gives the same tokens as the fused device loop
+    and the CPU restatement."""
+    from rnnt_amd import ops
+    from rnnt_amd.config import RNNTParam as R
+    e = dec.engine
+    lens = np.array([57, 31, 12, 44, 3], np.int32)
+    N, T = len(lens), int(lens.max())
+    n_pad = 256
+    x = synthetic.make_features(T, n_pad, seed=21, lens=np.pad(lens, (0, n_pad - N)))
+    xd = torch.from_numpy(x).cuda()
+    ld = torch.from_numpy(np.pad(lens, (0, n_pad - N))).cuda()
+    Tp = (T + 1) // 2
+    f = torch.empty((Tp, n_pad, 1024), dtype=torch.float32, device="cuda")
+    e.encode(xd, ld, lens, n=N, f_out=f)
+    max_res = 30 * Tp
+    # fused loop
+    res_f = torch.empty((N, max_res), dtype=torch.int32, device="cuda")
+    rl_f = torch.empty(N, dtype=torch.int32, device="cuda")
+    e.decode(res_f, rl_f)
+    # op-by-op loop
+    dev = "cuda"
+    f_lens = torch.from_numpy((lens + 1) // 2).to(dev)
+    symbols_added = torch.zeros(N, dtype=torch.int32, device=dev)
+    time_idx = torch.zeros(N, dtype=torch.int32, device=dev)
+    finish = (f_lens == 0).to(torch.int32)
+    res = torch.full((N, max_res), R.SOS, dtype=torch.int32, device=dev)
+    res_idx = torch.full((N,), -1, dtype=torch.int32, device=dev)
+    pre_g = torch.full((N,), R.SOS, dtype=torch.int32, device=dev)
+    pre_hg = torch.zeros((2, n_pad, 320), dtype=torch.bfloat16, device=dev)
+    pre_cg = torch.zeros((2, n_pad, 320), dtype=torch.float32, device=dev)
+    fi = f[0].clone()
+    embed = torch.from_numpy(np.asarray(model.embed, np.float32)).to(dev).to(torch.bfloat16)
+    for _ in range(30 * Tp + Tp + 2):
+        sos = pre_g.eq(R.SOS)
+        xg = embed[pre_g.clamp(min=0).long()].masked_fill(sos[:, None], 0.0)  # modeling_rnnt.py:193-197
+        g, hgl, cgl = ops.lstm_amx_bf16(xg.unsqueeze(0), [pre_hg[0, :N], pre_hg[1, :N]], [pre_cg[0, :N], pre_cg[1, :N]])
+        hg = torch.zeros_like(pre_hg)
+        cg = torch.zeros_like(pre_cg)
+        for l in range(2):
+            hg[l, :N] = hgl[l]
+            cg[l, :N] = cgl[l]
+        y1 = ops.amx_linear_bf16_accum_relu(fi[:N], None, g[0])
+        logits = ops.amx_linear_i16o32(y1)
+        assert torch.all(logits[:, R.num_labels:] == 0)
+        symbols = torch.argmax(logits[:, : R.num_labels], dim=1).to(torch.int32)
+        if ops.greedy_decode_update(symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg,
+                                    hg, cg, finish):
+            break
+    else:
+        raise AssertionError("op-by-op loop did not finish")
+    np.testing.assert_array_equal((res_idx + 1).cpu().numpy(), rl_f.cpu().numpy())
+    np.testing.assert_array_equal(res.cpu().numpy(), res_f.cpu().numpy())
+    fo = f.cpu().numpy()[:, :N]
+    ro, rlo, _ = oracle.greedy_decode(model, fo, (lens + 1) // 2, max_res=max_res)
+    np.testing.assert_array_equal(res.cpu().numpy(), ro)

@@ -10,7 +10,8 @@ build() {
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c engine.hip -o $OUTD/eng_$1.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c decoder.hip -o $OUTD/dec_$1.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c encoder_f32.hip -o $OUTD/f32_$1.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUTD/eng_$1.o $OUTD/dec_$1.o $OUTD/enc_$1.o $OUTD/f32_$1.o -o $OUTD/lib_$1.so
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c decoder_ops.hip -o $OUTD/dops_$1.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUTD/eng_$1.o $OUTD/dec_$1.o $OUTD/enc_$1.o $OUTD/f32_$1.o $OUTD/dops_$1.o -o $OUTD/lib_$1.so
 }
 for v in "$@"; do
   case $v in
