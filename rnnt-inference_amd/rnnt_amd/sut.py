@@ -146,3 +146,132 @@ class OfflineSUT:
 
     def flush_queries(self):
         pass
+
+
+class GpuQSL:
+    """QSL with every sample's features resident in HBM, ragged ([sum T_i, 240] fp32), and the
+    AssembleSamples gather done on the device (LoadSamplesToRam + AssembleSamples,
+    rnnt_qsl.cpp:150-188).  Synthetic N(0,1) features, seeded."""
+
+    def __init__(self, lengths, seed, device="cuda"):
+        import torch
+        self.lengths = np.asarray(lengths, np.int32)
+        self.count = len(self.lengths)
+        self.offsets = np.concatenate([[0], np.cumsum(self.lengths)[:-1]]).astype(np.int64)
+        g = torch.Generator(device=device)
+        g.manual_seed(int(seed))
+        self.feats = torch.randn((int(self.lengths.sum()), R.trans_input_size), device=device, generator=g)
+        self.device = device
+
+    def __len__(self):
+        return self.count
+
+    def assemble(self, indices, n_pad=None):
+        """-> (x cuda [T_max, n_pad, 256] fp32, lens cuda int32 [n_pad], lens_host [n])."""
+        import torch
+        idx = np.asarray(indices, np.int64)
+        n = len(idx)
+        n_pad = n_pad or pad_batch(n)
+        bl = self.lengths[idx].astype(np.int32)
+        lp = np.zeros(n_pad, np.int32)
+        lp[:n] = bl
+        T = int(bl.max())
+        t = torch.arange(T, device=self.device)[:, None]
+        ln = torch.from_numpy(bl).to(self.device)[None, :]
+        rows = torch.from_numpy(self.offsets[idx]).to(self.device)[None, :] + t
+        valid = t < ln
+        x = torch.zeros((T, n_pad, R.PADDED_INPUT_SIZE), dtype=torch.float32, device=self.device)
+        x[:, :n, : R.trans_input_size] = self.feats[torch.where(valid, rows, 0)] * valid[..., None]
+        return x, torch.from_numpy(lp).to(self.device), bl
+
+
+class ServerSUT:
+    """Server scenario SUT (reference ServerSUT, csrc/torch_sut.cpp:238-571, with
+    PipelineState continuous batching, metadata.cpp:97-194).  MI355X form: one worker thread
+    per engine (HIP stream each); whenever a worker is free it takes every pending sample (up
+    to max_batch, longest first), assembles the batch on the device, encodes (encoders take
+    turns), decodes and completes each sample with its token row.  A batch's latency on the GPU
+    (tens of ms) is far below the 1 s Server budget, so dynamic batching replaces the
+    reference's slot refilling.  Latency per sample = completion - issue time."""
+
+    def __init__(self, engines, qsl, max_batch=2048, on_complete=None):
+        import threading
+        self.engines = list(engines) if isinstance(engines, (list, tuple)) else [engines]
+        self.qsl, self.max_batch = qsl, max_batch
+        self.on_complete = on_complete
+        self.responses, self.latency = {}, {}
+        self._pending = []  # (issue_time, QuerySample)
+        self._cv = threading.Condition()
+        self._enc_lock = threading.Lock()
+        self._stop = False
+        self._threads = []
+        self.batches = 0
+        self.errors = []
+
+    def start(self):
+        import threading
+        for j in range(len(self.engines)):
+            t = threading.Thread(target=self._worker, args=(j,), daemon=True)
+            t.start()
+            self._threads.append(t)
+
+    def issue_query(self, samples, now=None):
+        import time
+        now = time.perf_counter() if now is None else now
+        with self._cv:
+            self._pending.extend((now, s) for s in samples)
+            self._cv.notify()
+
+    def stop(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        for t in self._threads:
+            t.join()
+
+    def _take(self):
+        with self._cv:
+            while not self._pending and not self._stop:
+                self._cv.wait()
+            if not self._pending:
+                return None
+            batch = self._pending[: self.max_batch]
+            del self._pending[: self.max_batch]
+            return batch
+
+    def _worker(self, j):
+        import time
+        import torch
+        eng = self.engines[j]
+        st = torch.cuda.Stream()
+        while True:
+            batch = self._take()
+            if batch is None:
+                return
+            try:
+                batch.sort(key=lambda b: -int(self.qsl.lengths[b[1].index]))  # rnnt_qsl.cpp:104-133
+                n = len(batch)
+                with torch.cuda.stream(st):
+                    x, lens, bl = self.qsl.assemble([b[1].index for b in batch])
+                    res = torch.empty((n, eng.max_res), dtype=torch.int32, device="cuda")
+                    rl = torch.empty(n, dtype=torch.int32, device="cuda")
+                with self._enc_lock:
+                    eng.encode(x, lens, bl, n=n, stream=st)
+                    st.synchronize()
+                eng.decode(res, rl, stream=st)
+                with torch.cuda.stream(st):
+                    rlh = rl.cpu()
+                    toks = res[:, : max(1, int(rlh.max()))].cpu().numpy()
+                done = time.perf_counter()
+                rlh = rlh.numpy()
+                for i, (t0, s) in enumerate(batch):
+                    row = toks[i, : rlh[i]].copy()
+                    self.responses[s.id] = row
+                    self.latency[s.id] = done - t0
+                    if self.on_complete:
+                        self.on_complete(s, row)
+                self.batches += 1
+            except Exception as ex:  # surface in the caller, never hang the query
+                self.errors.append(ex)
+                for t0, s in batch:
+                    self.latency[s.id] = float("inf")

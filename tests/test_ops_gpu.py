@@ -170,3 +170,37 @@ def test_op_by_op_greedy_loop(dec, model, oracle):
     fo = f.cpu().numpy()[:, :N]
     ro, rlo, _ = oracle.greedy_decode(model, fo, (lens + 1) // 2, max_res=max_res)
     np.testing.assert_array_equal(res.cpu().numpy(), ro)
+
+
+def test_server_sut_dynamic_batching(dec, model):
+    """ServerSUT (dynamic batching over two engines in flight) answers every sample with the
+    same tokens as the Offline path, whatever batches the arrivals happened to form."""
+    import time
+    from rnnt_amd.engine import Engine
+    from rnnt_amd.sut import GpuQSL, OfflineSUT, QuerySample, ServerSUT
+    lengths = np.minimum(synthetic.devclean_lengths(40, seed=51), 128)
+    qsl = GpuQSL(lengths, seed=52)
+    e2 = Engine(model, device=0, max_batch=64, max_frames=128)
+    try:
+        srv = ServerSUT([dec.engine, e2], qsl, max_batch=16)
+        srv.start()
+        samples = [QuerySample(id=i, index=i) for i in range(len(lengths))]
+        for k in range(0, len(samples), 7):
+            srv.issue_query(samples[k:k + 7])
+            time.sleep(0.002)
+        deadline = time.time() + 60
+        while len(srv.latency) < len(samples) and time.time() < deadline:
+            time.sleep(0.01)
+        srv.stop()
+        assert not srv.errors and len(srv.responses) == len(samples)
+        # reference answers: one Offline batch of the same samples (assembled from the same features)
+        x, lens, bl = qsl.assemble(list(range(len(lengths))))
+        n = len(lengths)
+        res = torch.empty((n, dec.engine.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(n, dtype=torch.int32, device="cuda")
+        dec.engine.infer(x, lens, bl, res, rl, n=n)
+        res, rl = res.cpu().numpy(), rl.cpu().numpy()
+        for i in range(n):
+            np.testing.assert_array_equal(srv.responses[i], res[i, : rl[i]])
+    finally:
+        e2.close()
