@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RNNT_ABI_VERSION 3
+#define RNNT_ABI_VERSION 4
 
 #define RNNT_OK 0
 #define RNNT_EINVAL (-22)
@@ -156,6 +156,44 @@ int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int32_t* symbo
                           int32_t* res_idx, const float* f, const int32_t* f_lens, int32_t* time_idx, float* fi,
                           int32_t* pre_g, uint16_t* pre_hg, float* pre_cg, const uint16_t* hg, const float* cg,
                           int32_t* finish, int n, int n_pad, int max_res, void* stream);
+
+/* ---- audio front end (the reference's AudioProcessor / FilterbankFeatures.forward,
+ * datasets/parts/features.py:185-252, csrc/rnnt_processor.hpp:29-48; used when WAV=true,
+ * launch_sut.sh:54).  Geometry fixed to configs/rnnt.toml [input_eval]; the window and filterbank
+ * are the module's buffers (torch.hann_window(320, periodic=False), librosa.filters.mel(16000, 512,
+ * 80) -- features.py:134-154), passed in as data. */
+typedef struct rnnt_featurizer rnnt_featurizer;
+typedef struct {
+  int sample_rate;     /* 16000 */
+  int n_fft;           /* 512 */
+  int win_length;      /* 320 = sample_rate * window_size */
+  int hop_length;      /* 160 = sample_rate * window_stride */
+  int nfilt;           /* 80 */
+  int frame_splicing;  /* 3 */
+  int pad_out_feat;    /* 256 (run_mode quant: pad_out_feat=True, process_librispeech.py:104) */
+  float preemph;       /* 0.97 (0 disables) */
+  float dither;        /* 1e-5: dither^2 is added to the power spectrum (features.py:219-220) */
+  float log_guard;     /* fb_bias 1e-20 (features.py:158-160) */
+  float norm_eps;      /* i_layernorm_pad eps 1e-12 (features.py:243-249) */
+} rnnt_featurizer_config;
+
+/* window host fp32 [win_length]; fb host fp32 [nfilt][n_fft/2+1]. */
+int rnnt_featurizer_create(const rnnt_featurizer_config* cfg, const float* window, const float* fb, int device,
+                           rnnt_featurizer** out);
+void rnnt_featurizer_destroy(rnnt_featurizer* f);
+/* Feature frames of a wav_len-sample utterance: ceil((1 + floor(wav_len/hop)) / 3), 0 for 0. */
+int64_t rnnt_featurizer_frames(int64_t wav_len);
+/* wav device fp32: row n's samples at wav + offsets[n] (offsets device int64 [n]) or, with
+ * offsets == NULL, at wav + n * stride (the reference's zero-padded [N][maxLength] batch,
+ * rnnt_qsl.cpp:166-179).  wav_lens device int32 [n] and the same on the host (wav_lens_host).
+ * Writes feats device fp32 [T_out][n_pad][256] -- the encoder's input layout -- normalised per
+ * utterance and channel, zero past feat_lens[n], in channels 240..255 and in rows n..n_pad-1;
+ * feat_lens device int32 [n_pad].  T_out >= the longest utterance's frames (else RNNT_EINVAL).
+ * The reference returns [n_pad][256][T] (features.py:241-250); the C++ SUT permutes it to this
+ * layout before encode (torch_sut.cpp:200). */
+int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
+                        const int32_t* wav_lens, const int32_t* wav_lens_host, int n, int n_pad, float* feats,
+                        int32_t* feat_lens, int T_out, void* stream);
 
 #ifdef __cplusplus
 }

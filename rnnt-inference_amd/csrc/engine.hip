@@ -28,6 +28,7 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+int rnnt_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
 #define HIPCHK(x)                                                                              \
   do {                                                                                         \
     hipError_t e_ = (x);                                                                       \

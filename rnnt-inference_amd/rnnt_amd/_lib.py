@@ -39,7 +39,19 @@ class RnntStats(C.Structure):
                 ("step_launches", C.c_int64), ("decode_steps", C.c_int64), ("encode_calls", C.c_int64), ("decode_calls", C.c_int64)]
 
 
+class RnntFeaturizerConfig(C.Structure):
+    _fields_ = [("sample_rate", C.c_int), ("n_fft", C.c_int), ("win_length", C.c_int), ("hop_length", C.c_int),
+                ("nfilt", C.c_int), ("frame_splicing", C.c_int), ("pad_out_feat", C.c_int),
+                ("preemph", C.c_float), ("dither", C.c_float), ("log_guard", C.c_float), ("norm_eps", C.c_float)]
+
+
 _SIGS = {
+    "rnnt_featurizer_create": (C.c_int, [C.POINTER(RnntFeaturizerConfig), C.c_void_p, C.c_void_p, C.c_int,
+                                         C.POINTER(C.c_void_p)]),
+    "rnnt_featurizer_destroy": (None, [C.c_void_p]),
+    "rnnt_featurizer_frames": (C.c_int64, [C.c_int64]),
+    "rnnt_featurizer_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
+                                      C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "rnnt_engine_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "rnnt_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(RnntStats), C.c_int]),
     "rnnt_abi_version": (C.c_int, []),

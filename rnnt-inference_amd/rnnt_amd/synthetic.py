@@ -10,6 +10,8 @@ SURVEY 8c (plain default-init weights give degenerate decodes): encoder LSTM wei
 U(+-4/sqrt(H)), joint fc1 std 0.1, fc2 std 0.3 and a positive blank bias, tuned so greedy
 decoding emits a LibriSpeech-like ~0.5 symbols per encoder frame and stays input-dependent.
 """
+import math
+
 import numpy as np
 
 from .config import RNNTParam as R
@@ -152,3 +154,53 @@ def devclean_lengths(count, seed, max_frames=R.MAX_FEA_LEN, min_frames=47):
 def uniform_lengths(count, seed, lo=47, hi=R.MAX_FEA_LEN):
     rng = np.random.default_rng(seed)
     return rng.integers(lo, hi + 1, size=count).astype(np.int32)
+
+
+def wav_lengths_for_frames(frames, seed):
+    """Sample counts whose spliced feature length is exactly frames[i]:
+    ceil((floor(L/160) + 1) / 3) = T  <=>  480 (T-1) <= L < 480 T  (features.py:212, :237)."""
+    rng = np.random.default_rng(seed)
+    f = np.asarray(frames, np.int64)
+    return (480 * (f - 1) + rng.integers(0, 480, size=f.shape)).astype(np.int32)
+
+
+def make_wavs(lengths, seed, device="cpu"):
+    """Speech-shaped synthetic 16 kHz audio, one float32 torch tensor per length on `device`:
+    voiced segments of 80-400 ms (f0 90-250 Hz with drift, 4 harmonics, random spectral tilt),
+    unvoiced noise bursts and exact-zero pauses (which exercise the dither floor), under a
+    per-segment amplitude envelope in roughly [-1, 1] like librosa's float loads."""
+    import torch
+    rng = np.random.default_rng(seed)
+    out = []
+    for L in np.asarray(lengths, np.int64):
+        L = int(L)
+        if L == 0:
+            out.append(torch.zeros(0, dtype=torch.float32, device=device))
+            continue
+        bounds, t = [0], 0
+        while t < L:
+            t = min(L, t + int(rng.integers(1280, 6400)))
+            bounds.append(t)
+        nseg = len(bounds) - 1
+        kind = rng.choice(3, size=nseg, p=[0.7, 0.2, 0.1])  # voiced / noise / silence
+        seg_id = np.repeat(np.arange(nseg), np.diff(bounds))
+        f0 = rng.uniform(90.0, 250.0, nseg)
+        drift = rng.uniform(-0.5, 0.5, nseg)
+        amp = np.exp(rng.uniform(np.log(0.01), np.log(0.5), nseg))
+        tilt = rng.uniform(0.3, 0.9, nseg)
+        g = torch.Generator().manual_seed(int(rng.integers(0, 2 ** 31)))
+        noise = torch.randn(L, generator=g).to(device)
+        sid = torch.from_numpy(seg_id).to(device)
+        pos = torch.arange(L, device=device, dtype=torch.float64)
+        start = torch.from_numpy(np.asarray(bounds[:-1], np.float64)).to(device)[sid]
+        tt = (pos - start) / 16000.0
+        f = torch.from_numpy(f0).to(device)[sid] * (1.0 + torch.from_numpy(drift).to(device)[sid] * tt)
+        phase = 2.0 * math.pi * torch.cumsum(f / 16000.0, 0)
+        til = torch.from_numpy(tilt).to(device)[sid]
+        voiced = sum(til ** k * torch.sin(phase * (k + 1)) for k in range(4))
+        k_t = torch.from_numpy(kind).to(device)[sid]
+        sig = torch.where(k_t == 0, voiced + 0.05 * noise.double(), 0.6 * noise.double())
+        sig = torch.where(k_t == 2, torch.zeros_like(sig), sig)
+        sig = sig * torch.from_numpy(amp).to(device)[sid]
+        out.append(sig.clamp(-1.0, 1.0).float())
+    return out

@@ -1,0 +1,130 @@
+"""HIP featurizer (rnnt_featurizer_run) vs the float64 restatement (oracle/featurizer.py).
+
+Tolerance: the GPU computes in fp32 (radix-4 FFT, fp32 mel sums, logf) and the oracle in
+float64; normalised features agree to FEAT_TOL absolute (unit-variance features, so this is
+also ~relative).  Padding (time past feat_lens, channels 240..255, batch rows past n) and the
+lengths are exact.  Rows are independent: a row's features are bit-identical whatever batch it
+is in and whether samples come from a zero-padded [N][stride] batch or ragged storage + offsets.
+"""
+import numpy as np
+import pytest
+
+from oracle import featurizer as OF
+from rnnt_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+FEAT_TOL = 2e-3
+
+# configs/rnnt.toml [input_eval] (the reference's featurizer kwargs; /root/reference is not on the GPU box)
+INPUT_EVAL = dict(normalize="per_feature", sample_rate=16000, window_size=0.02, window_stride=0.01, window="hann",
+                  features=80, n_fft=512, frame_splicing=3, dither=0.00001, feat_type="logfbank", pad_to=0)
+
+LENS = [0, 1, 100, 257, 479, 480, 16037, 160 * 96 + 5, 96000, 239999, 240000]
+
+
+@pytest.fixture(scope="module")
+def fz():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rnnt_amd.featurizer import AudioProcessing
+    proc = AudioProcessing("quant", **INPUT_EVAL)
+    yield proc.featurizer
+    proc.featurizer.close()
+
+
+def _batch(wavs):
+    n, L = len(wavs), max([len(w) for w in wavs] + [1])
+    x = torch.zeros((n, L), dtype=torch.float32)
+    for i, w in enumerate(wavs):
+        x[i, :len(w)] = w.cpu()
+    return x.cuda(), torch.tensor([len(w) for w in wavs], dtype=torch.int32)
+
+
+def _oracle(fz, wavs, n_pad, T_out):
+    return OF.featurize([w.double().numpy() for w in wavs], fz.window, fz.fb, n_pad=n_pad, T_out=T_out,
+                        preemph=0.97, dither=1e-5)
+
+
+def test_gpu_vs_oracle_ragged(fz):
+    wavs = synthetic.make_wavs(LENS, seed=21)
+    x, lens = _batch(wavs)
+    n_pad, T_out = 16, 505
+    feats, flen = fz.featurize(x, lens.cuda(), lens.numpy(), n_pad=n_pad, T_out=T_out)
+    torch.cuda.synchronize()
+    ref, rlen = _oracle(fz, wavs, n_pad, T_out)
+    g = feats.cpu().numpy()
+    np.testing.assert_array_equal(flen.cpu().numpy(), rlen)
+    assert rlen.tolist()[:len(LENS)] == [OF.frames(L)[1] for L in LENS]
+    pad = ref == 0.0
+    assert np.all(g[pad] == 0.0)  # exact zeros in every padding position
+    err = np.abs(g.astype(np.float64) - ref).max()
+    assert err <= FEAT_TOL, err
+    print("max |gpu - oracle| =", err)
+
+
+def test_offsets_and_batch_invariance(fz):
+    L = [48000, 3200, 0, 777, 150000]
+    wavs = synthetic.make_wavs(L, seed=22)
+    x, lens = _batch(wavs)
+    a, al = fz.featurize(x, lens.cuda(), lens.numpy(), n_pad=8, T_out=320)
+    flat = torch.cat([w.cuda() for w in wavs] + [torch.zeros(1, device="cuda")])
+    off = torch.tensor(np.concatenate([[0], np.cumsum(L)[:-1]]), dtype=torch.int64, device="cuda")
+    b, bl = fz.featurize(flat, lens.cuda(), lens.numpy(), n_pad=8, T_out=320, offsets=off)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a.cpu().numpy().view(np.uint32), b.cpu().numpy().view(np.uint32))
+    np.testing.assert_array_equal(al.cpu().numpy(), bl.cpu().numpy())
+    # one row alone (same T_out) == the same row inside the batch
+    c, _ = fz.featurize(x[4:5].contiguous(), lens[4:5].cuda(), lens[4:5].numpy(), n_pad=1, T_out=320)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(c.cpu().numpy()[:, 0].view(np.uint32), a.cpu().numpy()[:, 4].view(np.uint32))
+
+
+def test_forward_mirror_layout(fz):
+    wavs = synthetic.make_wavs([16000, 8000, 4000], seed=23)
+    x, lens = _batch(wavs)
+    y, yl = fz(x, lens, pad_batch_size=True)  # features.py:185-252 signature
+    torch.cuda.synchronize()
+    T = OF.frames(16000)[1]
+    assert tuple(y.shape) == (32, 256, T) and yl.shape[0] == 32
+    assert yl.cpu().tolist()[:4] == [T, OF.frames(8000)[1], OF.frames(4000)[1], 0]
+    ref, _ = _oracle(fz, wavs, 32, T)
+    assert np.abs(y.permute(2, 0, 1).cpu().numpy() - ref).max() <= FEAT_TOL
+
+
+def test_t_out_too_small_raises(fz):
+    from rnnt_amd._lib import EngineError
+    wavs = synthetic.make_wavs([240000], seed=24)
+    x, lens = _batch(wavs)
+    with pytest.raises(EngineError):
+        fz.featurize(x, lens.cuda(), lens.numpy(), n_pad=1, T_out=500)  # 15 s = 501 frames
+
+
+def test_wav_to_tokens_matches_oracle(fz, oracle):
+    """featurizer -> int8 engine end to end: tokens identical to the CPU restatement run on the
+    GPU features (the encoder/decoder parity of tests/test_gpu_parity.py, fed by the front end)."""
+    from rnnt_amd import weights
+    from rnnt_amd.engine import Engine
+    pm, _ = weights.build_model()
+    frames = np.array([60, 41, 17, 3, 1], np.int64)
+    L = synthetic.wav_lengths_for_frames(frames, seed=25)
+    wavs = synthetic.make_wavs(L, seed=25)
+    x, lens = _batch(wavs)
+    T, n, n_pad = int(frames.max()), len(L), 256
+    feats, flen = fz.featurize(x, lens.cuda(), lens.numpy(), n_pad=n_pad, T_out=T)
+    e = Engine(pm, device=0, max_batch=256, max_frames=500)
+    try:
+        res = torch.empty((n, e.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(n, dtype=torch.int32, device="cuda")
+        fl_host = flen.cpu().numpy()
+        e.infer(feats, flen, fl_host[:n], res, rl, n=n)
+        torch.cuda.synchronize()
+    finally:
+        e.close()
+    assert fl_host[:n].tolist() == frames.tolist()
+    fo = oracle.encoder_i8(pm, np.ascontiguousarray(feats.cpu().numpy()[:, :n]), fl_host[:n])
+    ro, rlo, _ = oracle.greedy_decode(pm, fo, (fl_host[:n] + 1) // 2, max_res=res.shape[1])
+    np.testing.assert_array_equal(rl.cpu().numpy(), rlo)
+    np.testing.assert_array_equal(res.cpu().numpy(), ro)
+    assert rlo.sum() > 0

@@ -11,11 +11,17 @@ build() {
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c decoder.hip -o $OUTD/dec_$1.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c encoder_f32.hip -o $OUTD/f32_$1.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c decoder_ops.hip -o $OUTD/dops_$1.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUTD/eng_$1.o $OUTD/dec_$1.o $OUTD/enc_$1.o $OUTD/f32_$1.o $OUTD/dops_$1.o -o $OUTD/lib_$1.so
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w "${@:2}" -c featurizer.hip -o $OUTD/fz_$1.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OUTD/eng_$1.o $OUTD/dec_$1.o $OUTD/enc_$1.o $OUTD/f32_$1.o $OUTD/dops_$1.o $OUTD/fz_$1.o -o $OUTD/lib_$1.so
 }
 for v in "$@"; do
   case $v in
     base) build base ;;
+    fz_noload) build fz_noload -DRNNT_DEV_FZ_NO_LOAD ;;
+    fz_nofft) build fz_nofft -DRNNT_DEV_FZ_NO_FFT ;;
+    fz_nomel) build fz_nomel -DRNNT_DEV_FZ_NO_MEL ;;
+    fz_nofft_nomel) build fz_nofft_nomel -DRNNT_DEV_FZ_NO_FFT -DRNNT_DEV_FZ_NO_MEL ;;
+    fz_none) build fz_none -DRNNT_DEV_FZ_NO_LOAD -DRNNT_DEV_FZ_NO_FFT -DRNNT_DEV_FZ_NO_MEL ;;
     noepi) build noepi -DRNNT_DEV_NO_EPI ;;
     nomfma) build nomfma -DRNNT_DEV_NO_MFMA ;;
     nomfma_noepi) build nomfma_noepi -DRNNT_DEV_NO_MFMA -DRNNT_DEV_NO_EPI ;;

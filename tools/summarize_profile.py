@@ -23,7 +23,7 @@ def main():
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(src, "pmc*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
             agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     summary = {}
     for k, cs in agg.items():
