@@ -48,6 +48,9 @@ def parse():
                          "batch's latency-bound greedy decode overlaps the next batch's encoder")
     ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--wav", action="store_true",
+                    help="WAV=true path (launch_sut.sh:53-55): the QSL holds 16 kHz audio and every batch runs the "
+                         "GPU featurizer (FilterbankFeatures.forward) inside the timed region")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (profiles/), if present")
     return ap.parse_args()
@@ -90,6 +93,38 @@ def build_qsl(count, seed):
     return dict(lens=lens, offs=offs, feats=feats)
 
 
+def build_wav_qsl(count, seed):
+    """WAV QSL: speech-shaped synthetic 16 kHz audio stored ragged in HBM, with sample counts
+    drawn so the feature lengths follow the same dev-clean shape as build_qsl."""
+    lens = synthetic.devclean_lengths(count, seed=seed)
+    wav_lens = synthetic.wav_lengths_for_frames(lens, seed=seed)
+    store = torch.cat(synthetic.make_wavs(wav_lens, seed=seed, device="cuda"))
+    offs = np.concatenate([[0], np.cumsum(wav_lens.astype(np.int64))[:-1]]).astype(np.int64)
+    return dict(lens=lens, wav_lens=wav_lens, wav_offs=offs, store=store)
+
+
+def make_wav_batches(qsl, query, batch):
+    """As make_batches, but each batch keeps only its samples' offsets into the ragged audio;
+    its feature buffer [T_max, n_pad, 256] is filled by the featurizer inside every step."""
+    count = len(qsl["lens"])
+    ids = np.arange(query) % count
+    ids = ids[np.argsort(-qsl["lens"][ids], kind="stable")]
+    out = []
+    for i in range(0, len(ids), batch):
+        idx = ids[i:i + batch]
+        n = len(idx)
+        n_pad = pad_batch(n)
+        bl = qsl["lens"][idx].astype(np.int32)
+        wl = qsl["wav_lens"][idx].astype(np.int32)
+        T = int(bl.max())
+        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, wav_lens_host=wl,
+                        wav_lens=torch.from_numpy(wl).cuda(), wav_off=torch.from_numpy(qsl["wav_offs"][idx]).cuda(),
+                        lens=torch.zeros(n_pad, dtype=torch.int32, device="cuda"),
+                        x=torch.zeros((T, n_pad, 256), dtype=torch.float32, device="cuda")))
+    torch.cuda.synchronize()
+    return out
+
+
 def make_batches(qsl, query, batch):
     """The Offline query (sample i -> QSL index i % count, as LoadGen repeats the QSL),
     sorted longest-first and split into batches; each batch assembled in HBM as
@@ -117,7 +152,7 @@ def make_batches(qsl, query, batch):
     return out
 
 
-def run_step(engines, streams, batches):
+def run_step(engines, streams, batches, featurizers=None, store=None):
     """One Offline query.  Batch i runs on engine i % inflight, each engine with its own HIP
     stream and host thread (ctypes releases the GIL).  Encoders take turns (a lock held until
     the encode has finished on the GPU), so each batch's latency-bound greedy decode overlaps
@@ -129,6 +164,10 @@ def run_step(engines, streams, batches):
 
     def worker(j):
         for b in batches[j::k]:
+            if featurizers is not None:  # audio -> features on this batch's stream
+                featurizers[j].featurize(store, b["wav_lens"], b["wav_lens_host"], n=b["n"], n_pad=b["n_pad"],
+                                         T_out=b["T"], offsets=b["wav_off"], out=b["x"], feat_lens=b["lens"],
+                                         stream=streams[j])
             with enc_lock:
                 engines[j].encode(b["x"], b["lens"], b["lens_host"], n=b["n"], stream=streams[j])
                 streams[j].synchronize()
@@ -174,19 +213,25 @@ def main():
     args = parse()
     rank, local, world = dist_setup()
     pm, _ = weights.build_model()
-    qsl = build_qsl(args.qsl, seed=4 + 1000 * rank)
+    qsl = (build_wav_qsl if args.wav else build_qsl)(args.qsl, seed=4 + 1000 * rank)
     lens = qsl["lens"]
     engines = [Engine(pm, device=local, max_batch=min(args.batch, args.query), max_frames=500)
                for _ in range(args.inflight)]
     engine = engines[0]
     streams = [torch.cuda.Stream() for _ in engines]
-    batches = make_batches(qsl, args.query, args.batch)
+    batches = (make_wav_batches if args.wav else make_batches)(qsl, args.query, args.batch)
+    fzs, store = None, None
+    if args.wav:
+        from rnnt_amd.featurizer import FilterbankFeatures
+        fzs = [FilterbankFeatures(sample_rate=16000, window="hann", n_fft=512, nfilt=80, frame_splicing=3,
+                                  pad_out_feat=True, device=local) for _ in engines]
+        store = qsl["store"]
     for b in batches:  # response buffers, allocated once (the engine fills them every call)
         b["res"] = torch.empty((b["n"], engine.max_res), dtype=torch.int32, device="cuda")
         b["rl"] = torch.empty(b["n"], dtype=torch.int32, device="cuda")
 
     for _ in range(args.warmup):
-        run_step(engines, streams, batches)
+        run_step(engines, streams, batches, fzs, store)
     torch.cuda.synchronize()
     for e in engines:  # HIP events around every encode / joint_trans / greedy call, on its stream
         e.set_profiling(True)
@@ -194,7 +239,7 @@ def main():
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lens_out, _ = run_step(engines, streams, batches)
+        lens_out, _ = run_step(engines, streams, batches, fzs, store)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
@@ -240,10 +285,13 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "utterances/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int8",
-        "data": "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)",
+        "data": ("synthetic (seeded dev-clean-shaped speech-like 16 kHz audio, random-init RNN-T weights)" if args.wav
+                 else "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)"),
         "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
                    "qsl_per_gpu": args.qsl, "query_samples_per_gpu": args.query, "batch_size": args.batch,
                    "batches_in_flight": args.inflight,
+                   "input": ("16 kHz audio: GPU featurizer (FilterbankFeatures.forward) in the timed region" if args.wav
+                             else "log-mel features resident in HBM"),
                    "encoder": "int8 (lstm_amx_int8)",
                    "decoder": "bf16 prediction/joint, fp32 accumulate, greedy (device loop)",
                    "parallelism": f"dp{world} (one process per GPU, sharded queries)",

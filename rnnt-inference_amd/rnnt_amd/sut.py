@@ -185,6 +185,55 @@ class GpuQSL:
         return x, torch.from_numpy(lp).to(self.device), bl
 
 
+class GpuWavQSL:
+    """WAV=true QSL (launch_sut.sh:53-55; AssembleSamples(processor=true) + AudioProcessor,
+    rnnt_qsl.cpp:150-188, torch_sut.cpp:192-200): every sample's 16 kHz audio resident in HBM,
+    ragged, and ``assemble`` runs the GPU featurizer straight from that storage (per-row
+    offsets: no padded [N, max_len] copy) into the engine's [T, n_pad, 256] layout.  One
+    featurizer per calling thread (its workspace is per object), on the caller's stream.
+    ``lengths`` are the feature lengths (what the SUT sorts by), ``wav_lengths`` the samples."""
+
+    def __init__(self, wavs, device="cuda", featurizer_kwargs=None):
+        import threading
+        import torch
+        from .featurizer import feature_frames
+        self.wav_lengths = np.array([len(w) for w in wavs], np.int32)
+        self.lengths = np.array([feature_frames(int(v)) for v in self.wav_lengths], np.int32)
+        self.count = len(wavs)
+        self.offsets = np.concatenate([[0], np.cumsum(self.wav_lengths.astype(np.int64))[:-1]]).astype(np.int64)
+        self.store = torch.cat([torch.as_tensor(w, dtype=torch.float32).to(device) for w in wavs] +
+                               [torch.zeros(1, device=device)])
+        self.device = device
+        self._kw = dict(sample_rate=16000, window="hann", n_fft=512, nfilt=80, frame_splicing=3, pad_out_feat=True)
+        self._kw.update(featurizer_kwargs or {})
+        self._tls = threading.local()
+
+    def __len__(self):
+        return self.count
+
+    def _featurizer(self):
+        fz = getattr(self._tls, "fz", None)
+        if fz is None:
+            import torch
+            from .featurizer import FilterbankFeatures
+            fz = FilterbankFeatures(device=torch.device(self.device).index or 0, **self._kw)
+            self._tls.fz = fz
+        return fz
+
+    def assemble(self, indices, n_pad=None):
+        """-> (x cuda [T_max, n_pad, 256] fp32, lens cuda int32 [n_pad], lens_host [n])."""
+        import torch
+        idx = np.asarray(indices, np.int64)
+        n = len(idx)
+        n_pad = n_pad or pad_batch(n)
+        bl = self.lengths[idx].astype(np.int32)
+        wl = self.wav_lengths[idx].astype(np.int32)
+        off = torch.from_numpy(self.offsets[idx]).to(self.device)
+        x, lens = self._featurizer().featurize(self.store, torch.from_numpy(wl).to(self.device), wl, n=n, n_pad=n_pad,
+                                               T_out=max(int(bl.max()), 1), offsets=off)
+        return x, lens, bl
+
+
 class ServerSUT:
     """Server scenario SUT (reference ServerSUT, csrc/torch_sut.cpp:238-571, with
     PipelineState continuous batching, metadata.cpp:97-194).  MI355X form: one worker thread

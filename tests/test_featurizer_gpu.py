@@ -128,3 +128,45 @@ def test_wav_to_tokens_matches_oracle(fz, oracle):
     np.testing.assert_array_equal(rl.cpu().numpy(), rlo)
     np.testing.assert_array_equal(res.cpu().numpy(), ro)
     assert rlo.sum() > 0
+
+
+def test_server_sut_over_wav_qsl():
+    """WAV=true Server path: GpuWavQSL featurizes each dynamic batch on the worker's stream;
+    every answer equals one Offline batch of the same audio (rows are independent in both the
+    featurizer and the engine)."""
+    import time
+    from rnnt_amd import weights
+    from rnnt_amd.engine import Engine
+    from rnnt_amd.sut import GpuWavQSL, QuerySample, ServerSUT
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    pm, _ = weights.build_model()
+    frames = np.minimum(synthetic.devclean_lengths(24, seed=61), 120)
+    wavs = synthetic.make_wavs(synthetic.wav_lengths_for_frames(frames, seed=61), seed=61, device="cuda")
+    qsl = GpuWavQSL(wavs)
+    assert qsl.lengths.tolist() == frames.tolist()
+    engines = [Engine(pm, device=0, max_batch=64, max_frames=128) for _ in range(2)]
+    try:
+        srv = ServerSUT(engines, qsl, max_batch=8)
+        srv.start()
+        samples = [QuerySample(id=i, index=i) for i in range(len(frames))]
+        for k in range(0, len(samples), 5):
+            srv.issue_query(samples[k:k + 5])
+            time.sleep(0.002)
+        deadline = time.time() + 60
+        while len(srv.latency) < len(samples) and time.time() < deadline:
+            time.sleep(0.01)
+        srv.stop()
+        assert not srv.errors and len(srv.responses) == len(samples)
+        x, lens, bl = qsl.assemble(list(range(len(frames))))
+        n = len(frames)
+        res = torch.empty((n, engines[0].max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(n, dtype=torch.int32, device="cuda")
+        engines[0].infer(x, lens, bl, res, rl, n=n)
+        res, rl = res.cpu().numpy(), rl.cpu().numpy()
+        assert rl.sum() > 0
+        for i in range(n):
+            np.testing.assert_array_equal(srv.responses[i], res[i, : rl[i]])
+    finally:
+        for e in engines:
+            e.close()
