@@ -209,10 +209,60 @@ def cpu_baseline(pm, lens, n_sample, seed):
                 cores=oracle.lib().oracle_num_threads(), frames=int(sl.sum()))
 
 
+def wer_vs_fp32(engine, ckpt, pm, cb, gpu_res, gpu_rl):
+    """BASELINE metric's second half ("WER vs fp32 ref") on the cpu_baseline sample, with its
+    decomposition.  Hypotheses: the GPU's int8-encoder + bf16-decode transcripts (the timed path).
+    References: the fp32 model -- fp32 encoder on the GPU (bit-exact with the fp32 restatement,
+    tests/test_f32_gpu.py) + the fp32 greedy decode of the CPU restatement (no fp32 decode
+    kernels on the GPU).  Decomposition: the same int8 encoder output decoded in bf16 (GPU) and
+    in fp32 (CPU) isolates the decoder's precision; the int8-vs-fp32 encoder outputs' relative
+    error on the first frames vs over whole utterances shows how the random-init recurrence
+    amplifies quantisation noise (a trained model's would not)."""
+    from oracle import oracle
+    from rnnt_amd import accuracy
+    sd = weights.migrate_state_dict(ckpt)
+    engine.load_f32_encoder([weights.enc_layer_params(sd, l) for l in range(5)])
+    n, sl, x = cb["n"], cb["sl"], cb["x"]
+    T, n_pad = x.shape[0], x.shape[1]
+    xd, ld = torch.from_numpy(x).cuda(), torch.from_numpy(cb["lens"]).cuda()
+    f32 = torch.empty(((T + 1) // 2, n_pad, 1024), dtype=torch.float32, device="cuda")
+    fi8 = torch.empty_like(f32)
+    engine.encode_f32(xd, ld, n, f32)
+    engine.encode(xd, ld, sl, n=n, f_out=fi8)
+    torch.cuda.synchronize()
+    f32, fi8 = f32.cpu().numpy()[:, :n], fi8.cpu().numpy()[:, :n]
+    pm32 = weights.prepare_model(ckpt, pm.amax, bf16=False)
+    fl = (sl + 1) // 2
+    r32, l32, _ = oracle.greedy_decode(pm32, np.ascontiguousarray(f32), fl, max_res=(500 // 2) * 30)
+    r8, l8, _ = oracle.greedy_decode(pm32, np.ascontiguousarray(fi8), fl, max_res=(500 // 2) * 30)
+
+    def sens(ra, la, rb, lb):
+        hyp = [accuracy.seq_to_sen(ra[i], la[i]) for i in range(n)]
+        ref = [accuracy.seq_to_sen(rb[i], lb[i]) for i in range(n)]
+        wer, errs, words = accuracy.word_error_rate(hyp, ref)
+        tok = sum(accuracy.edit_distance(list(ra[i, :la[i]]), list(rb[i, :lb[i]])) for i in range(n))
+        return {"wer": round(wer, 5), "word_errors": errs, "words": words,
+                "token_error_rate": round(tok / max(1, int(lb.sum())), 5)}
+
+    def rel(a, b):
+        return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+    first = rel(fi8[:2], f32[:2])
+    whole = rel(np.concatenate([fi8[: fl[i], i] for i in range(n)]), np.concatenate([f32[: fl[i], i] for i in range(n)]))
+    return {"utterances": n,
+            "int8_bf16_vs_fp32": sens(gpu_res, gpu_rl, r32, l32),
+            "bf16_decode_vs_fp32_decode_same_int8_encoder": sens(gpu_res, gpu_rl, r8, l8),
+            "encoder_rel_l2_int8_vs_fp32": {"first_2_frames": round(first, 5), "whole_utterances": round(whole, 5)},
+            "hypothesis": "int8 encoder + bf16 prediction/joint (GPU, the timed path)",
+            "reference": "fp32 encoder (GPU f32 path) + fp32 greedy decode (CPU restatement)",
+            "note": "synthetic random-init model (chaotic recurrence) and features: a quantisation-sensitivity "
+                    "figure, not LibriSpeech WER (no checkpoint / dataset offline)"}
+
+
 def main():
     args = parse()
     rank, local, world = dist_setup()
-    pm, _ = weights.build_model()
+    pm, ckpt = weights.build_model()
     qsl = (build_wav_qsl if args.wav else build_qsl)(args.qsl, seed=4 + 1000 * rank)
     lens = qsl["lens"]
     engines = [Engine(pm, device=local, max_batch=min(args.batch, args.query), max_frames=500)
@@ -312,6 +362,7 @@ def main():
                                "sample": f"{cb['n']} utterances ({cb['frames']} frames) drawn from the same QSL, "
                                          f"int8 encoder + greedy decode, {cb['seconds']:.1f} s"}
         out["parity_spot_check"] = {"utterances": cb["n"], "tokens_identical": same}
+        out["wer_vs_fp32"] = wer_vs_fp32(engine, ckpt, pm, cb, res.cpu().numpy(), rl.cpu().numpy())
     if rank == 0:
         print(json.dumps(out), flush=True)
     for e in engines:
