@@ -67,3 +67,18 @@ def test_eval_acc_end_to_end(tmp_path):
     A.write_accuracy_log({k: np.array(v, np.int32) for k, v in hyps.items()}, lp)
     wer, errors, words = A.eval_acc(str(lp), str(mp))
     assert (errors, words) == (1, 4) and wer == 0.25
+
+
+def test_eval_accuracy_cli(tmp_path):
+    import subprocess
+    import sys
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mp, lp = tmp_path / "m.json", tmp_path / "log.json"
+    mp.write_text(json.dumps([{"transcript": "ab c", "original_duration": 2.0}]))
+    A.write_accuracy_log({0: np.array([1, 2, 0, 3], np.int32)}, lp)
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "eval_accuracy.py"), "--log_path", str(lp),
+                          "--manifest_path", str(mp), "--hypotheses", str(tmp_path / "h.log")],
+                         capture_output=True, text=True, check=True).stdout
+    assert "Word Error Rate: 0.0%" in out
+    assert (tmp_path / "h.log").read_text() == "0::ab c\n"
