@@ -192,3 +192,73 @@ def build_model(seed=None, amax=None, calib_n=2, calib_T=120, bf16=True, recipe=
         feats = make_features(calib_T, calib_n, seed=seed ^ 0xCA1B, lens=lens)
         amax = calibrate_amax(migrate_state_dict(ckpt), feats, lens)
     return prepare_model(ckpt, amax, bf16=bf16), ckpt
+
+
+# ---- packed model file (the export that replaces the reference's calibrated state dict +
+# TorchScript jit files, models/main.py:21-58 / utils.py:97-110): the PreparedModel arrays in an
+# .npz (no pickles; load with allow_pickle=False), plus a JSON header.
+PACKED_FORMAT = "rnnt-mi355x-prepared/1"
+_LISTS = ("enc_w", "enc_bq", "pred_wih", "pred_whh", "pred_bih", "pred_bhh")
+_ARRAYS = ("enc_rb", "enc_in_s", "enc_out_s", "amax", "embed", "w1t", "w1p", "bt", "bp", "w2", "b2")
+
+
+def prepared_digest(pm):
+    import hashlib
+    h = hashlib.sha256()
+    for k in _LISTS:
+        for a in getattr(pm, k):
+            h.update(np.ascontiguousarray(a).tobytes())
+    for k in _ARRAYS:
+        h.update(np.ascontiguousarray(getattr(pm, k)).tobytes())
+    return h.hexdigest()
+
+
+def save_prepared(pm, path, extra=None):
+    import json
+    meta = {"format": PACKED_FORMAT, "bf16": bool(pm.bf16), "sha256": prepared_digest(pm)}
+    meta.update(extra or {})
+    arrs = {"meta": np.frombuffer(json.dumps(meta).encode(), np.uint8)}
+    for k in _LISTS:
+        for i, a in enumerate(getattr(pm, k)):
+            arrs[f"{k}_{i}"] = np.ascontiguousarray(a)
+    for k in _ARRAYS:
+        arrs[k] = np.ascontiguousarray(getattr(pm, k))
+    with open(path, "wb") as f:
+        np.savez(f, **arrs)
+    return meta
+
+
+def load_prepared(path):
+    """-> (PreparedModel, header); verifies the format tag and the content digest."""
+    import json
+    with np.load(path, allow_pickle=False) as z:
+        meta = json.loads(bytes(z["meta"]).decode())
+        if meta.get("format") != PACKED_FORMAT:
+            raise ValueError(f"{path}: not a {PACKED_FORMAT} file")
+        pm = PreparedModel(bf16=bool(meta["bf16"]))
+        for k in _LISTS:
+            n = sum(1 for key in z.files if key.rsplit("_", 1)[0] == k and key.rsplit("_", 1)[1].isdigit())
+            setattr(pm, k, [z[f"{k}_{i}"] for i in range(n)])
+        for k in _ARRAYS:
+            setattr(pm, k, z[k])
+    if prepared_digest(pm) != meta["sha256"]:
+        raise ValueError(f"{path}: content digest mismatch")
+    return pm, meta
+
+
+def load_checkpoint(path):
+    """A state dict of tensors (original or migrated keys) from .pt (torch.load weights_only=True),
+    .safetensors or .npz (allow_pickle=False) -> {key: float32 ndarray}."""
+    if path.endswith(".safetensors"):
+        from safetensors.numpy import load_file
+        sd = load_file(path)
+    elif path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            sd = {k: z[k] for k in z.files}
+    else:
+        import torch
+        obj = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(obj, dict) and "state_dict" in obj and isinstance(obj["state_dict"], dict):
+            obj = obj["state_dict"]
+        sd = {k: v.detach().float().numpy() for k, v in obj.items() if hasattr(v, "detach")}
+    return {k: np.asarray(v, np.float32) for k, v in sd.items()}
