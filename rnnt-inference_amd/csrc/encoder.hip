@@ -240,7 +240,13 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   const float4* tab = (const float4*)(smem + TAB_OFF);
   float4 bq[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) bq[i] = *(const float4*)(a.bq + m0 + wm * 64 + i * 16 + q * 4);
+  for (int i = 0; i < 4; ++i) {
+#ifdef RNNT_DEV_EPI_NOBQ  // development ablation: no bias load
+    bq[i] = float4{64.0f, 64.0f, 64.0f, 64.0f};
+#else
+    bq[i] = *(const float4*)(a.bq + m0 + wm * 64 + i * 16 + q * 4);
+#endif
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int n = nb + 16 * j;
@@ -258,6 +264,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       hq |= (uint32_t)(uint8_t)q8(hh * ins) << (8 * i);
       yq |= (uint32_t)(uint8_t)q8(hh * outs) << (8 * i);
     }
+#ifdef RNNT_DEV_EPI_NOSTORE  // development ablation: results kept live, nothing stored
+    asm volatile("" ::"v"(cw[0]), "v"(cw[1]), "v"(hq), "v"(yq), "v"(hv[0]));
+    continue;
+#endif
     *(uint2*)(a.c + (size_t)n * H + u0) = uint2{cw[0], cw[1]};
     *(uint32_t*)(a.h_out + (size_t)n * H + u0) = hq;
     if (a.mode == ENC_OUT_I8) {
@@ -282,27 +292,39 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 // workgroups resident on an XCD share 4 weight tiles and ~8 activation tiles through its L2
 // (weights fetched from HBM/MALL 2x, activations 4x per tick, instead of 1x / 8x).
 // 2 waves per SIMD either way: one 8-wave workgroup per CU (ENC_WN 2) or two 4-wave ones (1)
-__global__ void __launch_bounds__(NWAVE * 64, ENC_WN == 2 ? 1 : 2) lstm_i8_tick_kernel(EncTickArgs args) {
+#ifndef RNNT_PERSIST
+#define RNNT_PERSIST 0
+#endif
+constexpr int WG_PER_CU = ENC_WN == 2 ? 1 : 2;
+constexpr int SLOTS_PER_XCD = 32 * WG_PER_CU;  // resident workgroups per XCD (32 CUs)
+__global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(EncTickArgs args) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   const int xcd = blockIdx.x & 7, gg = xcd & 3, bg = xcd >> 2;
-  int k = blockIdx.x >> 3, jsel = -1, mt = 0, nt = 0;
-  for (int j = 0; j < args.njobs; ++j) {
-    const int nbt = args.nbt[j], h0 = (nbt + 1) >> 1;
-    const int cnt = 4 * (bg ? nbt - h0 : h0);
-    if (k < cnt) {
-      jsel = j;
-      mt = gg * 4 + (k & 3);
-      nt = (bg ? h0 : 0) + (k >> 2);
-      break;
-    }
-    k -= cnt;
-  }
-  if (jsel < 0) return;
   if (threadIdx.x < 128) ((float4*)(smem + TAB_OFF))[threadIdx.x] = g_act_tab[threadIdx.x];  // read after the
   // first stage barrier of the main loop (lgkmcnt(0) + s_barrier)
-  // wave-uniform runtime index into the kernarg segment: the job's fields stay scalar loads
-  lstm_i8_step(args.job[__builtin_amdgcn_readfirstlane(jsel)], __builtin_amdgcn_readfirstlane(mt),
-               __builtin_amdgcn_readfirstlane(nt), smem);
+  // RNNT_PERSIST: workgroup (xcd, slot) takes the XCD's tiles slot, slot + SLOTS_PER_XCD, ... in
+  // the order one-tile-per-workgroup rounds would run them (a layer-step 4 % shorter alone, but
+  // the resident grid then starves the other streams' decode kernels: off by default)
+  const int stride = RNNT_PERSIST ? (int)(gridDim.x >> 3) : 1 << 30;
+  for (int k0 = blockIdx.x >> 3;; k0 += stride) {
+    int k = k0, jsel = -1, mt = 0, nt = 0;
+    for (int j = 0; j < args.njobs; ++j) {
+      const int nbt = args.nbt[j], h0 = (nbt + 1) >> 1;
+      const int cnt = 4 * (bg ? nbt - h0 : h0);
+      if (k < cnt) {
+        jsel = j;
+        mt = gg * 4 + (k & 3);
+        nt = (bg ? h0 : 0) + (k >> 2);
+        break;
+      }
+      k -= cnt;
+    }
+    if (jsel < 0) return;
+    if (k0 != (int)(blockIdx.x >> 3)) __syncthreads();  // the previous tile's epilogue LDS reads are done
+    // wave-uniform runtime index into the kernarg segment: the job's fields stay scalar loads
+    lstm_i8_step(args.job[__builtin_amdgcn_readfirstlane(jsel)], __builtin_amdgcn_readfirstlane(mt),
+                 __builtin_amdgcn_readfirstlane(nt), smem);
+  }
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -326,7 +348,8 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
   int per_xcd = 0;  // the batch-half-0 XCDs carry the larger half
   for (int j = 0; j < a.njobs; ++j) per_xcd += 4 * ((a.nbt[j] + 1) >> 1);
   if (per_xcd <= 0) return 0;
-  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(8 * per_xcd), dim3(NWAVE * 64), SMEM_BYTES, st, a);
+  const int grid = 8 * (RNNT_PERSIST && per_xcd > SLOTS_PER_XCD ? SLOTS_PER_XCD : per_xcd);
+  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(grid), dim3(NWAVE * 64), SMEM_BYTES, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -17,6 +17,10 @@ build() {
 for v in "$@"; do
   case $v in
     base) build base ;;
+    persist) build persist -DRNNT_PERSIST=1 ;;
+    epi_nobq) build epi_nobq -DRNNT_DEV_EPI_NOBQ ;;
+    epi_nostore) build epi_nostore -DRNNT_DEV_EPI_NOSTORE ;;
+    epi_nostore_notab) build epi_nostore_notab -DRNNT_DEV_EPI_NOSTORE -DRNNT_DEV_NO_TAB ;;
     fz_noload) build fz_noload -DRNNT_DEV_FZ_NO_LOAD ;;
     fz_nofft) build fz_nofft -DRNNT_DEV_FZ_NO_FFT ;;
     fz_nomel) build fz_nomel -DRNNT_DEV_FZ_NO_MEL ;;
