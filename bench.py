@@ -43,9 +43,14 @@ def parse():
     ap.add_argument("--qsl", type=int, default=2513, help="QSL utterances per GPU (mlperf.conf:13)")
     ap.add_argument("--query", type=int, default=24576, help="samples per Offline query per GPU (mlperf.conf:63)")
     ap.add_argument("--batch", type=int, default=8192, help="utterances per encode+decode call")
+    ap.add_argument("--batch-sizes", default=None,
+                    help="comma-separated batch sizes over the sorted query (the last repeats), e.g. 8192,8192,4096,2048")
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches in flight per GPU: one engine + HIP stream + host thread each, so one "
                          "batch's latency-bound greedy decode overlaps the next batch's encoder")
+    ap.add_argument("--decode-priority", type=int, default=0,
+                    help="run each engine's decode on a separate stream of this priority (torch: lower = higher; "
+                         "0 = decode on the encode stream)")
     ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wav", action="store_true",
@@ -103,15 +108,27 @@ def build_wav_qsl(count, seed):
     return dict(lens=lens, wav_lens=wav_lens, wav_offs=offs, store=store)
 
 
-def make_wav_batches(qsl, query, batch):
+def batch_bounds(n, batch, sizes=None):
+    """Start/end of each batch over the sorted query: --batch-sizes (cycled; the last entry
+    repeats) or uniform --batch."""
+    out, i, k = [], 0, 0
+    while i < n:
+        b = sizes[min(k, len(sizes) - 1)] if sizes else batch
+        out.append((i, min(n, i + b)))
+        i += b
+        k += 1
+    return out
+
+
+def make_wav_batches(qsl, query, batch, sizes=None):
     """As make_batches, but each batch keeps only its samples' offsets into the ragged audio;
     its feature buffer [T_max, n_pad, 256] is filled by the featurizer inside every step."""
     count = len(qsl["lens"])
     ids = np.arange(query) % count
     ids = ids[np.argsort(-qsl["lens"][ids], kind="stable")]
     out = []
-    for i in range(0, len(ids), batch):
-        idx = ids[i:i + batch]
+    for i, e in batch_bounds(len(ids), batch, sizes):
+        idx = ids[i:e]
         n = len(idx)
         n_pad = pad_batch(n)
         bl = qsl["lens"][idx].astype(np.int32)
@@ -125,7 +142,7 @@ def make_wav_batches(qsl, query, batch):
     return out
 
 
-def make_batches(qsl, query, batch):
+def make_batches(qsl, query, batch, sizes=None):
     """The Offline query (sample i -> QSL index i % count, as LoadGen repeats the QSL),
     sorted longest-first and split into batches; each batch assembled in HBM as
     [T_max, n_pad, 256] fp32, zero padded (AssembleSamples, rnnt_qsl.cpp:150-188)."""
@@ -133,8 +150,8 @@ def make_batches(qsl, query, batch):
     ids = np.arange(query) % count
     ids = ids[np.argsort(-qsl["lens"][ids], kind="stable")]
     out = []
-    for i in range(0, len(ids), batch):
-        idx = ids[i:i + batch]
+    for i, e in batch_bounds(len(ids), batch, sizes):
+        idx = ids[i:e]
         bl = qsl["lens"][idx].astype(np.int32)
         n = len(idx)
         n_pad = pad_batch(n)
@@ -152,7 +169,7 @@ def make_batches(qsl, query, batch):
     return out
 
 
-def run_step(engines, streams, batches, featurizers=None, store=None):
+def run_step(engines, streams, batches, featurizers=None, store=None, dec_streams=None):
     """One Offline query.  Batch i runs on engine i % inflight, each engine with its own HIP
     stream and host thread (ctypes releases the GIL).  Encoders take turns (a lock held until
     the encode has finished on the GPU), so each batch's latency-bound greedy decode overlaps
@@ -168,10 +185,13 @@ def run_step(engines, streams, batches, featurizers=None, store=None):
                 featurizers[j].featurize(store, b["wav_lens"], b["wav_lens_host"], n=b["n"], n_pad=b["n_pad"],
                                          T_out=b["T"], offsets=b["wav_off"], out=b["x"], feat_lens=b["lens"],
                                          stream=streams[j])
+            ds = streams[j] if dec_streams is None else dec_streams[j]
+            if ds is not streams[j]:
+                streams[j].wait_stream(ds)  # the engine's previous decode has consumed its state
             with enc_lock:
                 engines[j].encode(b["x"], b["lens"], b["lens_host"], n=b["n"], stream=streams[j])
                 streams[j].synchronize()
-            engines[j].decode(b["res"], b["rl"], stream=streams[j])
+            engines[j].decode(b["res"], b["rl"], stream=ds)
 
     if k == 1:
         worker(0)
@@ -181,7 +201,7 @@ def run_step(engines, streams, batches, featurizers=None, store=None):
             t.start()
         for t in ths:
             t.join()
-    for s in streams:
+    for s in streams + (dec_streams or []):
         s.synchronize()
     # host gather of the responses: lengths, then each batch's used token columns
     lens = [b["rl"].cpu() for b in batches]
@@ -265,11 +285,13 @@ def main():
     pm, ckpt = weights.build_model()
     qsl = (build_wav_qsl if args.wav else build_qsl)(args.qsl, seed=4 + 1000 * rank)
     lens = qsl["lens"]
-    engines = [Engine(pm, device=local, max_batch=min(args.batch, args.query), max_frames=500)
+    sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None
+    engines = [Engine(pm, device=local, max_batch=min(max(sizes or [args.batch]), args.query), max_frames=500)
                for _ in range(args.inflight)]
     engine = engines[0]
     streams = [torch.cuda.Stream() for _ in engines]
-    batches = (make_wav_batches if args.wav else make_batches)(qsl, args.query, args.batch)
+    dec_streams = [torch.cuda.Stream(priority=args.decode_priority) for _ in engines] if args.decode_priority else None
+    batches = (make_wav_batches if args.wav else make_batches)(qsl, args.query, args.batch, sizes)
     fzs, store = None, None
     if args.wav:
         from rnnt_amd.featurizer import FilterbankFeatures
@@ -281,7 +303,7 @@ def main():
         b["rl"] = torch.empty(b["n"], dtype=torch.int32, device="cuda")
 
     for _ in range(args.warmup):
-        run_step(engines, streams, batches, fzs, store)
+        run_step(engines, streams, batches, fzs, store, dec_streams)
     torch.cuda.synchronize()
     for e in engines:  # HIP events around every encode / joint_trans / greedy call, on its stream
         e.set_profiling(True)
@@ -289,7 +311,7 @@ def main():
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lens_out, _ = run_step(engines, streams, batches, fzs, store)
+        lens_out, _ = run_step(engines, streams, batches, fzs, store, dec_streams)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
