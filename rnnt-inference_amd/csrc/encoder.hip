@@ -50,6 +50,15 @@ constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-
 #ifndef RNNT_INTERLEAVE
 #define RNNT_INTERLEAVE 0
 #endif
+#ifndef RNNT_STAGGER
+#define RNNT_STAGGER 1
+#endif
+#ifndef RNNT_PRIO_MODE  // 0: MFMA clusters at priority 1; 1: + late waves at 1 throughout; 2: static, late waves only
+#define RNNT_PRIO_MODE 0
+#endif
+#ifndef RNNT_STAGGER_AT
+#define RNNT_STAGGER_AT 2  // MFMA group (of 4) before which the late waves issue their pieces
+#endif
 constexpr int NSTAGE = RNNT_NSTAGE;          // LDS ring depth: NSTAGE-1 stages in flight
 constexpr int A_BYTES = BM * BK;             // 16 KiB
 constexpr int STAGE_BYTES = (BM + BN) * BK;  // 32 / 24 KiB
@@ -175,6 +184,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
+#if RNNT_PRIO_MODE != 0
+  if (RNNT_STAGGER && wn == 1) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int ks = 0; ks < nK; ++ks) {
     // LDS-DMA this wave may leave in flight: the stages issued after ks (min(NSTAGE - 2,
     // nK - 1 - ks)) and, once issued (step nK-NSTAGE+1, into stage nK-NSTAGE's buffer), the
@@ -182,8 +194,13 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     const int later = nK - 1 - ks < NSTAGE - 2 ? nK - 1 - ks : NSTAGE - 2;
     stage_barrier_n(later * GLDS_PER_STAGE + (ks > nK - NSTAGE + 1 ? C_GLDS : 0));
 #if !RNNT_INTERLEAVE
-    if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
-    else if (ks + NSTAGE - 1 == nK) issue_c();
+    // RNNT_STAGGER: waves 4-7 (each the SIMD partner of wave w-4) issue their pieces after half
+    // of their MFMAs, so one wave of a SIMD issues LDS-DMA while its partner runs MFMAs
+    const bool late = RNNT_STAGGER && wn == 1;
+    if (!late) {
+      if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
+      else if (ks + NSTAGE - 1 == nK) issue_c();
+    }
 #else
     const bool next = ks + NSTAGE - 1 < nK;
     if (ks + NSTAGE - 1 == nK) issue_c();
@@ -207,7 +224,11 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #pragma unroll
     for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(fra[i]), "v"(frb[i]), "v"(frb[i + 4]));
 #else
+#if RNNT_PRIO_MODE == 0
     __builtin_amdgcn_s_setprio(1);  // MFMA cluster at raised priority (guide T5)
+#elif RNNT_PRIO_MODE == 1
+    if (!late) __builtin_amdgcn_s_setprio(1);  // late waves hold priority 1 for the whole loop
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #if RNNT_INTERLEAVE
@@ -217,15 +238,32 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
         if (next) issue_piece(ks + NSTAGE - 1, pj);
       __builtin_amdgcn_sched_barrier(0);
 #endif
+#if !RNNT_INTERLEAVE
+      if (RNNT_STAGGER && i == RNNT_STAGGER_AT) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (late) {
+          if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
+          else if (ks + NSTAGE - 1 == nK) issue_c();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#endif
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
 #if RNNT_INTERLEAVE
       __builtin_amdgcn_sched_barrier(0);
 #endif
     }
+#if RNNT_PRIO_MODE == 0
     __builtin_amdgcn_s_setprio(0);
+#elif RNNT_PRIO_MODE == 1
+    if (!late) __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
   }
+#if RNNT_PRIO_MODE != 0
+  __builtin_amdgcn_s_setprio(0);
+#endif
   stage_barrier<0>();  // the cell-state DMA has landed for every wave
 #ifdef RNNT_DEV_NO_EPI  // development ablation: main loop only
 #pragma unroll

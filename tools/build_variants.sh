@@ -17,6 +17,11 @@ build() {
 for v in "$@"; do
   case $v in
     base) build base ;;
+    nostagger) build nostagger -DRNNT_STAGGER=0 ;;
+    stagger1) build stagger1 -DRNNT_STAGGER=1 -DRNNT_STAGGER_AT=1 ;;
+    stagger_p1) build stagger_p1 -DRNNT_STAGGER=1 -DRNNT_PRIO_MODE=1 ;;
+    stagger_p2) build stagger_p2 -DRNNT_STAGGER=1 -DRNNT_PRIO_MODE=2 ;;
+    stagger3) build stagger3 -DRNNT_STAGGER=1 -DRNNT_STAGGER_AT=3 ;;
     persist) build persist -DRNNT_PERSIST=1 ;;
     epi_nobq) build epi_nobq -DRNNT_DEV_EPI_NOBQ ;;
     epi_nostore) build epi_nostore -DRNNT_DEV_EPI_NOSTORE ;;
