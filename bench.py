@@ -29,7 +29,7 @@ import torch  # noqa: E402
 
 from rnnt_amd import synthetic, weights  # noqa: E402
 from rnnt_amd.config import encoder_frames, encoder_ops  # noqa: E402
-from rnnt_amd.engine import Engine, pad_batch  # noqa: E402
+from rnnt_amd.engine import Engine, PartitionedStream, cu_mask_words, pad_batch  # noqa: E402
 
 METRIC = "MLPerf Offline utterances/sec at 1/2/4/8 MI355X; WER vs fp32 ref"
 INT8_DENSE_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 MFMA = 2x the ~2.5 PF dense bf16 rate
@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--decode-priority", type=int, default=0,
                     help="run each engine's decode on a separate stream of this priority (torch: lower = higher; "
                          "0 = decode on the encode stream)")
+    ap.add_argument("--enc-reserve", type=int, default=0,
+                    help="CUs per XCD kept off the encoder streams (CU-masked HIP streams, rnnt_stream_create); "
+                         "each engine's decode then runs on its own unrestricted stream and always finds free CUs")
     ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wav", action="store_true",
@@ -289,8 +292,17 @@ def main():
     engines = [Engine(pm, device=local, max_batch=min(max(sizes or [args.batch]), args.query), max_frames=500)
                for _ in range(args.inflight)]
     engine = engines[0]
-    streams = [torch.cuda.Stream() for _ in engines]
-    dec_streams = [torch.cuda.Stream(priority=args.decode_priority) for _ in engines] if args.decode_priority else None
+    owned = []
+    if args.enc_reserve:
+        owned = [PartitionedStream(local, cu_mask_words(args.enc_reserve)) for _ in engines]
+        owned += [PartitionedStream(local) for _ in engines]
+        streams = [p.stream for p in owned[: len(engines)]]
+        dec_streams = [p.stream for p in owned[len(engines):]]
+    else:
+        streams = [torch.cuda.Stream() for _ in engines]
+        dec_streams = ([torch.cuda.Stream(priority=args.decode_priority) for _ in engines] if args.decode_priority
+                       else None)
+    iso_stream = torch.cuda.Stream()
     batches = (make_wav_batches if args.wav else make_batches)(qsl, args.query, args.batch, sizes)
     fzs, store = None, None
     if args.wav:
@@ -320,7 +332,7 @@ def main():
     st = {k: sum(x[k] for x in sts) for k in sts[0]}
     # isolated pass (untimed): the same query once more, batches back to back on one engine,
     # so the encoder's event time is not shared with an overlapping decode
-    run_step([engine], [streams[0]], batches)
+    run_step([engine], [iso_stream], batches)
     iso = engine.stats(reset=True)
     for e in engines:
         e.set_profiling(False)
@@ -362,6 +374,7 @@ def main():
         "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
                    "qsl_per_gpu": args.qsl, "query_samples_per_gpu": args.query, "batch_size": args.batch,
                    "batches_in_flight": args.inflight,
+                   "encoder_cu_reserve_per_xcd": args.enc_reserve,
                    "input": ("16 kHz audio: GPU featurizer (FilterbankFeatures.forward) in the timed region" if args.wav
                              else "log-mel features resident in HBM"),
                    "encoder": "int8 (lstm_amx_int8)",
@@ -389,6 +402,8 @@ def main():
         print(json.dumps(out), flush=True)
     for e in engines:
         e.close()
+    for p in owned:
+        p.close()
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

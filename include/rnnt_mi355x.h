@@ -70,6 +70,14 @@ typedef struct {
 int rnnt_abi_version(void);
 const char* rnnt_last_error(void);
 
+/* A HIP stream whose kernels run only on the CUs set in cu_mask (mask_words 32-bit words;
+ * bit b = CU slot b/8 of XCD b%8 on MI355X; every XCD needs at least one bit), or a plain
+ * non-blocking stream when cu_mask is NULL.  bench.py / the SUT keep the encoder off a few CUs
+ * per XCD so the latency-bound greedy decode of the previous batch always finds free CUs.
+ * Not a reference interface (the reference pins OpenMP teams to cores, torch_sut.cpp:143-149). */
+int rnnt_stream_create(int device, const uint32_t* cu_mask, int mask_words, void** out);
+int rnnt_stream_destroy(void* stream);
+
 /* Packs the model into the engine's device layouts on `device` and sizes the workspace. */
 int rnnt_engine_create(const rnnt_model_desc* model, int device, const rnnt_opts* opts, rnnt_engine** out);
 void rnnt_engine_destroy(rnnt_engine* e);

@@ -17,6 +17,7 @@
 #include "decoder.hpp"
 #include "decoder_ops.hpp"
 #include "encoder.hpp"
+#include <hip/hip_ext.h>
 #include "encoder_f32.hpp"
 #include "rnnt_device.hpp"
 
@@ -100,6 +101,31 @@ static int upload(rnnt_engine* e, T** p, const std::vector<T>& host) {
 
 extern "C" int rnnt_abi_version(void) { return RNNT_ABI_VERSION; }
 extern "C" const char* rnnt_last_error(void) { return g_err.c_str(); }
+
+// CU-partitioned streams (MI355X scheduling, not a reference interface): bit b of the mask is
+// CU slot b/8 of XCD b%8 (probe: tools/probe/probe_cumask.hip); every XCD must keep >= 1 bit
+// (an XCD with none is given all of its CUs by the runtime).
+extern "C" int rnnt_stream_create(int device, const uint32_t* cu_mask, int mask_words, void** out) {
+  if (!out || (cu_mask && (mask_words <= 0 || mask_words > 16))) return fail(RNNT_EINVAL, "rnnt_stream_create: bad mask");
+  HIPCHK(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  if (cu_mask) {
+    uint32_t per_xcd[8] = {0};
+    for (int b = 0; b < 32 * mask_words; ++b)
+      if (cu_mask[b >> 5] >> (b & 31) & 1u) per_xcd[b & 7]++;
+    for (int x = 0; x < 8; ++x)
+      if (!per_xcd[x]) return fail(RNNT_EINVAL, "rnnt_stream_create: every XCD needs at least one CU");
+    HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask_words, cu_mask));
+  } else {
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  *out = (void*)s;
+  return RNNT_OK;
+}
+extern "C" int rnnt_stream_destroy(void* stream) {
+  HIPCHK(hipStreamDestroy((hipStream_t)stream));
+  return RNNT_OK;
+}
 
 // ---- packing (natural layouts -> device layouts; see DESIGN.md "Data layout in HBM")
 static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {

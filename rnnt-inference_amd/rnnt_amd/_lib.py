@@ -55,6 +55,8 @@ _SIGS = {
     "rnnt_engine_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "rnnt_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(RnntStats), C.c_int]),
     "rnnt_abi_version": (C.c_int, []),
+    "rnnt_stream_create": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "rnnt_stream_destroy": (C.c_int, [C.c_void_p]),
     "rnnt_last_error": (C.c_char_p, []),
     "rnnt_engine_create": (C.c_int, [C.POINTER(RnntModelDesc), C.c_int, C.POINTER(RnntOpts), C.POINTER(C.c_void_p)]),
     "rnnt_engine_destroy": (None, [C.c_void_p]),

@@ -175,3 +175,38 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+
+def cu_mask_words(reserve_per_xcd, reserved=False, n_cu=256):
+    """32-bit mask words over the MI355X's CUs: bit b = CU slot b // 8 of XCD b % 8.
+    reserved=False: every CU except the first `reserve_per_xcd` slots of each XCD (the encoder's
+    share); reserved=True: only those slots."""
+    words = [0] * ((n_cu + 31) // 32)
+    for b in range(n_cu):
+        if (b // 8 < reserve_per_xcd) == reserved:
+            words[b // 32] |= 1 << (b % 32)
+    return words
+
+
+class PartitionedStream:
+    """A HIP stream restricted to a CU set (rnnt_stream_create), usable as a torch stream.
+    cu_mask=None gives a plain non-blocking stream."""
+
+    def __init__(self, device=0, cu_mask=None):
+        import torch
+        lib = _lib.lib()
+        h = C.c_void_p()
+        if cu_mask is None:
+            rc = lib.rnnt_stream_create(device, None, 0, C.byref(h))
+        else:
+            arr = (C.c_uint32 * len(cu_mask))(*cu_mask)
+            rc = lib.rnnt_stream_create(device, C.cast(arr, C.c_void_p), len(cu_mask), C.byref(h))
+        _lib.check(rc, "rnnt_stream_create")
+        self._h = h
+        self.stream = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", device))
+
+    def close(self):
+        if self._h:
+            self.stream.synchronize()
+            _lib.check(_lib.lib().rnnt_stream_destroy(self._h), "rnnt_stream_destroy")
+            self._h = None
