@@ -158,3 +158,14 @@ def infer_i8(pm, feat, lens):
     f_lens = (np.asarray(lens, np.int32) + 1) // 2
     res, res_len, steps = greedy_decode(pm, f, f_lens)
     return res, res_len, f, steps
+
+
+def mfma_bf16_dot(acc, a, b):
+    """acc [N] f32, a/b [N][K] bf16-exact f32 -> [N] f32 under the bf16-MFMA accumulation model."""
+    acc = _c(acc, np.float32)
+    a = _c(a, np.float32)
+    b = _c(b, np.float32)
+    N, K = a.shape
+    out = np.empty(N, np.float32)
+    lib().oracle_mfma_bf16_dot(C.c_int(N), C.c_int(K), _p(acc), _p(a), _p(b), _p(out))
+    return out

@@ -33,6 +33,9 @@ uint16_t oracle_f2h(float x);      /* f32 -> f16 bits, round-half-even */
 float oracle_h2f(uint16_t h);
 uint16_t oracle_f2bf(float x);     /* f32 -> bf16 bits, round-half-even */
 float oracle_bf2f(uint16_t b);
+/* bf16 MFMA dot (v_mfma_f32_16x16x32_bf16 accumulation model, see rnnt_oracle.c):
+ * out[n] = acc[n] (+) a[n][0:K] . b[n][0:K], K a multiple of 8, a/b bf16-exact floats. */
+void oracle_mfma_bf16_dot(int N, int K, const float* acc, const float* a, const float* b, float* out);
 int8_t oracle_q8(float v);         /* clamp(round_half_even(v), -128, 127): quant_modules.py:8-9,118-121 */
 
 /* Elementwise quantisation x_q = q8(x * scale). */

@@ -8,15 +8,16 @@ namespace rnnt {
 
 struct DecWeights {
   const uint16_t* embed;   // bf16 [28][320] natural
-  const uint16_t* wp[2];   // bf16 [1280][640] gate-interleaved rows, chain-permuted k ([W_ih | W_hh])
+  const uint16_t* wp[2];   // bf16 [1280][640] gate-interleaved rows (4u+g), natural k ([W_ih | W_hh])
   const float* bih_p[2];   // fp32 [1280] b_ih, gate-interleaved
   const float* bhh_p[2];   // fp32 [1280] b_hh, gate-interleaved
-  const uint16_t* w1t;     // bf16 [512][1024] chain-permuted k
-  const uint16_t* w1p;     // bf16 [512][320]  chain-permuted k
+  const uint16_t* w1t;     // bf16 [512][1024] natural k
+  const uint16_t* w1p;     // bf16 [512][320]  natural k
   const float* bt;         // [512]
   const float* bp;         // [512]
-  const uint16_t* w2;      // bf16 [32][512] chain-permuted k (rows 29..31 zero)
+  const uint16_t* w2;      // bf16 [32][512] natural k (rows 29..31 zero)
   const float* b2;         // [32] (29..31 zero)
+  const float* xtab;       // [29][1280] layer-0 input half b_ih + emb[g].W_ih^T, gate-interleaved (28 = SOS)
 };
 
 struct DecState {           // per-row greedy state, device arrays [Npad]
@@ -38,9 +39,12 @@ struct DecArgs {
   int N, Npad, max_res, max_iter;
 };
 
-// F = b_t + bf16(f) . W1t^T for every frame t < Tp and row tile holding a row with f_len > t.
-int launch_joint_trans(const DecWeights& w, const uint16_t* fperm, const int32_t* f_lens, float* F, int Tp,
+// F = b_t + bf16(f) . W1t^T for every frame t < Tp and row tile holding a row with f_len > t
+// (fbf: the encoder output as bf16 [Tp][Npad][1024], natural k).
+int launch_joint_trans(const DecWeights& w, const uint16_t* fbf, const int32_t* f_lens, float* F, int Tp,
                        int Npad, hipStream_t st);
+// xtab (device [29][1280] f32) from w.embed / w.wp[0] / w.bih_p[0]; w.xtab is not read.
+int launch_dec_xtab(const DecWeights& w, float* xtab, hipStream_t st);
 // Host-driven lock-step loop; polls the live-row counter (host_flags: 2 pinned words, evs: 2
 // events) one 32-step chunk behind.
 // Returns the number of steps enqueued (>= 0) or -1.

@@ -9,51 +9,40 @@
 //   amx_linear_bf16_accum_relu modeling_rnnt.py:269-275 -> op_joint_hidden_kernel
 //   amx_linear_i16o32          modeling_rnnt.py:280-283 -> op_joint_logits_kernel
 //   greedy_decode_update       modeling_rnnt.py:331-365 -> op_greedy_update_kernel
-// Row tiles are 16 rows; every dot product is a k-ordered fp32 chain on v_mfma_f32_16x16x4_f32.
+// Row tiles are 16 rows; every dot product is a bf16 MFMA chain (v_mfma_f32_16x16x32_bf16,
+// natural k order, from the bias) exactly as in the fused loop.
 #include "decoder_ops.hpp"
 #include "rnnt_device.hpp"
 
 namespace rnnt {
 
-#define MFMA4(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
-
-__device__ __forceinline__ v4f chain8o(const uint4 w, const float* x, v4f acc) {
-  acc = MFMA4(bits2f(w.x << 16), x[0], acc);
-  acc = MFMA4(bits2f(w.x & 0xffff0000u), x[1], acc);
-  acc = MFMA4(bits2f(w.y << 16), x[2], acc);
-  acc = MFMA4(bits2f(w.y & 0xffff0000u), x[3], acc);
-  acc = MFMA4(bits2f(w.z << 16), x[4], acc);
-  acc = MFMA4(bits2f(w.z & 0xffff0000u), x[5], acc);
-  acc = MFMA4(bits2f(w.w << 16), x[6], acc);
-  acc = MFMA4(bits2f(w.w & 0xffff0000u), x[7], acc);
-  return acc;
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ v4f mfma_bf16o(const uint4 a, const uint4 b, const v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, a), __builtin_bit_cast(v8bf, b), c, 0, 0, 0);
 }
-__device__ __forceinline__ v4f chain_blocks(const uint16_t* w, const float* x, int nblk, v4f acc) {
-  for (int b = 0; b < nblk; ++b) {
-    float xv[8];
-    *(float4*)&xv[0] = *(const float4*)(x + 32 * b);
-    *(float4*)&xv[4] = *(const float4*)(x + 32 * b + 4);
-    acc = chain8o(*(const uint4*)(w + 32 * b), xv, acc);
-  }
+// acc + chain over nblk 32-k blocks: w = this lane's A row at k offset 8q, x = its B row (LDS)
+__device__ __forceinline__ v4f chain_blocks(const uint16_t* w, const uint16_t* x, int nblk, v4f acc) {
+  for (int b = 0; b < nblk; ++b) acc = mfma_bf16o(*(const uint4*)(w + 32 * b), *(const uint4*)(x + 32 * b), acc);
   return acc;
 }
 
-constexpr int OXP = 640 + 4;   // LDS pitch of staged [x | h] rows
-constexpr int OFP = 1024 + 4;  // staged f rows
-constexpr int OYP = 512 + 4;   // staged y1 rows
+constexpr int OXP = 640 + 8;   // LDS pitch (bf16) of staged [x | h] rows
+constexpr int OFP = 1024 + 8;  // staged f rows
+constexpr int OGP = 320 + 8;   // staged g rows
+constexpr int OYP = 512 + 8;   // staged y1 rows
 
 // one prediction LSTM layer: gates = (b_ih + x.W_ih) + (b_hh + h.W_hh); c fp32, h bf16.
 // Grid: x = 10 groups of 8 gate tiles (2 per wave), y = 16-row tiles.
 __global__ void __launch_bounds__(256) op_lstm_bf16_kernel(DecWeights w, int layer, const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ h_in, const float* __restrict__ c_in,
                                                            uint16_t* __restrict__ h_out, float* __restrict__ c_out) {
-  __shared__ __attribute__((aligned(16))) float X[16][OXP];
+  __shared__ __attribute__((aligned(16))) uint16_t X[16][OXP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   const int r0 = blockIdx.y * 16;
   for (int i = tid; i < 16 * 640; i += 256) {
     const int m = i / 640, k = i % 640;
     const uint16_t v = k < P ? x[(size_t)(r0 + m) * P + k] : h_in[(size_t)(r0 + m) * P + k - P];
-    X[m][chain_pos(k)] = bf2f(v);
+    X[m][k] = (v & 0x7f80u) ? v : (uint16_t)(v & 0x8000u);  // subnormal bf16 -> 0 (MFMA contract)
   }
   __syncthreads();
   const int gt = blockIdx.x * 8 + wave * 2;
@@ -70,7 +59,7 @@ __global__ void __launch_bounds__(256) op_lstm_bf16_kernel(DecWeights w, int lay
     const float ig = det_sigmoid(g[0]), fg = det_sigmoid(g[1]), gg = det_tanh(g[2]), og = det_sigmoid(g[3]);
     const float cn = fg * c_in[(size_t)row * P + u] + ig * gg;
     c_out[(size_t)row * P + u] = cn;
-    h_out[(size_t)row * P + u] = f2bf(og * det_tanh(cn));
+    h_out[(size_t)row * P + u] = f2bf_ftz(og * det_tanh(cn));
   }
 }
 
@@ -78,17 +67,18 @@ __global__ void __launch_bounds__(256) op_lstm_bf16_kernel(DecWeights w, int lay
 // columns (one 16-column tile per wave), y = 16-row tiles.
 __global__ void __launch_bounds__(256) op_joint_hidden_kernel(DecWeights w, const float* __restrict__ f,
                                                               const uint16_t* __restrict__ g, uint16_t* __restrict__ y1) {
-  __shared__ __attribute__((aligned(16))) float Fx[16][OFP];
-  __shared__ __attribute__((aligned(16))) float Gx[16][P + 4];
+  __shared__ __attribute__((aligned(16))) uint16_t Fx[16][OFP];
+  __shared__ __attribute__((aligned(16))) uint16_t Gx[16][OGP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   const int r0 = blockIdx.y * 16;
   for (int i = tid; i < 16 * H; i += 256) {
     const int m = i / H, k = i % H;
-    Fx[m][chain_pos(k)] = bf_round(f[(size_t)(r0 + m) * H + k]);
+    Fx[m][k] = f2bf_ftz(f[(size_t)(r0 + m) * H + k]);
   }
   for (int i = tid; i < 16 * P; i += 256) {
     const int m = i / P, k = i % P;
-    Gx[m][chain_pos(k)] = bf2f(g[(size_t)(r0 + m) * P + k]);
+    const uint16_t v = g[(size_t)(r0 + m) * P + k];
+    Gx[m][k] = (v & 0x7f80u) ? v : (uint16_t)(v & 0x8000u);
   }
   __syncthreads();
   const int jt = blockIdx.x * 4 + wave;
@@ -98,7 +88,7 @@ __global__ void __launch_bounds__(256) op_joint_hidden_kernel(DecWeights w, cons
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float s = F[r] + G[r];
-    y1[(size_t)(r0 + c) * J + jt * 16 + 4 * q + r] = f2bf(s > 0.0f ? s : 0.0f);
+    y1[(size_t)(r0 + c) * J + jt * 16 + 4 * q + r] = f2bf_ftz(s > 0.0f ? s : 0.0f);
   }
 }
 
@@ -106,13 +96,14 @@ __global__ void __launch_bounds__(256) op_joint_hidden_kernel(DecWeights w, cons
 // joint's contract); columns 29..31 are exact zeros (zero weights and bias).
 __global__ void __launch_bounds__(256) op_joint_logits_kernel(DecWeights w, const uint16_t* __restrict__ y1,
                                                               float* __restrict__ logits) {
-  __shared__ __attribute__((aligned(16))) float X[16][OYP];
+  __shared__ __attribute__((aligned(16))) uint16_t X[16][OYP];
   __shared__ float Lp[4][16][NLAB_PAD + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   const int r0 = blockIdx.x * 16;
   for (int i = tid; i < 16 * J; i += 256) {
     const int m = i / J, k = i % J;
-    X[m][chain_pos(k)] = bf2f(y1[(size_t)(r0 + m) * J + k]);
+    const uint16_t v = y1[(size_t)(r0 + m) * J + k];
+    X[m][k] = (v & 0x7f80u) ? v : (uint16_t)(v & 0x8000u);
   }
   __syncthreads();
   const int lh = wave & 1, kb0 = 2 * (wave >> 1);

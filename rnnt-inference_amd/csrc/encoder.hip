@@ -318,8 +318,8 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       if (a.zero_next) *(uint32_t*)(dst + H) = 0u;
     } else {
       if (a.y32) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1], hv[2], hv[3]};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a.fperm[(size_t)n * H + chain_pos(u0 + i)] = f2bf(hv[i]);
+      *(uint2*)(a.fbf + (size_t)n * H + u0) = uint2{(uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1]) << 16),
+                                                      (uint32_t)f2bf_ftz(hv[2]) | ((uint32_t)f2bf_ftz(hv[3]) << 16)};
     }
   }
 }

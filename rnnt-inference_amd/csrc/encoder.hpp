@@ -34,7 +34,7 @@ struct EncStepArgs {
   uint16_t* c;         // [Npad][1024] fp16 cell state, in place
   int8_t* y8;          // I8: [Npad][1024] frame rows; STACKED: [Npad][2048] stacked frame rows
   float* y32;          // FINAL: optional fp32 f rows [Npad][1024]
-  uint16_t* fperm;     // FINAL: bf16 f rows [Npad][1024] in chain-permuted k order
+  uint16_t* fbf;     // FINAL: bf16 f rows [Npad][1024] (natural k, subnormals flushed): the joint's input
   const int32_t* lens; // [Npad] feature lengths (STACKED masking)
   int I;               // input width (256 / 1024 / 2048)
   int mode;            // EncOutMode

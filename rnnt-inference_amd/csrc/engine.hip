@@ -53,7 +53,7 @@ struct rnnt_engine {
   int8_t *x0q = nullptr, *yA = nullptr, *xs = nullptr, *yB = nullptr, *yC = nullptr;
   int8_t* h[5][2] = {};
   uint16_t* c[5] = {};
-  uint16_t* fperm = nullptr;
+  uint16_t* fbf = nullptr;
   float *F = nullptr, *hc = nullptr, *G = nullptr;
   int32_t* flen = nullptr;
   DecState ds{};
@@ -150,7 +150,7 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
     e->in_s[l] = m->enc_in_s[l];
     e->out_s[l] = m->enc_out_s[l];
   }
-  // prediction LSTM: rows gate-interleaved, k = [W_ih | W_hh] chain-permuted, biases separate
+  // prediction LSTM: rows gate-interleaved, k = [W_ih | W_hh] natural, biases separate
   // (the two chains b_ih + x.W_ih and b_hh + h.W_hh are summed after, oracle pred_row)
   for (int l = 0; l < 2; ++l) {
     if (!m->pred_w_ih[l] || !m->pred_w_hh[l] || !m->pred_b_ih[l] || !m->pred_b_hh[l])
@@ -161,7 +161,7 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
       for (int u = 0; u < P; ++u) {
         const int src = g * P + u, dst = 4 * u + g;
         for (int k = 0; k < 640; ++k)
-          w[(size_t)dst * 640 + chain_pos(k)] =
+          w[(size_t)dst * 640 + k] =
               k < P ? m->pred_w_ih[l][(size_t)src * P + k] : m->pred_w_hh[l][(size_t)src * P + k - P];
         b[dst] = m->pred_b_ih[l][src];
         b[PG4 + dst] = m->pred_b_hh[l][src];
@@ -175,10 +175,9 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
     e->dw.bih_p[l] = dbp;
     e->dw.bhh_p[l] = dbp + PG4;
   }
-  auto permute_rows = [](const uint16_t* src, int rows, int rows_pad, int K) {
+  auto pad_rows = [](const uint16_t* src, int rows, int rows_pad, int K) {
     std::vector<uint16_t> w((size_t)rows_pad * K, 0);
-    for (int r = 0; r < rows; ++r)
-      for (int k = 0; k < K; ++k) w[(size_t)r * K + chain_pos(k)] = src[(size_t)r * K + k];
+    std::copy(src, src + (size_t)rows * K, w.begin());
     return w;
   };
   if (!m->embed || !m->joint_w1t || !m->joint_w1p || !m->joint_w2 || !m->joint_bt || !m->joint_bp || !m->joint_b2)
@@ -186,9 +185,9 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
   uint16_t *emb, *w1t, *w1p, *w2;
   float *bt, *bp, *b2;
   int r = upload(e, &emb, std::vector<uint16_t>(m->embed, m->embed + 28 * P));
-  if (!r) r = upload(e, &w1t, permute_rows(m->joint_w1t, J, J, H));
-  if (!r) r = upload(e, &w1p, permute_rows(m->joint_w1p, J, J, P));
-  if (!r) r = upload(e, &w2, permute_rows(m->joint_w2, NLAB, NLAB_PAD, J));
+  if (!r) r = upload(e, &w1t, pad_rows(m->joint_w1t, J, J, H));
+  if (!r) r = upload(e, &w1p, pad_rows(m->joint_w1p, J, J, P));
+  if (!r) r = upload(e, &w2, pad_rows(m->joint_w2, NLAB, NLAB_PAD, J));
   if (!r) r = upload(e, &bt, std::vector<float>(m->joint_bt, m->joint_bt + J));
   if (!r) r = upload(e, &bp, std::vector<float>(m->joint_bp, m->joint_bp + J));
   if (!r) {
@@ -199,6 +198,12 @@ static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
   if (r) return r;
   e->dw.embed = emb; e->dw.w1t = w1t; e->dw.w1p = w1p; e->dw.w2 = w2;
   e->dw.bt = bt; e->dw.bp = bp; e->dw.b2 = b2;
+  // layer-0 input table (b_ih + emb[g].W_ih^T per label, same MFMA chain as the step kernels)
+  float* xtab;
+  if ((r = dev_alloc(e, &xtab, (size_t)29 * PG4))) return r;
+  if (launch_dec_xtab(e->dw, xtab, e->stream)) return fail(RNNT_EDEVICE, "xtab launch failed");
+  HIPCHK(hipStreamSynchronize(e->stream));
+  e->dw.xtab = xtab;
   return 0;
 }
 
@@ -215,7 +220,7 @@ static int alloc_workspace(rnnt_engine* e) {
     r = r ? r : dev_alloc(e, &e->h[l][1], NP * H);
     r = r ? r : dev_alloc(e, &e->c[l], NP * H);
   }
-  r = r ? r : dev_alloc(e, &e->fperm, TPM * NP * H);
+  r = r ? r : dev_alloc(e, &e->fbf, TPM * NP * H);
   r = r ? r : dev_alloc(e, &e->F, TPM * NP * J);
   r = r ? r : dev_alloc(e, &e->hc, NP * 2 * 4 * P);
   r = r ? r : dev_alloc(e, &e->G, NP * J);
@@ -327,7 +332,7 @@ static EncStepArgs make_job(rnnt_engine* e, int l, int t, int n_pad, const int8_
     a.y8 = (int8_t*)y + (size_t)t * n_pad * H;
   } else {
     a.y32 = y32 ? y32 + (size_t)t * n_pad * H : nullptr;
-    a.fperm = (uint16_t*)y + (size_t)t * n_pad * H;
+    a.fbf = (uint16_t*)y + (size_t)t * n_pad * H;
   }
   return a;
 }
@@ -417,7 +422,7 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
         const int tp = d / 2;
         if (l == 2) tb.add(make_job(e, 2, tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, lens, T), tiles(2 * tp));
         if (l == 3) tb.add(make_job(e, 3, tp, n_pad, e->yB, ENC_OUT_I8, e->yC, nullptr, lens, T), tiles(2 * tp));
-        if (l == 4) tb.add(make_job(e, 4, tp, n_pad, e->yC, ENC_OUT_FINAL, e->fperm, f_out, lens, T), tiles(2 * tp));
+        if (l == 4) tb.add(make_job(e, 4, tp, n_pad, e->yC, ENC_OUT_FINAL, e->fbf, f_out, lens, T), tiles(2 * tp));
       }
     }
     if ((r = tb.launch(e, st))) return r;
@@ -440,7 +445,7 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   hipStream_t st = pick(e, stream);
   const int Tp = (e->last_T + 1) / 2;
   hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
-  if (launch_joint_trans(e->dw, e->fperm, e->flen, e->F, Tp, e->last_npad, st))
+  if (launch_joint_trans(e->dw, e->fbf, e->flen, e->F, Tp, e->last_npad, st))
     return fail(RNNT_EDEVICE, "joint_trans launch failed");
   hipEvent_t ev1 = e->prof ? new_event(st) : nullptr;
   DecArgs a{};
@@ -533,7 +538,7 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
     int8_t* dst = last ? (int8_t*)y : ((cur == e->yA) ? e->yB : e->yA);
     int r;
     if (l == 4)
-      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_FINAL, e->fperm, (float*)y, st);
+      r = run_layer(e, l, T, n_pad, cur, ENC_OUT_FINAL, e->fbf, (float*)y, st);
     else
       r = run_layer(e, l, T, n_pad, cur, ENC_OUT_I8, dst, nullptr, st);
     if (r) return r;

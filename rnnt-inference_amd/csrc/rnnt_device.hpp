@@ -126,6 +126,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 }
 __device__ __forceinline__ float bf2f(uint16_t b) { return bits2f((uint32_t)b << 16); }
 __device__ __forceinline__ float bf_round(float x) { return bf2f(f2bf(x)); }
+// bf16 operands of the decoder's MFMA dot products: f32 subnormals flush to zero first (the
+// MFMA model counts bf16 subnormals as zero; flushing at the producer keeps both sides equal)
+__device__ __forceinline__ uint16_t f2bf_ftz(float f) {
+  return __builtin_fabsf(f) < 1.17549435e-38f ? (uint16_t)((f2bits(f) >> 16) & 0x8000u) : f2bf(f);
+}
+__device__ __forceinline__ float bf_round_ftz(float x) { return bf2f(f2bf_ftz(x)); }
 __device__ __forceinline__ int8_t q8(float v) {
   float r = __builtin_rintf(v);
   r = __builtin_fminf(__builtin_fmaxf(r, -128.0f), 127.0f);
