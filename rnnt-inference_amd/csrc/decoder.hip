@@ -20,6 +20,10 @@
 //     (and the joint's prediction half G) is evaluated once per emit, not once per step;
 //   * layer 0's input half b_ih + emb[g].W_ih^T depends only on the label: a [29][1280] table
 //     computed once per engine with the same instruction sequence (launch_dec_xtab).
+// The step is latency-bound (four dependent launches), so each kernel keeps its chain of
+// dependent memory round trips short: emit-list entries carry (row, slot, label), the list
+// entries of a workgroup's first tile are loaded beside the list length, the cell state is
+// fetched beside the input staging, and the joint walks a compact list of unfinished rows.
 #include "rnnt_device.hpp"
 #include "decoder.hpp"
 
@@ -35,6 +39,34 @@ __device__ __forceinline__ uint4 pack8(const float4 lo, const float4 hi) {
   return uint4{(f2bits(lo.x) >> 16) | (f2bits(lo.y) & 0xffff0000u), (f2bits(lo.z) >> 16) | (f2bits(lo.w) & 0xffff0000u),
                (f2bits(hi.x) >> 16) | (f2bits(hi.y) & 0xffff0000u), (f2bits(hi.z) >> 16) | (f2bits(hi.w) & 0xffff0000u)};
 }
+// emit-list entry: row | committed slot << 24 | label-table index << 25 (28 = SOS)
+__device__ __forceinline__ int emit_entry(int row, int slot, int label) { return row | (slot << 24) | (label << 25); }
+__device__ __forceinline__ int entry_row(int e) { return e & 0xffffff; }
+__device__ __forceinline__ int entry_slot(int e) { return (e >> 24) & 1; }
+__device__ __forceinline__ int entry_label(int e) { return (e >> 25) & 31; }
+
+// development instrumentation (-DRNNT_DEV_STAMPS, tools/build_variants.sh stamps): thread 0 of
+// each working workgroup of the step kernels records s_memrealtime (100 MHz) at kernel start,
+// once its list entries are known, after the input staging and after its first tile.
+#ifdef RNNT_DEV_STAMPS
+__device__ unsigned long long g_st[1 << 22];
+__device__ unsigned int g_st_n;
+#define ST_MARK(v) unsigned long long v = threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull
+#define ST_SET(v) if (threadIdx.x == 0 && v == 0ull) v = __builtin_amdgcn_s_memrealtime()
+#define ST_FLUSH(kid, a0, a1, a2, a3)                                                  \
+  if (threadIdx.x == 0) {                                                              \
+    const unsigned k_ = atomicAdd(&g_st_n, 1u);                                        \
+    if (k_ < (1u << 22) / 6) {                                                         \
+      g_st[6 * k_] = (kid); g_st[6 * k_ + 1] = blockIdx.x + 65536ull * blockIdx.y;     \
+      g_st[6 * k_ + 2] = a0; g_st[6 * k_ + 3] = a1; g_st[6 * k_ + 4] = a2;             \
+      g_st[6 * k_ + 5] = (a3) ? (a3) : __builtin_amdgcn_s_memrealtime();               \
+    }                                                                                  \
+  }
+#else
+#define ST_MARK(v)
+#define ST_SET(v)
+#define ST_FLUSH(kid, a0, a1, a2, a3)
+#endif
 
 // ---------------------------------------------------------------- layer-0 input table
 // xtab[g][r] = b_ih0[r] + emb[g].W_ih0[r]^T (g < 28), xtab[28] = b_ih0 (SOS: zero embedding).
@@ -117,8 +149,8 @@ __global__ void __launch_bounds__(256) joint_trans_kernel(DecWeights w, const ui
 // ---------------------------------------------------------------- greedy decode
 // Lock-step over the batch, like the reference's loop (rnnt_model.hpp:92-124), but only the
 // rows that emitted at the previous step re-run the prediction network:
-//   pred(layer 0) -> pred(layer 1) -> G  for the listed rows      (weight-stationary grids)
-//   joint + argmax + greedy update for every unfinished row -> next step's emit list
+//   pred(layer 0) -> pred(layer 1) -> G  for the emit list's rows   (weight-stationary grids)
+//   joint + argmax + greedy update for the live list's rows -> next step's emit / live lists
 
 __device__ __forceinline__ float* hc_part(float* hc, int row, int slot, int part) {
   return hc + ((size_t)row * 2 + slot) * 4 * P + part * P;  // parts 0:h0 1:h1 2:c0 3:c1
@@ -134,18 +166,27 @@ __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
   float* h = hc_part(a.hc, row, 0, 0);
   for (int k = 0; k < 4 * P; ++k) h[k] = 0.0f;  // committed state starts at zero (metadata.cpp:25-30)
   if (fl > 0) {
-    s.list[atomicAdd(&s.count[0], 1)] = row;  // every live row needs its first (SOS) prediction
+    s.list[atomicAdd(&s.count[0], 1)] = emit_entry(row, 0, 28);  // every live row needs its first (SOS) prediction
+    s.live[atomicAdd(&s.count[2], 1)] = row;
     atomicAdd(s.unfinished, 1);
   }
 }
 
 // One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates =
-// (b_ih + x.W_ih^T) + (b_hh + h.W_hh^T); c fp32, h bf16.  A workgroup (8 waves) owns 8*NT gate
-// tiles; wave w holds tiles NT*w .. NT*w+NT-1: their W_hh (and, layer 1, W_ih) rows stay in
-// registers for the launch (10 x 16 B per tile and chain per lane: NT = 2 for layer 0, whose
-// input half comes from the label table, 1 for layer 1).  Grid: x = 80 / (8 NT) gate groups,
-// y = row groups striding over the emit list's 16-row tiles.
-constexpr int PRED_THREADS = 512;
+// (b_ih + x.W_ih^T) + (b_hh + h.W_hh^T); c fp32, h bf16.  A workgroup (4 waves) owns 4 gate
+// tiles, one per wave, whose W_hh (and, layer 1, W_ih) rows stay in registers for the launch
+// (10 x 16 B per chain per lane; layer 0's input half comes from the label table).  Every
+// launch reloads its weights, and one CU takes in only a few tens of GB/s, so the slice per
+// workgroup is kept small (20-40 KB: in-kernel stamps showed 160-320 KB slices costing 12-20 us
+// per launch).  Grid: x = 20 gate groups, y = row groups striding over the emit list's tiles.
+constexpr int PRED_THREADS = 256;  // 4 waves, one gate tile each: 40 KB of weights per workgroup
+// rows per workgroup iteration of the step kernels (16: one MFMA row tile; 64 measured slower:
+// 148 vs 110 ms per query of greedy decode)
+#ifndef RNNT_DEC_RT
+#define RNNT_DEC_RT 16
+#endif
+constexpr int DEC_RT = RNNT_DEC_RT;
+constexpr int DEC_SUB = DEC_RT / 16;
 #ifndef RNNT_PRED_RG
 #define RNNT_PRED_RG 48
 #endif
@@ -161,18 +202,21 @@ constexpr int JOINT_GROUPS = RNNT_JOINT_G;
 
 template <int LAYER>
 __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int parity) {
-  constexpr int NT = LAYER ? 1 : 2;      // gate tiles per wave
+  constexpr int NT = 1;                  // gate tiles per wave
   constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
   constexpr int XP = KX + 8;             // bf16 pitch: +16 B per row (conflict-free b128 reads)
-  __shared__ __attribute__((aligned(16))) uint16_t X[16][XP];
-  __shared__ int rows[16], slots[16], pregs[16];
+  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][XP];
+  __shared__ int ents[DEC_RT];
   const DecState& s = a.s;
-  const int cnt = s.count[parity];
-  const int ntiles = (cnt + 15) >> 4;
-  if ((int)blockIdx.y >= ntiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  ST_MARK(st0);
   const int* list = s.list + parity * a.Npad;
-  const int t0 = (blockIdx.x * 8 + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
+  // the first tile's entries load beside the list length (the grid never exceeds Npad/DEC_RT tiles)
+  const int e_first = tid < DEC_RT ? list[blockIdx.y * DEC_RT + tid] : 0;
+  const int cnt = s.count[parity];
+  const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
+  if ((int)blockIdx.y >= ntiles) return;
+  const int t0 = (blockIdx.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
   uint4 wh[NT][P / 32], wx[NT][LAYER ? P / 32 : 1];
   float4 bh[NT], bx[NT];
 #pragma unroll
@@ -188,131 +232,169 @@ __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int p
     bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
   }
   for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
-    if (tid < 16) {
-      const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
-      rows[tid] = row;
-      slots[tid] = row >= 0 ? s.slot[row] : 0;
-      pregs[tid] = row >= 0 ? s.preg[row] : SOS;
+    if (tid < DEC_RT) {
+      const int e = rt == (int)blockIdx.y ? e_first : list[rt * DEC_RT + tid];
+      ents[tid] = rt * DEC_RT + tid < cnt ? e : -1;
     }
     __syncthreads();
+    ST_MARK(st1);
+    // this lane's committed cell states (sub-tile st: row ents[16 st + c]), fetched beside the
+    // input staging
+    float cp[DEC_SUB][NT];
+#pragma unroll
+    for (int st = 0; st < DEC_SUB; ++st) {
+      const int ec = ents[16 * st + c];
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt)
+        cp[st][tt] = ec >= 0 ? hc_part(a.hc, entry_row(ec), entry_slot(ec), 2 + LAYER)[(t0 + tt) * 4 + q] : 0.0f;
+    }
     // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1
     // [h0 of the candidate slot | h1 committed]
-    for (int i = tid; i < 16 * (KX / 8); i += PRED_THREADS) {
-      const int m = i / (KX / 8), k = (i % (KX / 8)) * 8, row = rows[m];
+    for (int i = tid; i < DEC_RT * (KX / 8); i += PRED_THREADS) {
+      const int m = i / (KX / 8), k = (i % (KX / 8)) * 8, em = ents[m];
       uint4 v = uint4{0u, 0u, 0u, 0u};
-      if (row >= 0) {
-        const int sl = slots[m];
-        const float* src = LAYER == 0 ? hc_part(a.hc, row, sl, 0) + k
-                                      : (k < P ? hc_part(a.hc, row, sl ^ 1, 0) + k : hc_part(a.hc, row, sl, 1) + k - P);
+      if (em >= 0) {
+        const int r = entry_row(em), smm = entry_slot(em);
+        const float* src = LAYER == 0 ? hc_part(a.hc, r, smm, 0) + k
+                                      : (k < P ? hc_part(a.hc, r, smm ^ 1, 0) + k : hc_part(a.hc, r, smm, 1) + k - P);
         v = pack8(*(const float4*)src, *(const float4*)(src + 4));
       }
       *(uint4*)&X[m][k] = v;
     }
     __syncthreads();
-    const int row = rows[c];
+    ST_MARK(st2);
 #pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-      v4f ah = v4f{bh[tt].x, bh[tt].y, bh[tt].z, bh[tt].w};
+    for (int st = 0; st < DEC_SUB; ++st) {
+      const int ec = ents[16 * st + c];
+      if (!__any(ec >= 0)) continue;  // wave-uniform: the whole sub-tile is past the list end
+      const int row = ec >= 0 ? entry_row(ec) : -1, sl = ec >= 0 ? entry_slot(ec) : 0;
+      const int lab = ec >= 0 ? entry_label(ec) : 28;
+      const uint16_t* xr = &X[16 * st + c][8 * q];
 #pragma unroll
-      for (int b = 0; b < P / 32; ++b) ah = mfma_bf16(wh[tt][b], *(const uint4*)&X[c][(LAYER ? P : 0) + 32 * b + 8 * q], ah);
-      v4f ax;
-      if (LAYER) {
-        ax = v4f{bx[tt].x, bx[tt].y, bx[tt].z, bx[tt].w};
+      for (int tt = 0; tt < NT; ++tt) {
+        v4f ah = v4f{bh[tt].x, bh[tt].y, bh[tt].z, bh[tt].w};
 #pragma unroll
-        for (int b = 0; b < P / 32; ++b) ax = mfma_bf16(wx[tt][b], *(const uint4*)&X[c][32 * b + 8 * q], ax);
-      } else {
-        const int g = pregs[c] == SOS ? 28 : pregs[c];
-        const float4 xt = *(const float4*)(a.w.xtab + (size_t)g * PG4 + (t0 + tt) * 16 + 4 * q);
-        ax = v4f{xt.x, xt.y, xt.z, xt.w};
-      }
-      if (row >= 0) {
-        const v4f gs = ax + ah;
-        const int sl = slots[c];
-        const int u = (t0 + tt) * 4 + q;
-        const float ig = det_sigmoid(gs[0]), fg = det_sigmoid(gs[1]), gg = det_tanh(gs[2]), og = det_sigmoid(gs[3]);
-        const float cp = hc_part(a.hc, row, sl, 2 + LAYER)[u];
-        const float cn = fg * cp + ig * gg;
-        const float hh = bf_round_ftz(og * det_tanh(cn));
-        hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
-        hc_part(a.hc, row, sl ^ 1, LAYER)[u] = hh;
+        for (int b = 0; b < P / 32; ++b) ah = mfma_bf16(wh[tt][b], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ah);
+        v4f ax;
+        if (LAYER) {
+          ax = v4f{bx[tt].x, bx[tt].y, bx[tt].z, bx[tt].w};
+#pragma unroll
+          for (int b = 0; b < P / 32; ++b) ax = mfma_bf16(wx[tt][b], *(const uint4*)(xr + 32 * b), ax);
+        } else {
+          const float4 xt = *(const float4*)(a.w.xtab + (size_t)lab * PG4 + (t0 + tt) * 16 + 4 * q);
+          ax = v4f{xt.x, xt.y, xt.z, xt.w};
+        }
+        if (row >= 0) {
+          const v4f gs = ax + ah;
+          const int u = (t0 + tt) * 4 + q;
+          const float ig = det_sigmoid(gs[0]), fg = det_sigmoid(gs[1]), gg = det_tanh(gs[2]), og = det_sigmoid(gs[3]);
+          const float cn = fg * cp[st][tt] + ig * gg;
+          const float hh = bf_round_ftz(og * det_tanh(cn));
+          hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
+          hc_part(a.hc, row, sl ^ 1, LAYER)[u] = hh;
+        }
       }
     }
-    __syncthreads();  // X / rows are restaged by the next tile
+    __syncthreads();  // X / ents are restaged by the next tile
+    ST_FLUSH(LAYER, st0, st1, st2, 0ull);
   }
 }
 
-// G = b_p + g . W1p^T for the listed rows' new candidates.  One workgroup (8 waves, 4 column
-// tiles each: all 512 columns, weights in registers) per row group striding over 16-row
-// tiles.  Also clears the other parity's emit list for the joint that follows.
+// G = b_p + g . W1p^T for the listed rows' new candidates.  Workgroups of 4 waves, one 16-column
+// tile (10 KB of W1p) per wave in registers: grid x = 8 column groups, y = row groups striding
+// over the emit list's tiles.  Also clears the next step's emit and live lists for the joint
+// that follows.
 constexpr int GXP = P + 8;
-__global__ void __launch_bounds__(512) dec_g_kernel(DecArgs a, int parity) {
-  __shared__ __attribute__((aligned(16))) uint16_t X[16][GXP];
-  __shared__ int rows[16], slots[16];
+constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each; grid x = 8 column groups
+__global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
+  __shared__ int ents[DEC_RT];
   DecState& s = a.s;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) s.count[parity ^ 1] = 0;
-  const int cnt = s.count[parity];
-  const int ntiles = (cnt + 15) >> 4;
-  if ((int)blockIdx.y >= ntiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  ST_MARK(st0);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
+    s.count[parity ^ 1] = 0;
+    s.count[2 + (parity ^ 1)] = 0;
+  }
   const int* list = s.list + parity * a.Npad;
-  uint4 wv[4][P / 32];
-  float4 b0[4];
+  const int e_first = tid < DEC_RT ? list[blockIdx.y * DEC_RT + tid] : 0;
+  const int cnt = s.count[parity];
+  const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
+  if ((int)blockIdx.y >= ntiles) return;
+  constexpr int NJ = 1;  // column tiles per wave
+  uint4 wv[NJ][P / 32];
+  float4 b0[NJ];
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const int jt = wave * 4 + jj;
+  for (int jj = 0; jj < NJ; ++jj) {
+    const int jt = (blockIdx.x * (G_THREADS / 64) + wave) * NJ + jj;
     const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
     b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
   }
   for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
-    if (tid < 16) {
-      const int row = (rt * 16 + tid < cnt) ? list[rt * 16 + tid] : -1;
-      rows[tid] = row;
-      slots[tid] = row >= 0 ? s.slot[row] : 0;
+    if (tid < DEC_RT) {
+      const int e = rt == (int)blockIdx.y ? e_first : list[rt * DEC_RT + tid];
+      ents[tid] = rt * DEC_RT + tid < cnt ? e : -1;
     }
     __syncthreads();
-    for (int i = tid; i < 16 * (P / 8); i += 512) {
-      const int m = i / (P / 8), k = (i % (P / 8)) * 8, row = rows[m];
+    ST_MARK(st1);
+    for (int i = tid; i < DEC_RT * (P / 8); i += G_THREADS) {
+      const int m = i / (P / 8), k = (i % (P / 8)) * 8, em = ents[m];
       uint4 v = uint4{0u, 0u, 0u, 0u};
-      if (row >= 0) {
-        const float* src = hc_part(a.hc, row, slots[m] ^ 1, 1) + k;
+      if (em >= 0) {
+        const float* src = hc_part(a.hc, entry_row(em), entry_slot(em) ^ 1, 1) + k;
         v = pack8(*(const float4*)src, *(const float4*)(src + 4));
       }
       *(uint4*)&X[m][k] = v;
     }
     __syncthreads();
-    const int row = rows[c];
+    ST_MARK(st2);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      v4f acc = v4f{b0[jj].x, b0[jj].y, b0[jj].z, b0[jj].w};
+    for (int st = 0; st < DEC_SUB; ++st) {
+      const int ec = ents[16 * st + c];
+      if (!__any(ec >= 0)) continue;
+      const uint16_t* xr = &X[16 * st + c][8 * q];
 #pragma unroll
-      for (int b = 0; b < P / 32; ++b) acc = mfma_bf16(wv[jj][b], *(const uint4*)&X[c][32 * b + 8 * q], acc);
-      if (row >= 0)
-        *(float4*)(a.G + (size_t)row * J + (wave * 4 + jj) * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
+      for (int jj = 0; jj < NJ; ++jj) {
+        v4f acc = v4f{b0[jj].x, b0[jj].y, b0[jj].z, b0[jj].w};
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) acc = mfma_bf16(wv[jj][b], *(const uint4*)(xr + 32 * b), acc);
+        const int jt = (blockIdx.x * (G_THREADS / 64) + wave) * NJ + jj;
+        if (ec >= 0)
+          *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
+      }
     }
     __syncthreads();
+    ST_FLUSH(2, st0, st1, st2, 0ull);
   }
 }
 
 // joint (y1 = bf16(relu(F[t] + G)), logits = b2 + y1.W2^T) + argmax + greedy_decode_update
-// (decoder.py:137-167) for 16 rows per workgroup.  A blank (or a forced advance after
-// max_symbols_per_step) moves the row to its next frame with the SAME prediction, so the
+// (decoder.py:137-167) for DEC_RT live-list rows per workgroup tile.  A blank (or a forced advance
+// after max_symbols_per_step) moves the row to its next frame with the SAME prediction, so the
 // workgroup evaluates up to RNNT_JOINT_ITERS frames per launch, stopping a row at its first
 // emission (it then needs a new prediction: next step's emit list) or at its last frame; rows
-// still in a blank run stay live for the next step.  Identical results for any cap; the cap
+// not finished go to the next step's live list.  Identical results for any cap; the cap
 // trades lock-step steps against the length of each step.
 #ifndef RNNT_JOINT_ITERS
 #define RNNT_JOINT_ITERS 2
 #endif
 constexpr int YP = J + 8;
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
-  __shared__ __attribute__((aligned(16))) uint16_t X[16][YP];
-  __shared__ float L[16][NLAB_PAD + 1];
-  __shared__ float Lp[4][16][NLAB_PAD + 1];
-  __shared__ int live[16], tidx[16];
+  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][YP];
+  __shared__ float L[DEC_RT][NLAB_PAD + 1];
+  __shared__ float Lp[4][DEC_RT][NLAB_PAD + 1];
+  __shared__ int rows[DEC_RT], walking[DEC_RT], tidx[DEC_RT];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  ST_MARK(st0);
+  const int* llist = s.live + parity * a.Npad;
+  int* nlist = s.live + (parity ^ 1) * a.Npad;
+  const int r_first = tid < DEC_RT ? llist[blockIdx.x * DEC_RT + tid] : 0;
+  const int lcnt = s.count[2 + parity];
+  const int ntiles = (lcnt + DEC_RT - 1) / DEC_RT;
+  if ((int)blockIdx.x >= ntiles) return;
   // logits = ((s0 + s1) + s2) + s3, s_b = y1[128b : 128b+128] . W2^T (s0 from b2): wave w runs
   // label half w&1 over k blocks 2(w>>1) and 2(w>>1)+1 as two independent 4-instruction chains
   const int lh = wave & 1, kb0 = 2 * (wave >> 1);
@@ -330,24 +412,28 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     const float4 b0 = *(const float4*)(a.w.b2 + lh * 16 + 4 * q);
     bias = v4f{b0.x, b0.y, b0.z, b0.w};
   }
-  for (int rtile = blockIdx.x; rtile < (a.N + 15) / 16; rtile += gridDim.x) {
-    const int r0 = rtile * 16;
-    if (tid < 16) {
-      const int row = r0 + tid;
-      const int lv = (row < a.N) && !s.fin[row];
-      live[tid] = lv;
-      tidx[tid] = lv ? s.time[row] : 0;
+  for (int rt = blockIdx.x; rt < ntiles; rt += gridDim.x) {
+    if (tid < DEC_RT) {
+      const int i = rt * DEC_RT + tid;
+      const int r = i < lcnt ? (rt == (int)blockIdx.x ? r_first : llist[i]) : -1;
+      rows[tid] = r;
+      walking[tid] = r >= 0;
+      tidx[tid] = r >= 0 ? s.time[r] : 0;
     }
     __syncthreads();
+    ST_MARK(st1);
+#ifdef RNNT_DEV_STAMPS
+    unsigned long long st2 = 0ull;
+#endif
     for (int it = 0; it < RNNT_JOINT_ITERS; ++it) {
       bool any = false;
-#pragma unroll
-      for (int m = 0; m < 16; ++m) any |= live[m] != 0;
+      for (int m = 0; m < DEC_RT; ++m) any |= walking[m] != 0;
       if (!any) break;
-      for (int i = tid; i < 16 * (J / 8); i += 256) {
-        const int m = i / (J / 8), k = (i % (J / 8)) * 8, row = r0 + m;
+      for (int i = tid; i < DEC_RT * (J / 8); i += 256) {
+        const int m = i / (J / 8), k = (i % (J / 8)) * 8;
         uint4 v = uint4{0u, 0u, 0u, 0u};
-        if (live[m]) {
+        if (walking[m]) {
+          const int row = rows[m];
           const float* fr = a.F + ((size_t)tidx[m] * a.Npad + row) * J + k;
           const float* gr = a.G + (size_t)row * J + k;
           float y[8];
@@ -366,27 +452,31 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
         *(uint4*)&X[m][k] = v;
       }
       __syncthreads();
-      {
+      ST_SET(st2);
+#pragma unroll
+      for (int st = 0; st < DEC_SUB; ++st) {
+        if (!__any(walking[16 * st + c] != 0)) continue;
+        const uint16_t* xr = &X[16 * st + c][8 * q];
         v4f s0 = bias, s1 = v4f{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          s0 = mfma_bf16(wv[b], *(const uint4*)&X[c][128 * kb0 + 32 * b + 8 * q], s0);
-          s1 = mfma_bf16(wv[4 + b], *(const uint4*)&X[c][128 * (kb0 + 1) + 32 * b + 8 * q], s1);
+          s0 = mfma_bf16(wv[b], *(const uint4*)(xr + 128 * kb0 + 32 * b), s0);
+          s1 = mfma_bf16(wv[4 + b], *(const uint4*)(xr + 128 * (kb0 + 1) + 32 * b), s1);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          Lp[kb0][c][lh * 16 + 4 * q + r] = s0[r];
-          Lp[kb0 + 1][c][lh * 16 + 4 * q + r] = s1[r];
+          Lp[kb0][16 * st + c][lh * 16 + 4 * q + r] = s0[r];
+          Lp[kb0 + 1][16 * st + c][lh * 16 + 4 * q + r] = s1[r];
         }
       }
       __syncthreads();
-      for (int i = tid; i < 16 * NLAB_PAD; i += 256) {
+      for (int i = tid; i < DEC_RT * NLAB_PAD; i += 256) {
         const int m = i / NLAB_PAD, j = i % NLAB_PAD;
         L[m][j] = ((Lp[0][m][j] + Lp[1][m][j]) + Lp[2][m][j]) + Lp[3][m][j];
       }
       __syncthreads();
-      if (tid < 16 && live[tid]) {
-        const int m = tid, row = r0 + m;
+      if (tid < DEC_RT && walking[tid]) {
+        const int m = tid, row = rows[m];
         int best = 0;
         float bv = L[m][0];
         for (int j = 1; j < NLAB; ++j)
@@ -396,16 +486,18 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
           s.added[row]++;
           s.preg[row] = best;
-          s.slot[row] ^= 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
-          s.list[(parity ^ 1) * a.Npad + atomicAdd(&s.count[parity ^ 1], 1)] = row;
-          live[m] = 0;
+          const int nsl = s.slot[row] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+          s.slot[row] = nsl;
+          s.list[(parity ^ 1) * a.Npad + atomicAdd(&s.count[parity ^ 1], 1)] = emit_entry(row, nsl, best);
+          walking[m] = 0;
         } else {
           const int fl = a.f_lens[row];
           int t = tidx[m] + 1;
           if (t >= fl) {
             s.fin[row] = 1;
             atomicSub(s.unfinished, 1);
-            live[m] = 0;
+            walking[m] = 0;
+            rows[m] = -1;  // finished: not in the next live list
             t = fl - 1;
           }
           tidx[m] = t;
@@ -415,7 +507,9 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       }
       __syncthreads();
     }
-    __syncthreads();  // live / tidx / X are reused by the next row tile
+    if (tid < DEC_RT && rows[tid] >= 0) nlist[atomicAdd(&s.count[2 + (parity ^ 1)], 1)] = rows[tid];
+    __syncthreads();  // rows / walking / tidx / X are reused by the next row tile
+    ST_FLUSH(3, st0, st1, st2, 0ull);
   }
 }
 
@@ -425,7 +519,7 @@ __global__ void dec_finish_kernel(DecArgs a) {
 }
 
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st) {
-  const int rt = a.Npad / 16;
+  const int rt = a.Npad / DEC_RT;
   if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.s.unfinished, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
@@ -436,16 +530,18 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   bool done = false;
   while (!done && step < a.max_iter) {
     // row-tile workgroups per launch: one resident round, and no more than the live rows need
-    const int lt = (live_bound + 15) / 16 < rt ? (live_bound + 15) / 16 : rt;
+    const int lt = (live_bound + DEC_RT - 1) / DEC_RT < rt ? (live_bound + DEC_RT - 1) / DEC_RT : rt;
     const int lt1 = lt > 0 ? lt : 1;
     const int rg_pred = lt1 < PRED_ROW_GROUPS ? lt1 : PRED_ROW_GROUPS;
     const int rg_g = lt1 < G_ROW_GROUPS ? lt1 : G_ROW_GROUPS;
-    const int rg_joint = rt < JOINT_GROUPS ? rt : JOINT_GROUPS;
+    const int rg_joint = lt1 < JOINT_GROUPS ? lt1 : JOINT_GROUPS;
     for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      hipLaunchKernelGGL(dec_pred_kernel<0>, dim3(PG4 / 256, rg_pred), dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL(dec_pred_kernel<1>, dim3(PG4 / 128, rg_pred), dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL(dec_g_kernel, dim3(1, rg_g), dim3(512), 0, st, a, p);
+      hipLaunchKernelGGL(dec_pred_kernel<0>, dim3(PG4 / (16 * (PRED_THREADS / 64)), rg_pred), dim3(PRED_THREADS), 0, st,
+                         a, p);
+      hipLaunchKernelGGL(dec_pred_kernel<1>, dim3(PG4 / (16 * (PRED_THREADS / 64)), rg_pred), dim3(PRED_THREADS), 0, st,
+                         a, p);
+      hipLaunchKernelGGL(dec_g_kernel, dim3(J / (16 * (G_THREADS / 64)), rg_g), dim3(G_THREADS), 0, st, a, p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
     }
     // poll the live-row counter one chunk behind, so the host never drains the queue
@@ -487,3 +583,17 @@ int launch_dec_xtab(const DecWeights& w, float* xtab, hipStream_t st) {
 }
 
 }  // namespace rnnt
+
+#ifdef RNNT_DEV_STAMPS
+// development: copy out (and reset) the step kernels' stamp records (6 x u64 each)
+extern "C" int rnnt_dev_read_stamps(unsigned long long* out, int max_records) {
+  unsigned int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(rnnt::g_st_n), sizeof(n)) != hipSuccess) return -1;
+  if (n > (1u << 22) / 6) n = (1u << 22) / 6;
+  if ((int)n > max_records) n = max_records;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_st), (size_t)n * 6 * 8) != hipSuccess) return -1;
+  const unsigned int z = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_st_n), &z, sizeof(z)) != hipSuccess) return -1;
+  return (int)n;
+}
+#endif

@@ -228,6 +228,7 @@ static int alloc_workspace(rnnt_engine* e) {
   int32_t** ints[] = {&e->ds.time, &e->ds.added, &e->ds.idx, &e->ds.preg, &e->ds.slot, &e->ds.fin};
   for (auto pp : ints) r = r ? r : dev_alloc(e, pp, NP);
   r = r ? r : dev_alloc(e, &e->ds.list, 2 * NP);
+  r = r ? r : dev_alloc(e, &e->ds.live, 2 * NP);
   r = r ? r : dev_alloc(e, &e->ds.count, 4);
   r = r ? r : dev_alloc(e, &e->ds.unfinished, 4);
   if (!r && hipHostMalloc((void**)&e->host_flags, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)

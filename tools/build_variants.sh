@@ -38,6 +38,12 @@ for v in "$@"; do
     noload_noepi) build noload_noepi -DRNNT_DEV_NO_LOAD -DRNNT_DEV_NO_EPI ;;
     noload) build noload -DRNNT_DEV_NO_LOAD ;;
     ji1) build ji1 -DRNNT_JOINT_ITERS=1 ;;
+    stamps) build stamps -DRNNT_DEV_STAMPS ;;
+    rt64) build rt64 -DRNNT_DEC_RT=64 ;;
+    ji3) build ji3 -DRNNT_JOINT_ITERS=3 ;;
+    ji6) build ji6 -DRNNT_JOINT_ITERS=6 ;;
+    jg128) build jg128 -DRNNT_JOINT_G=128 ;;
+    jg256) build jg256 -DRNNT_JOINT_G=256 ;;
     ji2) build ji2 -DRNNT_JOINT_ITERS=2 ;;
     ji4) build ji4 -DRNNT_JOINT_ITERS=4 ;;
     ji8) build ji8 -DRNNT_JOINT_ITERS=8 ;;
