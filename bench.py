@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--enc-reserve", type=int, default=0,
                     help="CUs per XCD kept off the encoder streams (CU-masked HIP streams, rnnt_stream_create); "
                          "each engine's decode then runs on its own unrestricted stream and always finds free CUs")
+    ap.add_argument("--dec-cus", type=int, default=0,
+                    help="CUs per XCD the decode streams may use (CU-masked; 0 = all): bounds how many CUs the "
+                         "overlapped greedy decode takes from the encoder")
     ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wav", action="store_true",
@@ -293,7 +296,11 @@ def main():
                for _ in range(args.inflight)]
     engine = engines[0]
     owned = []
-    if args.enc_reserve:
+    if args.dec_cus:
+        owned = [PartitionedStream(local, cu_mask_words(args.dec_cus, reserved=True)) for _ in engines]
+        streams = [torch.cuda.Stream() for _ in engines]
+        dec_streams = [p.stream for p in owned]
+    elif args.enc_reserve:
         owned = [PartitionedStream(local, cu_mask_words(args.enc_reserve)) for _ in engines]
         owned += [PartitionedStream(local) for _ in engines]
         streams = [p.stream for p in owned[: len(engines)]]
@@ -374,7 +381,7 @@ def main():
         "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
                    "qsl_per_gpu": args.qsl, "query_samples_per_gpu": args.query, "batch_size": args.batch,
                    "batches_in_flight": args.inflight,
-                   "encoder_cu_reserve_per_xcd": args.enc_reserve,
+                   "encoder_cu_reserve_per_xcd": args.enc_reserve, "decode_cus_per_xcd": args.dec_cus or 32,
                    "input": ("16 kHz audio: GPU featurizer (FilterbankFeatures.forward) in the timed region" if args.wav
                              else "log-mel features resident in HBM"),
                    "encoder": "int8 (lstm_amx_int8)",

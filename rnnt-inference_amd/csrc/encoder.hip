@@ -70,6 +70,7 @@ constexpr int TAB_OFF = NSTAGE * STAGE_BYTES;   // LDS: sigma table after the ri
 constexpr int SMEM_BYTES = TAB_OFF + 128 * 16;
 static_assert(BPW == 2 && (APW == 2 || APW == 4) && C_GLDS == 4, "staging split");
 static_assert(BN * 128 <= STAGE_BYTES, "the cell-state image fits one ring buffer");
+static_assert(NSTAGE >= 3 && BN * 80 <= STAGE_BYTES, "the epilogue's h / y images fit two other ring buffers");
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) char lds_char;
@@ -285,10 +286,18 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     bq[i] = *(const float4*)(a.bq + m0 + wm * 64 + i * 16 + q * 4);
 #endif
   }
+  // results go to LDS first and leave as whole 128-/64-byte row segments (16 B per lane,
+  // full cache lines per wave instruction) instead of 4-/8-byte scattered per-lane stores:
+  // c_new in place over the c_in image (each lane rewrites exactly what it read), h and y / the
+  // bf16 output in two other ring buffers (all free after the main loop)
+  const int ul = u0 - (m0 >> 2);  // this lane's first unit within the tile's 64
+  lds_char* hs = lds + ((cbuf / STAGE_BYTES + 1) % NSTAGE) * STAGE_BYTES;
+  lds_char* ys = lds + ((cbuf / STAGE_BYTES + 2) % NSTAGE) * STAGE_BYTES;
+  constexpr int HP = 80;  // int8 image pitch (64 B + 16: conflict-free 4-byte writes, 16-B aligned rows)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int n = nb + 16 * j;
-    const uint2 cv = *(const uint2*)(smem + cbuf + (n - n0) * 128 + (u0 - (m0 >> 2)) * 2);
+    const int n = nb + 16 * j, r = n - n0;
+    const uint2 cv = *(const uint2*)(smem + cbuf + r * 128 + ul * 2);
     const float cin[4] = {h2f((uint16_t)(cv.x & 0xffff)), h2f((uint16_t)(cv.x >> 16)), h2f((uint16_t)(cv.y & 0xffff)),
                           h2f((uint16_t)(cv.y >> 16))};
     uint32_t cw[2] = {0u, 0u}, hq = 0, yq = 0;
@@ -306,20 +315,43 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     asm volatile("" ::"v"(cw[0]), "v"(cw[1]), "v"(hq), "v"(yq), "v"(hv[0]));
     continue;
 #endif
-    *(uint2*)(a.c + (size_t)n * H + u0) = uint2{cw[0], cw[1]};
-    *(uint32_t*)(a.h_out + (size_t)n * H + u0) = hq;
+    *(uint2*)(smem + cbuf + r * 128 + ul * 2) = uint2{cw[0], cw[1]};
+    *(uint32_t*)(hs + r * HP + ul) = hq;
+    if (a.mode == ENC_OUT_FINAL) {
+      if (a.y32) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1], hv[2], hv[3]};
+      *(uint2*)(ys + r * 128 + ul * 2) = uint2{(uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1]) << 16),
+                                               (uint32_t)f2bf_ftz(hv[2]) | ((uint32_t)f2bf_ftz(hv[3]) << 16)};
+    } else {
+      *(uint32_t*)(ys + r * HP + ul) = yq;
+    }
+  }
+#ifdef RNNT_DEV_EPI_NOSTORE
+  return;
+#endif
+  __syncthreads();
+  // copy-out: thread t moves 16-byte chunks; a wave instruction writes 8 (c, bf16 f) or 16 (h, y)
+  // whole row segments
+  const int um = m0 >> 2;
+#pragma unroll
+  for (int it = 0; it < BN * 8 / (NWAVE * 64); ++it) {  // c: BN rows x 128 B
+    const int idx = it * NWAVE * 64 + tid, r = idx >> 3, ch = idx & 7;
+    *(uint4*)(a.c + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(smem + cbuf + r * 128 + ch * 16);
+    if (a.mode == ENC_OUT_FINAL)
+      *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + r * 128 + ch * 16);
+  }
+#pragma unroll
+  for (int it = 0; it < BN * 4 / (NWAVE * 64); ++it) {  // h, y: BN rows x 64 B
+    const int idx = it * NWAVE * 64 + tid, r = idx >> 2, ch = idx & 3, n = n0 + r;
+    *(uint4*)(a.h_out + (size_t)n * H + um + ch * 16) = *(const uint4*)(hs + r * HP + ch * 16);
     if (a.mode == ENC_OUT_I8) {
-      *(uint32_t*)(a.y8 + (size_t)n * H + u0) = yq;
+      *(uint4*)(a.y8 + (size_t)n * H + um + ch * 16) = *(const uint4*)(ys + r * HP + ch * 16);
     } else if (a.mode == ENC_OUT_STACKED) {
       // StackTime (modeling_rnnt.py:314-324): frame t -> stacked frame t/2, half t%2;
       // frames t >= x_lens[n] are zeroed; the odd-T pad frame is zero too.
-      int8_t* dst = a.y8 + (size_t)n * (2 * H) + u0;
-      *(uint32_t*)(dst + a.half * H) = (a.t < a.lens[n]) ? yq : 0u;
-      if (a.zero_next) *(uint32_t*)(dst + H) = 0u;
-    } else {
-      if (a.y32) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1], hv[2], hv[3]};
-      *(uint2*)(a.fbf + (size_t)n * H + u0) = uint2{(uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1]) << 16),
-                                                      (uint32_t)f2bf_ftz(hv[2]) | ((uint32_t)f2bf_ftz(hv[3]) << 16)};
+      int8_t* dst = a.y8 + (size_t)n * (2 * H) + um + ch * 16;
+      const uint4 z = uint4{0u, 0u, 0u, 0u};
+      *(uint4*)(dst + a.half * H) = (a.t < a.lens[n]) ? *(const uint4*)(ys + r * HP + ch * 16) : z;
+      if (a.zero_next) *(uint4*)(dst + H) = z;
     }
   }
 }
