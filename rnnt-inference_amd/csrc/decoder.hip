@@ -68,6 +68,19 @@ __device__ unsigned int g_st_n;
 #define ST_FLUSH(kid, a0, a1, a2, a3)
 #endif
 
+// XCD-aware decomposition of a 1-D grid of 8 * X * Y8 workgroups into (column group x, row group
+// y < 8 * Y8): workgroup id goes to XCD id & 7 (round-robin dispatch), and all X column groups
+// of a row group run on one XCD, so a row tile's inputs are fetched into one L2 (measured before:
+// the column groups of a row tile spread over every XCD, each fetching the rows).
+struct GridXY {
+  int x, y, ny;
+};
+__device__ __forceinline__ GridXY xcd_grid(int X) {
+  const int id = blockIdx.x, t = id >> 3;
+  return GridXY{t % X, (id & 7) + 8 * (t / X), 8 * (int)(gridDim.x / (8 * X))};
+}
+static inline int xcd_grid_size(int X, int rows) { return 8 * X * ((rows + 7) / 8); }
+
 // ---------------------------------------------------------------- layer-0 input table
 // xtab[g][r] = b_ih0[r] + emb[g].W_ih0[r]^T (g < 28), xtab[28] = b_ih0 (SOS: zero embedding).
 // One workgroup per 16 gate rows; one wave per 16 labels (rows 28..31 are zero embeddings).
@@ -96,8 +109,10 @@ __global__ void __launch_bounds__(256) joint_trans_kernel(DecWeights w, const ui
                                                           float* __restrict__ F, int Npad, int nrows) {
   extern __shared__ __attribute__((aligned(16))) uint16_t Ws[];  // [64][JT_PITCH]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
-  const int j0 = blockIdx.x * 64;
-  const int row0 = blockIdx.y * JT_ROWS;
+  const GridXY gxy = xcd_grid(J / 64);
+  if (gxy.y * JT_ROWS >= nrows) return;
+  const int j0 = gxy.x * 64;
+  const int row0 = gxy.y * JT_ROWS;
   // live 16-row tiles of this wave (row = t * Npad + n valid iff t < f_lens[n])
   bool live[4];
   bool any = false;
@@ -141,8 +156,7 @@ __global__ void __launch_bounds__(256) joint_trans_kernel(DecWeights w, const ui
     const int row = row0 + wave * 64 + i * 16 + c;
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
-      *(float4*)(F + (size_t)row * J + j0 + jt * 16 + 4 * q) =
-          float4{acc[i][jt][0], acc[i][jt][1], acc[i][jt][2], acc[i][jt][3]};
+      __builtin_nontemporal_store(acc[i][jt], (v4f*)(F + (size_t)row * J + j0 + jt * 16 + 4 * q));
   }
 }
 
@@ -210,13 +224,15 @@ __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int p
   const DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
+  const GridXY gxy = xcd_grid(PG4 / (16 * (PRED_THREADS / 64)));
   const int* list = s.list + parity * a.Npad;
-  // the first tile's entries load beside the list length (the grid never exceeds Npad/DEC_RT tiles)
-  const int e_first = tid < DEC_RT ? list[blockIdx.y * DEC_RT + tid] : 0;
+  // the first tile's entries load beside the list length (row groups never exceed Npad/DEC_RT
+  // tiles... except the XCD rounding: guarded)
+  const int e_first = (tid < DEC_RT && gxy.y * DEC_RT < a.Npad) ? list[gxy.y * DEC_RT + tid] : 0;
   const int cnt = s.count[parity];
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
-  if ((int)blockIdx.y >= ntiles) return;
-  const int t0 = (blockIdx.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
+  if (gxy.y >= ntiles) return;
+  const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
   uint4 wh[NT][P / 32], wx[NT][LAYER ? P / 32 : 1];
   float4 bh[NT], bx[NT];
 #pragma unroll
@@ -231,9 +247,9 @@ __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int p
     }
     bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
   }
-  for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
+  for (int rt = gxy.y; rt < ntiles; rt += gxy.ny) {
     if (tid < DEC_RT) {
-      const int e = rt == (int)blockIdx.y ? e_first : list[rt * DEC_RT + tid];
+      const int e = rt == gxy.y ? e_first : list[rt * DEC_RT + tid];
       ents[tid] = rt * DEC_RT + tid < cnt ? e : -1;
     }
     __syncthreads();
@@ -312,29 +328,30 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
-  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) {
+  const GridXY gxy = xcd_grid(J / (16 * (G_THREADS / 64)));
+  if (blockIdx.x == 0 && tid == 0) {
     s.count[parity ^ 1] = 0;
     s.count[2 + (parity ^ 1)] = 0;
   }
   const int* list = s.list + parity * a.Npad;
-  const int e_first = tid < DEC_RT ? list[blockIdx.y * DEC_RT + tid] : 0;
+  const int e_first = (tid < DEC_RT && gxy.y * DEC_RT < a.Npad) ? list[gxy.y * DEC_RT + tid] : 0;
   const int cnt = s.count[parity];
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
-  if ((int)blockIdx.y >= ntiles) return;
+  if (gxy.y >= ntiles) return;
   constexpr int NJ = 1;  // column tiles per wave
   uint4 wv[NJ][P / 32];
   float4 b0[NJ];
 #pragma unroll
   for (int jj = 0; jj < NJ; ++jj) {
-    const int jt = (blockIdx.x * (G_THREADS / 64) + wave) * NJ + jj;
+    const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
     const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
     b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
   }
-  for (int rt = blockIdx.y; rt < ntiles; rt += gridDim.y) {
+  for (int rt = gxy.y; rt < ntiles; rt += gxy.ny) {
     if (tid < DEC_RT) {
-      const int e = rt == (int)blockIdx.y ? e_first : list[rt * DEC_RT + tid];
+      const int e = rt == gxy.y ? e_first : list[rt * DEC_RT + tid];
       ents[tid] = rt * DEC_RT + tid < cnt ? e : -1;
     }
     __syncthreads();
@@ -360,7 +377,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
         v4f acc = v4f{b0[jj].x, b0[jj].y, b0[jj].z, b0[jj].w};
 #pragma unroll
         for (int b = 0; b < P / 32; ++b) acc = mfma_bf16(wv[jj][b], *(const uint4*)(xr + 32 * b), acc);
-        const int jt = (blockIdx.x * (G_THREADS / 64) + wave) * NJ + jj;
+        const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
         if (ec >= 0)
           *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
       }
@@ -439,7 +456,8 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           float y[8];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            const float4 f4 = *(const float4*)(fr + 4 * h);
+            const v4f f4v = __builtin_nontemporal_load((const v4f*)(fr + 4 * h));  // streamed once
+            const float4 f4 = float4{f4v[0], f4v[1], f4v[2], f4v[3]};
             const float4 g4 = *(const float4*)(gr + 4 * h);
             const float s0 = f4.x + g4.x, s1 = f4.y + g4.y, s2 = f4.z + g4.z, s3 = f4.w + g4.w;
             y[4 * h + 0] = bf_round_ftz(s0 > 0.0f ? s0 : 0.0f);
@@ -537,11 +555,12 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_joint = lt1 < JOINT_GROUPS ? lt1 : JOINT_GROUPS;
     for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      hipLaunchKernelGGL(dec_pred_kernel<0>, dim3(PG4 / (16 * (PRED_THREADS / 64)), rg_pred), dim3(PRED_THREADS), 0, st,
-                         a, p);
-      hipLaunchKernelGGL(dec_pred_kernel<1>, dim3(PG4 / (16 * (PRED_THREADS / 64)), rg_pred), dim3(PRED_THREADS), 0, st,
-                         a, p);
-      hipLaunchKernelGGL(dec_g_kernel, dim3(J / (16 * (G_THREADS / 64)), rg_g), dim3(G_THREADS), 0, st, a, p);
+      hipLaunchKernelGGL(dec_pred_kernel<0>, dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                         dim3(PRED_THREADS), 0, st, a, p);
+      hipLaunchKernelGGL(dec_pred_kernel<1>, dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                         dim3(PRED_THREADS), 0, st, a, p);
+      hipLaunchKernelGGL(dec_g_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), rg_g)), dim3(G_THREADS), 0, st, a,
+                         p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
     }
     // poll the live-row counter one chunk behind, so the host never drains the queue
@@ -572,8 +591,8 @@ int launch_joint_trans(const DecWeights& w, const uint16_t* fbf, const int32_t* 
     attr = true;
   }
   const int nrows = Tp * Npad;
-  hipLaunchKernelGGL(joint_trans_kernel, dim3(J / 64, (nrows + JT_ROWS - 1) / JT_ROWS), dim3(256), smem, st, w, fbf,
-                     f_lens, F, Npad, nrows);
+  hipLaunchKernelGGL(joint_trans_kernel, dim3(xcd_grid_size(J / 64, (nrows + JT_ROWS - 1) / JT_ROWS)), dim3(256), smem,
+                     st, w, fbf, f_lens, F, Npad, nrows);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -53,6 +53,9 @@ constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-
 #ifndef RNNT_STAGGER
 #define RNNT_STAGGER 1
 #endif
+#ifndef RNNT_READAHEAD  // 1: fragments of the next k step read during this step's MFMAs
+#define RNNT_READAHEAD 0
+#endif
 #ifndef RNNT_PRIO_MODE  // 0: MFMA clusters at priority 1; 1: + late waves at 1 throughout; 2: static, late waves only
 #define RNNT_PRIO_MODE 0
 #endif
@@ -183,6 +186,52 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // column lane>>4; +16 rows is +1 KiB in the image (the swizzle repeats every 16 rows)
   const int fa = swz(wm * 64 + col, q), fb = A_BYTES + swz(wn * 128 + col, q);
 
+#if RNNT_READAHEAD
+  // Read-ahead main loop: the fragments of stage ks+1 are read from LDS while the MFMAs of stage
+  // ks run on fragments already in registers, so no wave waits on an LDS burst after the
+  // per-step barrier.  Stage j is read during step j-1 and consumed in step j; the barrier at
+  // the top of step ks (after this wave's DMA of stage ks+1 has landed) certifies every wave's
+  // reads of stage ks-1 done, so stage ks+NSTAGE-1 is DMA'd into that buffer; two stages stay in
+  // flight.  The cell state goes into the buffer of stage nK-NSTAGE at step nK-NSTAGE+1 as before.
+  static_assert(NSTAGE == 4, "read-ahead ring: 1 being read, 2 in flight, 1 being refilled");
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
+  stage_barrier_n((NSTAGE - 2) * GLDS_PER_STAGE);  // stage 0 landed everywhere
+  v4i fra[4], frb[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(smem + fa + i * 1024);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(smem + fb + j * 1024);
+  for (int ks = 0; ks < nK; ++ks) {
+    const bool more = ks + 1 < nK;
+    const int8_t* st = smem + ((ks + 1) % NSTAGE) * STAGE_BYTES;
+    v4i fna[4];
+    if (more) {
+      // stage ks+1 landed: this wave may leave stage ks+2 (if issued) and the cell-state pieces
+      // (issued at step nK-NSTAGE+1) in flight
+      const int later = ks + 2 < nK ? 1 : 0;
+      stage_barrier_n(later * GLDS_PER_STAGE + (ks >= nK - NSTAGE + 2 ? C_GLDS : 0));
+      if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
+      else if (ks + NSTAGE - 1 == nK) issue_c();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fna[i] = *(const v4i*)(st + fa + i * 1024);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    // column-major MFMA order: once B fragment j has fed its 4 MFMAs its registers take the next
+    // stage's fragment j (register budget: 128 accumulators + 16 A + 16 next-A + 32 B)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+      if (more) frb[j] = *(const v4i*)(st + fb + j * 1024);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fra[i] = fna[i];
+    }
+  }
+#else
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
 #if RNNT_PRIO_MODE != 0
@@ -262,6 +311,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #endif
 #endif
   }
+#endif
 #if RNNT_PRIO_MODE != 0
   __builtin_amdgcn_s_setprio(0);
 #endif

@@ -39,6 +39,9 @@ for v in "$@"; do
     noload) build noload -DRNNT_DEV_NO_LOAD ;;
     ji1) build ji1 -DRNNT_JOINT_ITERS=1 ;;
     stamps) build stamps -DRNNT_DEV_STAMPS ;;
+    ra) build ra -DRNNT_READAHEAD=1 ;;
+    ra_noepi) build ra_noepi -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_EPI ;;
+    ra_noload) build ra_noload -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_LOAD ;;
     rt64) build rt64 -DRNNT_DEC_RT=64 ;;
     ji3) build ji3 -DRNNT_JOINT_ITERS=3 ;;
     ji6) build ji6 -DRNNT_JOINT_ITERS=6 ;;
