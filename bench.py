@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--decode-priority", type=int, default=0,
                     help="run each engine's decode on a separate stream of this priority (torch: lower = higher; "
                          "0 = decode on the encode stream)")
+    ap.add_argument("--enc-concurrency", type=int, default=1,
+                    help="encoders allowed on the GPU at once (1: encoders take turns, each batch's decode beside "
+                         "the next encoder; 2+: the next encoder also fills the CUs a finishing encoder's short "
+                         "length-sorted tail ticks leave idle)")
     ap.add_argument("--enc-reserve", type=int, default=0,
                     help="CUs per XCD kept off the encoder streams (CU-masked HIP streams, rnnt_stream_create); "
                          "each engine's decode then runs on its own unrestricted stream and always finds free CUs")
@@ -175,7 +179,7 @@ def make_batches(qsl, query, batch, sizes=None):
     return out
 
 
-def run_step(engines, streams, batches, featurizers=None, store=None, dec_streams=None):
+def run_step(engines, streams, batches, featurizers=None, store=None, dec_streams=None, enc_concurrency=1):
     """One Offline query.  Batch i runs on engine i % inflight, each engine with its own HIP
     stream and host thread (ctypes releases the GIL).  Encoders take turns (a lock held until
     the encode has finished on the GPU), so each batch's latency-bound greedy decode overlaps
@@ -183,7 +187,7 @@ def run_step(engines, streams, batches, featurizers=None, store=None, dec_stream
     are gathered to the host."""
     import threading
     k = len(engines)
-    enc_lock = threading.Lock()
+    enc_lock = threading.Semaphore(enc_concurrency)
 
     def worker(j):
         for b in batches[j::k]:
@@ -322,7 +326,7 @@ def main():
         b["rl"] = torch.empty(b["n"], dtype=torch.int32, device="cuda")
 
     for _ in range(args.warmup):
-        run_step(engines, streams, batches, fzs, store, dec_streams)
+        run_step(engines, streams, batches, fzs, store, dec_streams, args.enc_concurrency)
     torch.cuda.synchronize()
     for e in engines:  # HIP events around every encode / joint_trans / greedy call, on its stream
         e.set_profiling(True)
@@ -330,7 +334,7 @@ def main():
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lens_out, _ = run_step(engines, streams, batches, fzs, store, dec_streams)
+        lens_out, _ = run_step(engines, streams, batches, fzs, store, dec_streams, args.enc_concurrency)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
@@ -380,7 +384,7 @@ def main():
                  else "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)"),
         "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
                    "qsl_per_gpu": args.qsl, "query_samples_per_gpu": args.query, "batch_size": args.batch,
-                   "batches_in_flight": args.inflight,
+                   "batches_in_flight": args.inflight, "encoder_concurrency": args.enc_concurrency,
                    "encoder_cu_reserve_per_xcd": args.enc_reserve, "decode_cus_per_xcd": args.dec_cus or 32,
                    "input": ("16 kHz audio: GPU featurizer (FilterbankFeatures.forward) in the timed region" if args.wav
                              else "log-mel features resident in HBM"),

@@ -106,6 +106,9 @@ __device__ __forceinline__ void stage_barrier_n(int n) {
   }
 }
 
+// byte offset of (row r, byte b < 128) in a swizzled [rows][128 B] epilogue image
+__device__ __forceinline__ int cimg_off(int r, int b) { return r * 128 + ((((b >> 4) ^ r) & 7) << 4) + (b & 15); }
+
 __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
@@ -167,7 +170,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // nK-NSTAGE once it has been read; piece p, lane l: row 8p + (l>>3), 16-B chunk l&7
   const int cbuf = ((nK - NSTAGE) % NSTAGE) * STAGE_BYTES;
   auto issue_c = [&]() __attribute__((always_inline)) {
-    const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + (lane & 7) * 8;
+    // image row r holds logical 16-B chunk ch at chunk slot ch ^ (r & 7) (cimg_off), so the
+    // epilogue's per-lane 8-byte accesses of 16 consecutive rows hit 2-way instead of 8-way
+    // bank conflicts; lane l of piece p lands in slot l & 7 of row 8p + (l >> 3)
+    const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
 #pragma unroll
     for (int pc = 0; pc < C_GLDS; ++pc) {
       const int p = wave * C_GLDS + pc;
@@ -347,7 +353,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int n = nb + 16 * j, r = n - n0;
-    const uint2 cv = *(const uint2*)(smem + cbuf + r * 128 + ul * 2);
+    const uint2 cv = *(const uint2*)(smem + cbuf + cimg_off(r, ul * 2));
     const float cin[4] = {h2f((uint16_t)(cv.x & 0xffff)), h2f((uint16_t)(cv.x >> 16)), h2f((uint16_t)(cv.y & 0xffff)),
                           h2f((uint16_t)(cv.y >> 16))};
     uint32_t cw[2] = {0u, 0u}, hq = 0, yq = 0;
@@ -365,11 +371,11 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     asm volatile("" ::"v"(cw[0]), "v"(cw[1]), "v"(hq), "v"(yq), "v"(hv[0]));
     continue;
 #endif
-    *(uint2*)(smem + cbuf + r * 128 + ul * 2) = uint2{cw[0], cw[1]};
+    *(uint2*)(smem + cbuf + cimg_off(r, ul * 2)) = uint2{cw[0], cw[1]};
     *(uint32_t*)(hs + r * HP + ul) = hq;
     if (a.mode == ENC_OUT_FINAL) {
       if (a.y32) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1], hv[2], hv[3]};
-      *(uint2*)(ys + r * 128 + ul * 2) = uint2{(uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1]) << 16),
+      *(uint2*)(ys + cimg_off(r, ul * 2)) = uint2{(uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1]) << 16),
                                                (uint32_t)f2bf_ftz(hv[2]) | ((uint32_t)f2bf_ftz(hv[3]) << 16)};
     } else {
       *(uint32_t*)(ys + r * HP + ul) = yq;
@@ -385,9 +391,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #pragma unroll
   for (int it = 0; it < BN * 8 / (NWAVE * 64); ++it) {  // c: BN rows x 128 B
     const int idx = it * NWAVE * 64 + tid, r = idx >> 3, ch = idx & 7;
-    *(uint4*)(a.c + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(smem + cbuf + r * 128 + ch * 16);
+    *(uint4*)(a.c + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(smem + cbuf + cimg_off(r, ch * 16));
     if (a.mode == ENC_OUT_FINAL)
-      *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + r * 128 + ch * 16);
+      *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + cimg_off(r, ch * 16));
   }
 #pragma unroll
   for (int it = 0; it < BN * 4 / (NWAVE * 64); ++it) {  // h, y: BN rows x 64 B
