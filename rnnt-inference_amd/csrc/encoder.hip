@@ -56,6 +56,9 @@ constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-
 #ifndef RNNT_READAHEAD  // 1: fragments of the next k step read during this step's MFMAs
 #define RNNT_READAHEAD 0
 #endif
+#ifndef RNNT_PINGPONG  // 1: the two wave groups alternate memory and MFMA phases (see the main loop)
+#define RNNT_PINGPONG 0
+#endif
 #ifndef RNNT_PRIO_MODE  // 0: MFMA clusters at priority 1; 1: + late waves at 1 throughout; 2: static, late waves only
 #define RNNT_PRIO_MODE 0
 #endif
@@ -192,7 +195,62 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // column lane>>4; +16 rows is +1 KiB in the image (the swizzle repeats every 16 rows)
   const int fa = swz(wm * 64 + col, q), fb = A_BYTES + swz(wn * 128 + col, q);
 
-#if RNNT_READAHEAD
+#if RNNT_PINGPONG
+  // Ping-pong main loop: waves 0-3 (group A) and 4-7 (group B, one per SIMD beside an A wave)
+  // run offset by one phase.  A wave alternates a memory phase (read k step ks's fragments from
+  // LDS, issue its LDS-DMA pieces of stage ks+3, retire the reads) and an MFMA phase (32 MFMAs
+  // on those fragments); with B one phase behind, every SIMD always has one wave in an MFMA
+  // phase while its partner does the memory work.  One raw barrier per phase.  Ordering (stage
+  // s in ring buffer s % 4): A reads stage s in phase 2s, B in 2s+1; A waits for its pieces of
+  // stage s in its MFMA phase 2s-1, B in its memory phase 2s-1, both before the barrier ending
+  // that phase (RAW).  Stage s+3 goes into the buffer of stage s-1 in phases 2s (A) / 2s+1 (B),
+  // after both groups retired their reads of it (lgkmcnt(0) before the barriers ending phases
+  // 2s-2 / 2s-1: WAR).  The cell state goes into the buffer of stage nK-4 as before.
+  static_assert(NSTAGE == 4, "ping-pong ring: stage s+3 refills the buffer of stage s-1");
+  auto vm_wait = [&](int n) __attribute__((always_inline)) {
+    switch (n) {
+#define RNNT_VW(v) \
+  case v: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(v) : "memory"); break;
+      RNNT_VW(0) RNNT_VW(4) RNNT_VW(8) RNNT_VW(12) RNNT_VW(16)
+#undef RNNT_VW
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  };
+  static_assert(GLDS_PER_STAGE == 4 && C_GLDS == 4, "vm_wait immediates");
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s) issue(s);
+  stage_barrier<2 * GLDS_PER_STAGE>();  // stage 0 landed for every wave
+  const int grp = wn;
+  v4i fra[4], frb[8];
+  for (int ph = 0; ph <= 2 * nK; ++ph) {
+    const int lp = ph - grp;
+    if (lp >= 0 && lp < 2 * nK) {
+      const int ks = lp >> 1;
+      if ((lp & 1) == 0) {  // memory phase of k step ks
+        if (grp == 1 && ks + 1 < nK)  // stage ks+1 landed (A reads it next phase)
+          vm_wait((ks + 2 < nK ? GLDS_PER_STAGE : 0) + (ks > nK - NSTAGE + 1 ? C_GLDS : 0));
+        const int8_t* st = smem + (ks % NSTAGE) * STAGE_BYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa + i * 1024);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb + j * 1024);
+        if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
+        else if (ks + NSTAGE - 1 == nK) issue_c();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {  // MFMA phase of k step ks
+        if (grp == 0 && ks + 1 < nK)  // stage ks+1 landed (read next phase)
+          vm_wait(((ks + 2 < nK) + (ks + 3 < nK)) * GLDS_PER_STAGE + (ks >= nK - NSTAGE + 1 ? C_GLDS : 0));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    asm volatile("s_barrier" ::: "memory");
+  }
+#elif RNNT_READAHEAD
   // Read-ahead main loop: the fragments of stage ks+1 are read from LDS while the MFMAs of stage
   // ks run on fragments already in registers, so no wave waits on an LDS burst after the
   // per-step barrier.  Stage j is read during step j-1 and consumed in step j; the barrier at

@@ -40,6 +40,8 @@ for v in "$@"; do
     ji1) build ji1 -DRNNT_JOINT_ITERS=1 ;;
     stamps) build stamps -DRNNT_DEV_STAMPS ;;
     ra) build ra -DRNNT_READAHEAD=1 ;;
+    pp) build pp -DRNNT_PINGPONG=1 ;;
+    pp_noepi) build pp_noepi -DRNNT_PINGPONG=1 -DRNNT_DEV_NO_EPI ;;
     ra_noepi) build ra_noepi -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_EPI ;;
     ra_noload) build ra_noload -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_LOAD ;;
     rt64) build rt64 -DRNNT_DEC_RT=64 ;;
