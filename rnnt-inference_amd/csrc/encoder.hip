@@ -56,6 +56,9 @@ constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-
 #ifndef RNNT_READAHEAD  // 1: fragments of the next k step read during this step's MFMAs
 #define RNNT_READAHEAD 0
 #endif
+#ifndef RNNT_PHASES  // 2: two barrier-bracketed MFMA phases per k step (see the main loop)
+#define RNNT_PHASES 0
+#endif
 #ifndef RNNT_PINGPONG  // 1: the two wave groups alternate memory and MFMA phases (see the main loop)
 #define RNNT_PINGPONG 0
 #endif
@@ -72,8 +75,14 @@ constexpr int APW = (BM / 16) / NWAVE;       // 16-row A pieces (1 KiB LDS-DMA e
 constexpr int BPW = (BN / 16) / NWAVE;       // B pieces per wave: 2
 constexpr int GLDS_PER_STAGE = APW + BPW;
 constexpr int C_GLDS = (BN * 128 / 1024) / NWAVE;  // cell-state DMA pieces per wave: 4
+#ifndef RNNT_TAB_COPIES  // sigma-table copies in LDS: 16 = one per 16-byte bank slot
+#define RNNT_TAB_COPIES 1
+#endif
+constexpr int TAB_COPIES = RNNT_TAB_COPIES;
 constexpr int TAB_OFF = NSTAGE * STAGE_BYTES;   // LDS: sigma table after the ring
-constexpr int SMEM_BYTES = TAB_OFF + 128 * 16;
+constexpr int SMEM_BYTES = TAB_OFF + 128 * 16 * TAB_COPIES;
+static_assert(TAB_COPIES == 1 || TAB_COPIES == 16, "table copies");
+static_assert(SMEM_BYTES <= 160 * 1024, "LDS");
 static_assert(BPW == 2 && (APW == 2 || APW == 4) && C_GLDS == 4, "staging split");
 static_assert(BN * 128 <= STAGE_BYTES, "the cell-state image fits one ring buffer");
 static_assert(NSTAGE >= 3 && BN * 80 <= STAGE_BYTES, "the epilogue's h / y images fit two other ring buffers");
@@ -295,6 +304,71 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       for (int i = 0; i < 4; ++i) fra[i] = fna[i];
     }
   }
+#elif RNNT_PHASES == 2
+  // Two barrier-bracketed phases per k step (the guide's 8-phase GEMM structure at this tile):
+  // each phase reads its fragments and issues half of this wave's pieces of stage ks+3, meets
+  // the other waves at a barrier, retires its reads and runs 16 MFMAs, and closes with a
+  // barrier, so every wave's MFMA cluster runs while the others' are running.  Stage ks+3
+  // refills the buffer of stage ks-1 (all reads of it retired before the barriers closing step
+  // ks-1); phase B waits for this wave's pieces of stage ks+1, so after its closing barrier
+  // stage ks+1 has landed everywhere.  The cell state goes into stage nK-4's buffer at ks = nK-3.
+  static_assert(NSTAGE == 4 && GLDS_PER_STAGE == 4 && C_GLDS == 4, "two-phase ring");
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s) issue(s);
+  stage_barrier<2 * GLDS_PER_STAGE>();  // stage 0 landed for every wave
+  for (int ks = 0; ks < nK; ++ks) {
+    const int8_t* st = smem + (ks % NSTAGE) * STAGE_BYTES;
+    const int nxt = ks + NSTAGE - 1;
+    v4i fra[2], frb[8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fra[i] = *(const v4i*)(st + fa + i * 1024);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb + j * 1024);
+    if (nxt < nK) {
+      issue_piece(nxt, 0);
+      issue_piece(nxt, 1);
+    } else if (nxt == nK) {
+      issue_c();
+    }
+    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    v4i frc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) frc[i] = *(const v4i*)(st + fa + (i + 2) * 1024);
+    if (nxt < nK) {
+      issue_piece(nxt, 2);
+      issue_piece(nxt, 3);
+    }
+    if (ks + 1 < nK) {
+      // pieces issued after stage ks+1's: stages ks+2, ks+3 (when they exist) and the cell state
+      const int n = 4 * (ks + 2 < nK) + 4 * (ks + 3 < nK) + 4 * (ks >= nK - 3);
+      if (n == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (n == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i + 2][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(frc[i], frb[j], acc[i + 2][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #else
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
@@ -390,7 +464,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 
   // ---- fused LSTM cell epilogue (quant_lstm.py:162-183 semantics; oracle_enc_cell)
   const float As = a.rb * 4.0f, Ag = a.rb * 8.0f, ins = a.in_s, outs = a.out_s;
-  const float4* tab = (const float4*)(smem + TAB_OFF);
+  // table lookups are random gathers: with 16 copies, entry k of copy s at slot 16k + s, lane l
+  // reads copy l & 15, so the 16 lanes of each ds_read_b128 lane group ({0-3,12-15,20-27}, ...)
+  // sit on 16 distinct bank slots whatever entries they pick (no bank conflicts)
+  const float4* tab = (const float4*)(smem + TAB_OFF) + (TAB_COPIES == 16 ? (lane & 15) : 0);
   float4 bq[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -419,7 +496,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float cn, hh;
-      enc_cell(tab, acc[i][j], bq[i], As, Ag, cin[i], cn, hh);
+      enc_cell<TAB_COPIES>(tab, acc[i][j], bq[i], As, Ag, cin[i], cn, hh);
       cw[i >> 1] |= (uint32_t)f2h(cn) << (16 * (i & 1));
       hv[i] = hh;
       hq |= (uint32_t)(uint8_t)q8(hh * ins) << (8 * i);
@@ -484,7 +561,13 @@ constexpr int SLOTS_PER_XCD = 32 * WG_PER_CU;  // resident workgroups per XCD (3
 __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(EncTickArgs args) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   const int xcd = blockIdx.x & 7, gg = xcd & 3, bg = xcd >> 2;
-  if (threadIdx.x < 128) ((float4*)(smem + TAB_OFF))[threadIdx.x] = g_act_tab[threadIdx.x];  // read after the
+#pragma unroll
+  for (int it = 0; it < 128 * TAB_COPIES / (NWAVE * 64); ++it) {
+    const int idx = it * NWAVE * 64 + threadIdx.x;
+    ((float4*)(smem + TAB_OFF))[idx] = g_act_tab[TAB_COPIES == 16 ? idx >> 4 : idx];
+  }
+  if (128 * TAB_COPIES < NWAVE * 64 && threadIdx.x < 128 * TAB_COPIES)
+    ((float4*)(smem + TAB_OFF))[threadIdx.x] = g_act_tab[TAB_COPIES == 16 ? threadIdx.x >> 4 : threadIdx.x];  // read after the
   // first stage barrier of the main loop (lgkmcnt(0) + s_barrier)
   // RNNT_PERSIST: workgroup (xcd, slot) takes the XCD's tiles slot, slot + SLOTS_PER_XCD, ... in
   // the order one-tile-per-workgroup rounds would run them (a layer-step 4 % shorter alone, but

@@ -57,7 +57,9 @@ __device__ __forceinline__ float det_tanh(float x) {
 // ---- int8 encoder cell (bit-identical to oracle_act_sig_t / oracle_enc_cell, where the
 // contract is documented): sigma from a 128-interval piecewise-cubic table held in LDS
 // (float4 per interval), indexed by t = 4x + 64; tanh(x) = 2 sigma(2x) - 1; the
-// dequantisation folded into the index, t = fma((float)acc, A, B).
+// dequantisation folded into the index, t = fma((float)acc, A, B).  STRIDE: entry k sits at
+// tab[k * STRIDE] (the encoder keeps 16 interleaved copies, one per 16-byte LDS bank slot).
+template <int STRIDE = 1>
 __device__ __forceinline__ float act_sig_t(const float4* __restrict__ tab, float t) {
   t = __builtin_fminf(__builtin_fmaxf(t, 0.0f), 127.99998f);
   const int k = (int)t;
@@ -65,24 +67,25 @@ __device__ __forceinline__ float act_sig_t(const float4* __restrict__ tab, float
 #ifdef RNNT_DEV_NO_TAB  // development ablation: no LDS lookup
   const float4 c = float4{t * 0.001f, (float)k, 0.5f, 0.25f};
 #else
-  const float4 c = tab[k];
+  const float4 c = tab[k * STRIDE];
 #endif
   return __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c.w, fr, c.z), fr, c.y), fr, c.x);
 }
 // acc: int32 gate sums (i, f, g, o); B: packed per-gate bias terms (oracle_enc_bias);
 // As = 4 rb, Ag = 8 rb.  Returns c (fp32) and h.
+template <int STRIDE = 1>
 __device__ __forceinline__ void enc_cell(const float4* __restrict__ tab, const v4i acc, const float4 B, float As,
                                          float Ag, float c_prev, float& c_out, float& h_out) {
-  const float ig = act_sig_t(tab, __builtin_fmaf((float)acc[0], As, B.x));
-  const float fg = act_sig_t(tab, __builtin_fmaf((float)acc[1], As, B.y));
-  const float gg = __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf((float)acc[2], Ag, B.z)), -1.0f);
-  const float og = act_sig_t(tab, __builtin_fmaf((float)acc[3], As, B.w));
+  const float ig = act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[0], As, B.x));
+  const float fg = act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[1], As, B.y));
+  const float gg = __builtin_fmaf(2.0f, act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[2], Ag, B.z)), -1.0f);
+  const float og = act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[3], As, B.w));
   float c = __builtin_fmaf(fg, c_prev, ig * gg);
   // opaque here: otherwise the backend folds fma + the later f32->f16 store conversion into
   // v_fma_mixlo_f16 (one rounding straight to f16), which is not the contract's fp32 c
   // rounded to fp16
   asm volatile("" : "+v"(c));
-  const float tc = __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf(c, 8.0f, 64.0f)), -1.0f);
+  const float tc = __builtin_fmaf(2.0f, act_sig_t<STRIDE>(tab, __builtin_fmaf(c, 8.0f, 64.0f)), -1.0f);
   c_out = c;
   h_out = og * tc;
 }

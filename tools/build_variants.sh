@@ -41,6 +41,9 @@ for v in "$@"; do
     stamps) build stamps -DRNNT_DEV_STAMPS ;;
     ra) build ra -DRNNT_READAHEAD=1 ;;
     pp) build pp -DRNNT_PINGPONG=1 ;;
+    ph2) build ph2 -DRNNT_PHASES=2 ;;
+    tab16) build tab16 -DRNNT_TAB_COPIES=16 ;;
+    ph2_noepi) build ph2_noepi -DRNNT_PHASES=2 -DRNNT_DEV_NO_EPI ;;
     pp_noepi) build pp_noepi -DRNNT_PINGPONG=1 -DRNNT_DEV_NO_EPI ;;
     ra_noepi) build ra_noepi -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_EPI ;;
     ra_noload) build ra_noload -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_LOAD ;;
