@@ -21,6 +21,18 @@ __device__ const float4 g_act_tab[128] = {
 #include "act_table.inc"
 };
 
+// development instrumentation (-DRNNT_DEV_STAMPS, tools/enc_stamps.py): thread 0 of every tile
+// records s_memrealtime (100 MHz) at workgroup start, once stage 0 has landed, after the main
+// loop and after the epilogue, with the tile and the CU it ran on.
+#ifdef RNNT_DEV_STAMPS
+__device__ unsigned long long g_est[1 << 22];
+__device__ unsigned int g_est_n;
+#define EST_MARK(v) v = threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull
+#define EST_CLK(v) v = threadIdx.x == 0 ? __builtin_amdgcn_s_memtime() : 0ull
+#else
+#define EST_MARK(v)
+#endif
+
 // ---------------------------------------------------------------- feature quantisation
 // x_q = q8(x * in_scale[0]) over [T][Npad][256] (layer-0 input quantizer, calibrated on
 // cat([x, h]); quant_modules.py:118-121).
@@ -55,6 +67,12 @@ constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-
 #endif
 #ifndef RNNT_READAHEAD  // 1: fragments of the next k step read during this step's MFMAs
 #define RNNT_READAHEAD 0
+#endif
+#ifndef RNNT_BK128  // 1: 128-byte-row stages, two buffers (see the main loop); 0: 64-byte stages, 4 buffers
+#define RNNT_BK128 (ENC_WN == 2)
+#endif
+#ifndef RNNT_BK128_ISSUE  // 128-byte stages: 0 all pieces at the stage top; 1 waves 4-7 mid-stage; 2 A top, B mid
+#define RNNT_BK128_ISSUE 2
 #endif
 #ifndef RNNT_PHASES  // 2: two barrier-bracketed MFMA phases per k step (see the main loop)
 #define RNNT_PHASES 0
@@ -121,7 +139,10 @@ __device__ __forceinline__ void stage_barrier_n(int n) {
 // byte offset of (row r, byte b < 128) in a swizzled [rows][128 B] epilogue image
 __device__ __forceinline__ int cimg_off(int r, int b) { return r * 128 + ((((b >> 4) ^ r) & 7) << 4) + (b & 15); }
 
-__device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem) {
+__device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem,
+                                             unsigned long long st_t0 = 0ull) {
+  unsigned long long st_t1 = 0ull, st_t2 = 0ull, st_c1 = 0ull, st_c2 = 0ull;
+  (void)st_t0; (void)st_t1; (void)st_t2; (void)st_c1; (void)st_c2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
   const int m0 = mt * BM;  // packed gate row base
@@ -180,7 +201,14 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 
   // the tile's fp16 cell state (BN rows x 64 units x 2 B) DMA'd into the ring buffer of stage
   // nK-NSTAGE once it has been read; piece p, lane l: row 8p + (l>>3), 16-B chunk l&7
+#if RNNT_BK128
+  // two 64 KiB stages of 128-byte rows; the cell state goes into the buffer the last stage does
+  // not occupy (stage nS-2's, issued once that stage's reads are retired)
+  const int nS = K / 128;
+  const int cbuf = (nS & 1) * 65536;
+#else
   const int cbuf = ((nK - NSTAGE) % NSTAGE) * STAGE_BYTES;
+#endif
   auto issue_c = [&]() __attribute__((always_inline)) {
     // image row r holds logical 16-B chunk ch at chunk slot ch ^ (r & 7) (cimg_off), so the
     // epilogue's per-lane 8-byte accesses of 16 consecutive rows hit 2-way instead of 8-way
@@ -203,8 +231,106 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // fragment reads: A rows wm*64 + i*16 + (lane&15), B rows wn*128 + j*16 + (lane&15), 16-byte
   // column lane>>4; +16 rows is +1 KiB in the image (the swizzle repeats every 16 rows)
   const int fa = swz(wm * 64 + col, q), fb = A_BYTES + swz(wn * 128 + col, q);
+  (void)nK; (void)fa; (void)fb; (void)issue;  // the 64-byte-stage loops' helpers (unused with RNNT_BK128)
 
-#if RNNT_PINGPONG
+#if RNNT_BK128
+  // 128-byte staging: a stage holds two MFMA k steps (K bytes k0..k0+127) of all 256 A and 256 B
+  // rows, so each LDS-DMA piece moves 8 whole 128-byte rows (8 full cache lines) instead of 16
+  // half lines -- half the address/tag work per byte on the load path.  Image: 16-byte column c
+  // of row r at slot c ^ ((r >> 1) & 7) (rows of 128 B, two per 256-byte bank row): conflict-free
+  // for the ds_read_b128 lane groups.  Two buffers: stage s+1 is DMA'd while stage s is consumed.
+  static_assert(BM == 256 && BN == 256 && NWAVE == 8, "128-byte staging layout");
+  {
+    const int r8 = lane >> 3;                                   // row within a piece
+    const int sl = lane & 7;                                    // 16-byte slot within the row
+    const int gc0 = (sl ^ ((r8 >> 1) & 7)) * 16;                // even pieces: rows 8p + r8, p even
+    const int gc1 = (sl ^ (((8 + r8) >> 1) & 7)) * 16;          // odd pieces
+    // per-lane 32-bit offsets (even / odd pieces differ in the swizzle) from SGPR tile bases
+    const uint32_t rl = (uint32_t)(32 * wave + r8);
+    const uint32_t oA0 = rl * K + gc0, oA1 = rl * K + gc1;
+    const uint32_t oX0 = rl * a.I + gc0, oX1 = rl * a.I + gc1;
+    const uint32_t oH0 = rl * H + gc0, oH1 = rl * H + gc1;
+    auto issue128A = [&](int s) __attribute__((always_inline)) {
+      const int k = s * 128;
+      lds_char* st = lds + (s & 1) * 65536 + wave * 4096;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // A pieces 4w..4w+3: rows 32w + 8j + r8
+        __builtin_amdgcn_global_load_lds((glb_void*)(wbase + (size_t)(8 * j) * K + k + ((j & 1) ? oA1 : oA0)),
+                                         (lds_void*)(st + j * 1024), 16, 0, 0);
+    };
+    auto issue128B = [&](int s) __attribute__((always_inline)) {
+      const int k = s * 128;
+      lds_char* st = lds + (s & 1) * 65536 + wave * 4096;
+      if (k < a.I) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_global_load_lds((glb_void*)(xbase0 + (size_t)(8 * j) * a.I + k + ((j & 1) ? oX1 : oX0)),
+                                           (lds_void*)(st + 32768 + j * 1024), 16, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_global_load_lds((glb_void*)(hbase0 + (size_t)(8 * j) * H + k + ((j & 1) ? oH1 : oH0)),
+                                           (lds_void*)(st + 32768 + j * 1024), 16, 0, 0);
+      }
+    };
+    auto issue128 = [&](int s) __attribute__((always_inline)) {
+      issue128A(s);
+      issue128B(s);
+    };
+    const int sw = col >> 1;  // (row >> 1) & 7 for rows 16i + col
+    const int fa0 = (wm * 64 + col) * 128, fb0 = 32768 + (wn * 128 + col) * 128;
+    // RNNT_BK128_ISSUE 2: every wave issues its A pieces of stage s+1 at the top of stage s and
+    // its B pieces after the first k step's MFMAs (the load path sees two half bursts per stage);
+    // 1: waves 4-7 issue all of theirs after the first k step; 0: all at the top
+    const bool late = RNNT_BK128_ISSUE == 1 && wn == 1;
+    issue128(0);
+    for (int s = 0; s < nS; ++s) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#ifdef RNNT_DEV_STAMPS
+      if (s == 0) {
+        EST_MARK(st_t1);
+        EST_CLK(st_c1);
+      }
+#endif
+      if (RNNT_BK128_ISSUE == 2) {
+        if (s + 1 < nS) issue128A(s + 1);
+        else issue_c();
+      } else if (!late) {
+        if (s + 1 < nS) issue128(s + 1);
+        else issue_c();
+      }
+      const int8_t* st = smem + (s & 1) * 65536;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int cs = ((kk * 4 + q) ^ sw) << 4;
+        v4i fra[4], frb[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa0 + cs + i * 2048);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb0 + cs + j * 2048);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (RNNT_BK128_ISSUE == 2 && kk == 0 && s + 1 < nS) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue128B(s + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (late && kk == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (s + 1 < nS) issue128(s + 1);
+          else issue_c();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  }
+#elif RNNT_PINGPONG
   // Ping-pong main loop: waves 0-3 (group A) and 4-7 (group B, one per SIMD beside an A wave)
   // run offset by one phase.  A wave alternates a memory phase (read k step ks's fragments from
   // LDS, issue its LDS-DMA pieces of stage ks+3, retire the reads) and an MFMA phase (32 MFMAs
@@ -381,6 +507,12 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     // cell-state pieces
     const int later = nK - 1 - ks < NSTAGE - 2 ? nK - 1 - ks : NSTAGE - 2;
     stage_barrier_n(later * GLDS_PER_STAGE + (ks > nK - NSTAGE + 1 ? C_GLDS : 0));
+#ifdef RNNT_DEV_STAMPS
+    if (ks == 0) {
+      EST_MARK(st_t1);
+      EST_CLK(st_c1);
+    }
+#endif
 #if !RNNT_INTERLEAVE
     // RNNT_STAGGER: waves 4-7 (each the SIMD partner of wave w-4) issue their pieces after half
     // of their MFMAs, so one wave of a SIMD issues LDS-DMA while its partner runs MFMAs
@@ -454,6 +586,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   __builtin_amdgcn_s_setprio(0);
 #endif
   stage_barrier<0>();  // the cell-state DMA has landed for every wave
+#ifdef RNNT_DEV_STAMPS
+  EST_MARK(st_t2);
+  EST_CLK(st_c2);
+#endif
 #ifdef RNNT_DEV_NO_EPI  // development ablation: main loop only
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -482,8 +618,13 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // c_new in place over the c_in image (each lane rewrites exactly what it read), h and y / the
   // bf16 output in two other ring buffers (all free after the main loop)
   const int ul = u0 - (m0 >> 2);  // this lane's first unit within the tile's 64
+#if RNNT_BK128
+  lds_char* hs = lds + cbuf + 32768;
+  lds_char* ys = lds + ((nS - 1) & 1) * 65536;
+#else
   lds_char* hs = lds + ((cbuf / STAGE_BYTES + 1) % NSTAGE) * STAGE_BYTES;
   lds_char* ys = lds + ((cbuf / STAGE_BYTES + 2) % NSTAGE) * STAGE_BYTES;
+#endif
   constexpr int HP = 80;  // int8 image pitch (64 B + 16: conflict-free 4-byte writes, 16-B aligned rows)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -545,6 +686,20 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       if (a.zero_next) *(uint4*)(dst + H) = z;
     }
   }
+#ifdef RNNT_DEV_STAMPS
+  if (threadIdx.x == 0) {
+    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+    const unsigned k_ = atomicAdd(&g_est_n, 1u);
+    if (k_ < (1u << 22) / 6) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+      g_est[6 * k_] = (unsigned long long)K | ((unsigned long long)mt << 16) | ((unsigned long long)nt << 24) |
+                      ((unsigned long long)hw << 32);
+      g_est[6 * k_ + 1] = (unsigned long long)(xcc & 0xff) | ((st_c2 - st_c1) << 8);  // + main-loop shader clocks
+      g_est[6 * k_ + 2] = st_t0; g_est[6 * k_ + 3] = st_t1; g_est[6 * k_ + 4] = st_t2; g_est[6 * k_ + 5] = t3;
+    }
+  }
+#endif
 }
 
 // One launch = one wavefront tick: up to 5 independent layer-steps (jobs, longest K first).
@@ -561,6 +716,8 @@ constexpr int SLOTS_PER_XCD = 32 * WG_PER_CU;  // resident workgroups per XCD (3
 __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(EncTickArgs args) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   const int xcd = blockIdx.x & 7, gg = xcd & 3, bg = xcd >> 2;
+  unsigned long long st_t0 = 0ull;
+  EST_MARK(st_t0);
 #pragma unroll
   for (int it = 0; it < 128 * TAB_COPIES / (NWAVE * 64); ++it) {
     const int idx = it * NWAVE * 64 + threadIdx.x;
@@ -590,7 +747,7 @@ __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(Enc
     if (k0 != (int)(blockIdx.x >> 3)) __syncthreads();  // the previous tile's epilogue LDS reads are done
     // wave-uniform runtime index into the kernarg segment: the job's fields stay scalar loads
     lstm_i8_step(args.job[__builtin_amdgcn_readfirstlane(jsel)], __builtin_amdgcn_readfirstlane(mt),
-                 __builtin_amdgcn_readfirstlane(nt), smem);
+                 __builtin_amdgcn_readfirstlane(nt), smem, st_t0);
   }
 }
 
@@ -621,3 +778,17 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
 }
 
 }  // namespace rnnt
+
+#ifdef RNNT_DEV_STAMPS
+// development: copy out (and reset) the tick kernel's per-tile stamp records (6 x u64 each)
+extern "C" int rnnt_dev_read_enc_stamps(unsigned long long* out, int max_records) {
+  unsigned int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(rnnt::g_est_n), sizeof(n)) != hipSuccess) return -1;
+  if (n > (1u << 22) / 6) n = (1u << 22) / 6;
+  if ((int)n > max_records) n = max_records;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_est), (size_t)n * 6 * 8) != hipSuccess) return -1;
+  const unsigned int z = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_est_n), &z, sizeof(z)) != hipSuccess) return -1;
+  return (int)n;
+}
+#endif
