@@ -160,6 +160,100 @@ __global__ void __launch_bounds__(256) joint_trans_kernel(DecWeights w, const ui
   }
 }
 
+// F as a 256 (j) x 256 (frame row) tile GEMM, staged like the encoder's tick kernel: both
+// operands DMA'd into LDS as 128-byte row segments (64 k, two MFMA k steps; 8 whole cache lines
+// per piece), two 64 KiB buffers, XOR-swizzled image (slot c ^ ((r >> 1) & 7)); 8 waves as
+// 4 (j) x 2 (rows), each 64 j x 128 rows = 4 x 8 bf16 MFMA tiles.  Same per-element chain as
+// joint_trans_kernel (bias first, natural k in 32-k instructions), so F is bit-identical.
+// Grid: the two j tiles of a row tile sit on one XCD (frame rows fetched into one L2).
+typedef __attribute__((address_space(3))) void jg_lds_void;
+typedef __attribute__((address_space(1))) void jg_glb_void;
+constexpr int JG_SMEM = 2 * 65536;
+__global__ void __launch_bounds__(512, 1) joint_trans_gemm_kernel(DecWeights w, const uint16_t* __restrict__ fbf,
+                                                                 const int32_t* __restrict__ f_lens,
+                                                                 float* __restrict__ F, int Npad, int nrt) {
+  extern __shared__ __attribute__((aligned(16))) int8_t jsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 3, wn = wave >> 2;
+  const int q = lane >> 4, col = lane & 15;
+  const int id = blockIdx.x, xcd = id & 7, rest = id >> 3;
+  const int ct = rest & 1, rt = (rest >> 1) * 8 + xcd;
+  if (rt >= nrt) return;
+  const int j0 = ct * 256, row0 = rt * 256;
+  const int t = row0 / Npad, n0 = row0 % Npad;  // Npad is a multiple of 256: one frame per tile
+  const bool my_valid = f_lens[n0 + (tid & 255)] > t;
+  if (!__syncthreads_or(my_valid)) return;
+  // ---- staging: wave w moves A (W1t) pieces 4w..4w+3 and B (frame) pieces 4w..4w+3, piece p =
+  // rows 8p..8p+7 x 128 B; lane l -> row 8p + (l >> 3), LDS slot l & 7 holding 16-B column
+  // (l & 7) ^ ((row >> 1) & 7)
+  const int r8 = lane >> 3, sl = lane & 7;
+  const uint32_t gc0 = (uint32_t)(sl ^ ((r8 >> 1) & 7)) * 16, gc1 = (uint32_t)(sl ^ (((8 + r8) >> 1) & 7)) * 16;
+  const uint32_t rl = (uint32_t)(32 * wave + r8);
+  const uint32_t o0 = rl * (H * 2) + gc0, o1 = rl * (H * 2) + gc1;  // same row pitch (2 KiB) for both operands
+  const char* abase = (const char*)(w.w1t + (size_t)j0 * H);
+  const char* bbase = (const char*)(fbf + (size_t)row0 * H);
+  auto issueA = [&](int s) __attribute__((always_inline)) {
+    int8_t* st = jsm + (s & 1) * 65536 + wave * 4096;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((jg_glb_void*)(abase + (size_t)(8 * j) * (H * 2) + s * 128 + ((j & 1) ? o1 : o0)),
+                                       (jg_lds_void*)(st + j * 1024), 16, 0, 0);
+  };
+  auto issueB = [&](int s) __attribute__((always_inline)) {
+    int8_t* st = jsm + (s & 1) * 65536 + 32768 + wave * 4096;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((jg_glb_void*)(bbase + (size_t)(8 * j) * (H * 2) + s * 128 + ((j & 1) ? o1 : o0)),
+                                       (jg_lds_void*)(st + j * 1024), 16, 0, 0);
+  };
+  v4f acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 b = *(const float4*)(w.bt + j0 + wm * 64 + i * 16 + 4 * q);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) acc[i][jj] = v4f{b.x, b.y, b.z, b.w};
+  }
+  const int sw = col >> 1;
+  const int fa0 = (wm * 64 + col) * 128, fb0 = 32768 + (wn * 128 + col) * 128;
+  constexpr int NS = H * 2 / 128;  // 16 stages of 64 k
+  issueA(0);
+  issueB(0);
+  for (int s = 0; s < NS; ++s) {
+    // this wave's pieces of stage s landed and every wave's reads of stage s-1 retired
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (s + 1 < NS) issueA(s + 1);
+    const int8_t* st = jsm + (s & 1) * 65536;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int cs = ((kk * 4 + q) ^ sw) << 4;
+      uint4 fra[4], frb[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fra[i] = *(const uint4*)(st + fa0 + cs + i * 2048);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) frb[jj] = *(const uint4*)(st + fb0 + cs + jj * 2048);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) acc[i][jj] = mfma_bf16(fra[i], frb[jj], acc[i][jj]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kk == 0 && s + 1 < NS) {
+        issueB(s + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // F[row][j]: lane holds j = j0 + wm*64 + 16 i + 4q .. +3 of row row0 + wn*128 + 16 jj + col
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int n = n0 + wn * 128 + jj * 16 + col;
+    if (f_lens[n] <= t) continue;
+    float* dst = F + (size_t)(row0 + wn * 128 + jj * 16 + col) * J + j0 + wm * 64 + 4 * q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(acc[i][jj], (v4f*)(dst + i * 16));
+  }
+}
+
 // ---------------------------------------------------------------- greedy decode
 // Lock-step over the batch, like the reference's loop (rnnt_model.hpp:92-124), but only the
 // rows that emitted at the previous step re-run the prediction network:
@@ -582,6 +676,22 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
 int launch_joint_trans(const DecWeights& w, const uint16_t* fbf, const int32_t* f_lens, float* F, int Tp, int Npad,
                        hipStream_t st) {
   if (Tp <= 0) return 0;
+#ifndef RNNT_JT_GEMM
+#define RNNT_JT_GEMM 1
+#endif
+  if (RNNT_JT_GEMM && Npad % 256 == 0) {
+    static bool gattr = false;
+    if (!gattr) {
+      if (hipFuncSetAttribute((const void*)joint_trans_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              JG_SMEM) != hipSuccess)
+        return -1;
+      gattr = true;
+    }
+    const int nrt = Tp * Npad / 256;
+    hipLaunchKernelGGL(joint_trans_gemm_kernel, dim3(16 * ((nrt + 7) / 8)), dim3(512), JG_SMEM, st, w, fbf, f_lens, F,
+                       Npad, nrt);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   static bool attr = false;
   const int smem = 64 * JT_PITCH * 2;
   if (!attr) {

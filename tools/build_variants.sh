@@ -43,6 +43,7 @@ for v in "$@"; do
     pp) build pp -DRNNT_BK128=0 -DRNNT_PINGPONG=1 ;;
     ph2) build ph2 -DRNNT_BK128=0 -DRNNT_PHASES=2 ;;
     bk64) build bk64 -DRNNT_BK128=0 ;;
+    jt_old) build jt_old -DRNNT_JT_GEMM=0 ;;
     bk128_i1) build bk128_i1 -DRNNT_BK128_ISSUE=1 ;;
     stamps_bk64) build stamps_bk64 -DRNNT_DEV_STAMPS -DRNNT_BK128=0 ;;
     bk128_i0) build bk128_i0 -DRNNT_BK128_ISSUE=0 ;;
