@@ -27,10 +27,13 @@ __device__ const float4 g_act_tab[128] = {
 #ifdef RNNT_DEV_STAMPS
 __device__ unsigned long long g_est[1 << 22];
 __device__ unsigned int g_est_n;
-#define EST_MARK(v) v = threadIdx.x == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull
-#define EST_CLK(v) v = threadIdx.x == 0 ? __builtin_amdgcn_s_memtime() : 0ull
+#define EST_MARK(v) v = __builtin_amdgcn_s_memrealtime()
+// record slot i of this tile's 8-word record (thread 0 stores at once: nothing stays live)
+#define EST_PUT(i, v) \
+  if (threadIdx.x == 0 && est_k < (1u << 22) / 8) g_est[8 * est_k + (i)] = (v)
 #else
 #define EST_MARK(v)
+#define EST_PUT(i, v)
 #endif
 
 // ---------------------------------------------------------------- feature quantisation
@@ -98,7 +101,11 @@ constexpr int C_GLDS = (BN * 128 / 1024) / NWAVE;  // cell-state DMA pieces per 
 #endif
 constexpr int TAB_COPIES = RNNT_TAB_COPIES;
 constexpr int TAB_OFF = NSTAGE * STAGE_BYTES;   // LDS: sigma table after the ring
-constexpr int SMEM_BYTES = TAB_OFF + 128 * 16 * TAB_COPIES;
+#ifndef RNNT_PERSIST
+#define RNNT_PERSIST 0
+#endif
+constexpr int YS_OFF = TAB_OFF + 128 * 16 * TAB_COPIES;  // RNNT_PERSIST 2: the y image (256 x 80 B)
+constexpr int SMEM_BYTES = YS_OFF + (RNNT_PERSIST == 2 ? BN * 80 : 0);
 static_assert(TAB_COPIES == 1 || TAB_COPIES == 16, "table copies");
 static_assert(SMEM_BYTES <= 160 * 1024, "LDS");
 static_assert(BPW == 2 && (APW == 2 || APW == 4) && C_GLDS == 4, "staging split");
@@ -139,10 +146,25 @@ __device__ __forceinline__ void stage_barrier_n(int n) {
 // byte offset of (row r, byte b < 128) in a swizzled [rows][128 B] epilogue image
 __device__ __forceinline__ int cimg_off(int r, int b) { return r * 128 + ((((b >> 4) ^ r) & 7) << 4) + (b & 15); }
 
+// RNNT_PERSIST 2 (persistent workgroups, 128-byte stages): the next tile's stage 0 (job nx, tile
+// nmt/nnt; nx == nullptr: none) is DMA'd during this tile's epilogue into the buffer the last
+// stage used; roff: this tile's ring offset (stage s in buffer (s + roff) & 1); pre0: stage 0
+// was issued by the previous tile.
 __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem,
-                                             unsigned long long st_t0 = 0ull) {
-  unsigned long long st_t1 = 0ull, st_t2 = 0ull, st_c1 = 0ull, st_c2 = 0ull;
-  (void)st_t0; (void)st_t1; (void)st_t2; (void)st_c1; (void)st_c2;
+                                             unsigned long long st_t0 = 0ull, const EncStepArgs* nxp = nullptr,
+                                             bool has_nx = false, int nmt = 0, int nnt = 0, int roff = 0,
+                                             bool pre0 = false) {
+  (void)nxp; (void)has_nx; (void)nmt; (void)nnt; (void)roff; (void)pre0;
+  (void)st_t0;
+#ifdef RNNT_DEV_STAMPS
+  unsigned est_k;
+  {
+    unsigned v = 0;
+    if (threadIdx.x == 0) v = atomicAdd(&g_est_n, 1u);
+    est_k = __builtin_amdgcn_readfirstlane(v);  // wave 0 (the only writer) holds thread 0's ticket
+  }
+  EST_PUT(2, st_t0);
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
   const int m0 = mt * BM;  // packed gate row base
@@ -205,7 +227,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // two 64 KiB stages of 128-byte rows; the cell state goes into the buffer the last stage does
   // not occupy (stage nS-2's, issued once that stage's reads are retired)
   const int nS = K / 128;
-  const int cbuf = (nS & 1) * 65536;
+  const int cbuf = ((nS + roff) & 1) * 65536;
 #else
   const int cbuf = ((nK - NSTAGE) % NSTAGE) * STAGE_BYTES;
 #endif
@@ -252,7 +274,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     const uint32_t oH0 = rl * H + gc0, oH1 = rl * H + gc1;
     auto issue128A = [&](int s) __attribute__((always_inline)) {
       const int k = s * 128;
-      lds_char* st = lds + (s & 1) * 65536 + wave * 4096;
+      lds_char* st = lds + ((s + roff) & 1) * 65536 + wave * 4096;
 #pragma unroll
       for (int j = 0; j < 4; ++j)  // A pieces 4w..4w+3: rows 32w + 8j + r8
         __builtin_amdgcn_global_load_lds((glb_void*)(wbase + (size_t)(8 * j) * K + k + ((j & 1) ? oA1 : oA0)),
@@ -260,7 +282,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     };
     auto issue128B = [&](int s) __attribute__((always_inline)) {
       const int k = s * 128;
-      lds_char* st = lds + (s & 1) * 65536 + wave * 4096;
+      lds_char* st = lds + ((s + roff) & 1) * 65536 + wave * 4096;
       if (k < a.I) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -283,15 +305,14 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     // its B pieces after the first k step's MFMAs (the load path sees two half bursts per stage);
     // 1: waves 4-7 issue all of theirs after the first k step; 0: all at the top
     const bool late = RNNT_BK128_ISSUE == 1 && wn == 1;
-    issue128(0);
+    if (!pre0) issue128(0);
+#ifdef RNNT_DEV_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stamps only: stage 0 landed (this wave)
+    EST_PUT(3, __builtin_amdgcn_s_memrealtime());
+    EST_PUT(6, __builtin_amdgcn_s_memtime());
+#endif
     for (int s = 0; s < nS; ++s) {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#ifdef RNNT_DEV_STAMPS
-      if (s == 0) {
-        EST_MARK(st_t1);
-        EST_CLK(st_c1);
-      }
-#endif
       if (RNNT_BK128_ISSUE == 2) {
         if (s + 1 < nS) issue128A(s + 1);
         else issue_c();
@@ -299,7 +320,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
         if (s + 1 < nS) issue128(s + 1);
         else issue_c();
       }
-      const int8_t* st = smem + (s & 1) * 65536;
+      const int8_t* st = smem + ((s + roff) & 1) * 65536;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int cs = ((kk * 4 + q) ^ sw) << 4;
@@ -509,8 +530,8 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     stage_barrier_n(later * GLDS_PER_STAGE + (ks > nK - NSTAGE + 1 ? C_GLDS : 0));
 #ifdef RNNT_DEV_STAMPS
     if (ks == 0) {
-      EST_MARK(st_t1);
-      EST_CLK(st_c1);
+      EST_PUT(3, __builtin_amdgcn_s_memrealtime());
+      EST_PUT(6, __builtin_amdgcn_s_memtime());
     }
 #endif
 #if !RNNT_INTERLEAVE
@@ -587,8 +608,8 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #endif
   stage_barrier<0>();  // the cell-state DMA has landed for every wave
 #ifdef RNNT_DEV_STAMPS
-  EST_MARK(st_t2);
-  EST_CLK(st_c2);
+  EST_PUT(4, __builtin_amdgcn_s_memrealtime());
+  EST_PUT(7, __builtin_amdgcn_s_memtime());
 #endif
 #ifdef RNNT_DEV_NO_EPI  // development ablation: main loop only
 #pragma unroll
@@ -620,7 +641,32 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   const int ul = u0 - (m0 >> 2);  // this lane's first unit within the tile's 64
 #if RNNT_BK128
   lds_char* hs = lds + cbuf + 32768;
-  lds_char* ys = lds + ((nS - 1) & 1) * 65536;
+  // with a next-tile prefetch the last stage's buffer is taken: the int8 y image goes after the
+  // table (the caller passes no next tile for ENC_OUT_FINAL, whose bf16 image needs 32 KiB)
+  lds_char* ys = (RNNT_PERSIST == 2 && has_nx) ? lds + YS_OFF : lds + ((nS - 1 + roff) & 1) * 65536;
+#if RNNT_PERSIST == 2
+  if (has_nx) {
+    const EncStepArgs* nx = nxp;
+    // next tile's stage 0 into the last stage's buffer (its reads retired at the barrier above);
+    // issued after the bias loads so waiting for those does not wait for these
+    asm volatile("" ::: "memory");
+    const int K2 = nx->I + H, I2 = nx->I;
+    const int r8 = lane >> 3, sl = lane & 7;
+    const uint32_t gc0 = (sl ^ ((r8 >> 1) & 7)) * 16, gc1 = (sl ^ (((8 + r8) >> 1) & 7)) * 16;
+    const uint32_t rl = (uint32_t)(32 * wave + r8);
+    const int8_t* wb = nx->W + (size_t)nmt * BM * K2;
+    const int8_t* xb = nx->x + (size_t)nnt * BN * I2;
+    lds_char* st = lds + ((nS - 1 + roff) & 1) * 65536 + wave * 4096;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((glb_void*)(wb + (size_t)(8 * j) * K2 + ((j & 1) ? rl * K2 + gc1 : rl * K2 + gc0)),
+                                       (lds_void*)(st + j * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // k = 0 < I2: the x part
+      __builtin_amdgcn_global_load_lds((glb_void*)(xb + (size_t)(8 * j) * I2 + ((j & 1) ? rl * I2 + gc1 : rl * I2 + gc0)),
+                                       (lds_void*)(st + 32768 + j * 1024), 16, 0, 0);
+  }
+#endif
 #else
   lds_char* hs = lds + ((cbuf / STAGE_BYTES + 1) % NSTAGE) * STAGE_BYTES;
   lds_char* ys = lds + ((cbuf / STAGE_BYTES + 2) % NSTAGE) * STAGE_BYTES;
@@ -687,18 +733,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     }
   }
 #ifdef RNNT_DEV_STAMPS
-  if (threadIdx.x == 0) {
-    const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
-    const unsigned k_ = atomicAdd(&g_est_n, 1u);
-    if (k_ < (1u << 22) / 6) {
-      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-      g_est[6 * k_] = (unsigned long long)K | ((unsigned long long)mt << 16) | ((unsigned long long)nt << 24) |
-                      ((unsigned long long)hw << 32);
-      g_est[6 * k_ + 1] = (unsigned long long)(xcc & 0xff) | ((st_c2 - st_c1) << 8);  // + main-loop shader clocks
-      g_est[6 * k_ + 2] = st_t0; g_est[6 * k_ + 3] = st_t1; g_est[6 * k_ + 4] = st_t2; g_est[6 * k_ + 5] = t3;
-    }
-  }
+  EST_PUT(5, __builtin_amdgcn_s_memrealtime());
+  EST_PUT(0, (unsigned long long)K | ((unsigned long long)mt << 16) | ((unsigned long long)nt << 24) |
+                 ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32));  // HW_REG_HW_ID
+  EST_PUT(1, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20));        // HW_REG_XCC_ID
 #endif
 }
 
@@ -708,9 +746,6 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 // workgroups resident on an XCD share 4 weight tiles and ~8 activation tiles through its L2
 // (weights fetched from HBM/MALL 2x, activations 4x per tick, instead of 1x / 8x).
 // 2 waves per SIMD either way: one 8-wave workgroup per CU (ENC_WN 2) or two 4-wave ones (1)
-#ifndef RNNT_PERSIST
-#define RNNT_PERSIST 0
-#endif
 constexpr int WG_PER_CU = ENC_WN == 2 ? 1 : 2;
 constexpr int SLOTS_PER_XCD = 32 * WG_PER_CU;  // resident workgroups per XCD (32 CUs)
 __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(EncTickArgs args) {
@@ -730,6 +765,43 @@ __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(Enc
   // the order one-tile-per-workgroup rounds would run them (a layer-step 4 % shorter alone, but
   // the resident grid then starves the other streams' decode kernels: off by default)
   const int stride = RNNT_PERSIST ? (int)(gridDim.x >> 3) : 1 << 30;
+#if RNNT_PERSIST == 2
+  static_assert(RNNT_BK128, "next-tile prefetch uses the 128-byte stage ring");
+  auto pick = [&](int k, int& mt, int& nt) -> int {
+    for (int j = 0; j < args.njobs; ++j) {
+      const int nbt = args.nbt[j], h0 = (nbt + 1) >> 1;
+      const int cnt = 4 * (bg ? nbt - h0 : h0);
+      if (k < cnt) {
+        mt = gg * 4 + (k & 3);
+        nt = (bg ? h0 : 0) + (k >> 2);
+        return j;
+      }
+      k -= cnt;
+    }
+    return -1;
+  };
+  int k0 = blockIdx.x >> 3, mt = 0, nt = 0;
+  int jsel = pick(k0, mt, nt);
+  int roff = 0;
+  bool pre0 = false;
+  while (jsel >= 0) {
+    int nmt = 0, nnt = 0;
+    const int jn = pick(k0 + stride, nmt, nnt);
+    if (k0 != (int)(blockIdx.x >> 3)) __syncthreads();  // the previous tile's epilogue LDS reads are done
+    const EncStepArgs& cur = args.job[__builtin_amdgcn_readfirstlane(jsel)];
+    const bool pf = jn >= 0 && cur.mode != ENC_OUT_FINAL;
+    lstm_i8_step(cur, __builtin_amdgcn_readfirstlane(mt), __builtin_amdgcn_readfirstlane(nt), smem, st_t0,
+                 &args.job[__builtin_amdgcn_readfirstlane(jn >= 0 ? jn : jsel)], pf,
+                 __builtin_amdgcn_readfirstlane(nmt), __builtin_amdgcn_readfirstlane(nnt), roff, pre0);
+    roff = ((cur.I + H) / 128 - 1 + roff) & 1;  // the next tile starts in the last stage's buffer
+    pre0 = pf;
+    jsel = jn;
+    mt = nmt;
+    nt = nnt;
+    k0 += stride;
+  }
+  return;
+#endif
   for (int k0 = blockIdx.x >> 3;; k0 += stride) {
     int k = k0, jsel = -1, mt = 0, nt = 0;
     for (int j = 0; j < args.njobs; ++j) {
@@ -772,7 +844,11 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
   int per_xcd = 0;  // the batch-half-0 XCDs carry the larger half
   for (int j = 0; j < a.njobs; ++j) per_xcd += 4 * ((a.nbt[j] + 1) >> 1);
   if (per_xcd <= 0) return 0;
-  const int grid = 8 * (RNNT_PERSIST && per_xcd > SLOTS_PER_XCD ? SLOTS_PER_XCD : per_xcd);
+#ifndef RNNT_PERSIST_FREE  // persistent grids: workgroup slots per XCD left to other streams
+#define RNNT_PERSIST_FREE 0
+#endif
+  constexpr int PSLOTS = SLOTS_PER_XCD - RNNT_PERSIST_FREE;
+  const int grid = 8 * (RNNT_PERSIST && per_xcd > PSLOTS ? PSLOTS : per_xcd);
   hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(grid), dim3(NWAVE * 64), SMEM_BYTES, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -780,13 +856,13 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
 }  // namespace rnnt
 
 #ifdef RNNT_DEV_STAMPS
-// development: copy out (and reset) the tick kernel's per-tile stamp records (6 x u64 each)
+// development: copy out (and reset) the tick kernel's per-tile stamp records (8 x u64 each)
 extern "C" int rnnt_dev_read_enc_stamps(unsigned long long* out, int max_records) {
   unsigned int n = 0;
   if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(rnnt::g_est_n), sizeof(n)) != hipSuccess) return -1;
-  if (n > (1u << 22) / 6) n = (1u << 22) / 6;
+  if (n > (1u << 22) / 8) n = (1u << 22) / 8;
   if ((int)n > max_records) n = max_records;
-  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_est), (size_t)n * 6 * 8) != hipSuccess) return -1;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_est), (size_t)n * 8 * 8) != hipSuccess) return -1;
   const unsigned int z = 0;
   if (hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_est_n), &z, sizeof(z)) != hipSuccess) return -1;
   return (int)n;

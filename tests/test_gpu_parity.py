@@ -127,3 +127,46 @@ def test_config3_int8_full_batch128(engine, model, oracle):
     rl, steps = _run(engine, model, oracle, int(lens.max()), lens, seed=3)
     emit_rate = rl.sum() / ((lens + 1) // 2).sum()
     assert 0.02 < emit_rate < 5, emit_rate
+
+
+def test_large_batch_rows_match_small_batch(engine, model, oracle):
+    """N=4096 (16 batch tiles: several tiles per workgroup / CU, every tick schedule path) vs the
+    same rows run as small batches: the int8 encoder is exact and row-independent, so encoder
+    frames must be bit-identical and tokens identical whatever the batch composition; the first
+    rows are also checked against the oracle directly."""
+    from rnnt_amd.engine import Engine
+    n, T = 4096, 20
+    lens = np.sort(np.random.default_rng(11).integers(1, T + 1, n).astype(np.int32))[::-1].copy()
+    x = synthetic.make_features(T, n, seed=11, lens=lens)
+    Tp = (T + 1) // 2
+    big = Engine(model, device=0, max_batch=n, max_frames=T)
+    try:
+        f = torch.zeros((Tp, n, 1024), dtype=torch.float32, device="cuda")
+        res = torch.empty((n, big.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(n, dtype=torch.int32, device="cuda")
+        big.encode(_cuda(x), _cuda(lens), lens, n=n, f_out=f)
+        big.decode(res, rl)
+        torch.cuda.synchronize()
+        fg, res_g, rl_g = f.cpu().numpy(), res.cpu().numpy(), rl.cpu().numpy()
+    finally:
+        big.close()
+    for lo in (0, 1800, 4096 - 200):
+        rows = np.arange(lo, lo + 200)
+        sl = lens[rows]
+        xs = np.zeros((T, 256, x.shape[2]), np.float32)
+        xs[:, :200] = x[:, rows]
+        lp = np.zeros(256, np.int32)
+        lp[:200] = sl
+        fs = torch.zeros((Tp, 256, 1024), dtype=torch.float32, device="cuda")
+        rs = torch.empty((200, res_g.shape[1]), dtype=torch.int32, device="cuda")
+        rls = torch.empty(200, dtype=torch.int32, device="cuda")
+        engine.encode(_cuda(xs), _cuda(lp), sl, n=200, f_out=fs)
+        engine.decode(rs, rls)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(_valid(fs.cpu().numpy()[:, :200], sl).view(np.uint32),
+                                      _valid(fg[:, rows], sl).view(np.uint32))
+        np.testing.assert_array_equal(rls.cpu().numpy(), rl_g[rows])
+        np.testing.assert_array_equal(rs.cpu().numpy(), res_g[rows])
+        if lo == 0:
+            fo = oracle.encoder_i8(model, xs[:, :8], lp[:8])
+            np.testing.assert_array_equal(_valid(fg[:, :8], lens[:8]).view(np.uint32), _valid(fo, lens[:8]).view(np.uint32))

@@ -54,12 +54,12 @@ def main():
     rd(None, 0)
     eng.lstm_int8(args.first, 1, x, hx, cx, y)
     torch.cuda.synchronize()
-    buf = np.zeros(6 * (1 << 20), np.uint64)
-    n = rd(C.c_void_p(buf.ctypes.data), len(buf) // 6)
-    r = buf[: 6 * n].reshape(n, 6).astype(np.int64)
+    buf = np.zeros(8 * (1 << 19), np.uint64)
+    n = rd(C.c_void_p(buf.ctypes.data), len(buf) // 8)
+    r = buf[: 8 * n].reshape(n, 8).astype(np.int64)
     # HW_ID bits 8-15 (cu_id, sh_id, se_id) + XCC_ID: one value per CU
     cu = ((r[:, 0] >> 40) & 0xFF) | ((r[:, 1] & 0xFF) << 8)
-    clk = (r[:, 1] >> 8).astype(np.float64)  # shader clocks over the main loop (s_memtime)
+    clk = (r[:, 7] - r[:, 6]).astype(np.float64)  # shader clocks over the main loop (s_memtime)
     t0, t1, t2, t3 = r[:, 2], r[:, 3], r[:, 4], r[:, 5]
     order = np.argsort(t0)
     # launches: consecutive tiles whose start precedes the running max end belong together
