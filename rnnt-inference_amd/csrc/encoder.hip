@@ -74,6 +74,9 @@ constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-
 #ifndef RNNT_BK128  // 1: 128-byte-row stages, two buffers (see the main loop); 0: 64-byte stages, 4 buffers
 #define RNNT_BK128 (ENC_WN == 2)
 #endif
+#ifndef RNNT_BK128_PRELOAD  // 1: a stage's second k step's fragments read during the first's MFMAs
+#define RNNT_BK128_PRELOAD 0
+#endif
 #ifndef RNNT_BK128_ISSUE  // 128-byte stages: 0 all pieces at the stage top; 1 waves 4-7 mid-stage; 2 A top, B mid
 #define RNNT_BK128_ISSUE 2
 #endif
@@ -272,25 +275,25 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     const uint32_t oA0 = rl * K + gc0, oA1 = rl * K + gc1;
     const uint32_t oX0 = rl * a.I + gc0, oX1 = rl * a.I + gc1;
     const uint32_t oH0 = rl * H + gc0, oH1 = rl * H + gc1;
-    auto issue128A = [&](int s) __attribute__((always_inline)) {
+    auto issue128A = [&](int s, int jb = 0, int je = 4) __attribute__((always_inline)) {
       const int k = s * 128;
       lds_char* st = lds + ((s + roff) & 1) * 65536 + wave * 4096;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)  // A pieces 4w..4w+3: rows 32w + 8j + r8
+      for (int j = jb; j < je; ++j)  // A pieces 4w..4w+3: rows 32w + 8j + r8
         __builtin_amdgcn_global_load_lds((glb_void*)(wbase + (size_t)(8 * j) * K + k + ((j & 1) ? oA1 : oA0)),
                                          (lds_void*)(st + j * 1024), 16, 0, 0);
     };
-    auto issue128B = [&](int s) __attribute__((always_inline)) {
+    auto issue128B = [&](int s, int jb = 0, int je = 4) __attribute__((always_inline)) {
       const int k = s * 128;
       lds_char* st = lds + ((s + roff) & 1) * 65536 + wave * 4096;
       if (k < a.I) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = jb; j < je; ++j)
           __builtin_amdgcn_global_load_lds((glb_void*)(xbase0 + (size_t)(8 * j) * a.I + k + ((j & 1) ? oX1 : oX0)),
                                            (lds_void*)(st + 32768 + j * 1024), 16, 0, 0);
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = jb; j < je; ++j)
           __builtin_amdgcn_global_load_lds((glb_void*)(hbase0 + (size_t)(8 * j) * H + k + ((j & 1) ? oH1 : oH0)),
                                            (lds_void*)(st + 32768 + j * 1024), 16, 0, 0);
       }
@@ -298,6 +301,24 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     auto issue128 = [&](int s) __attribute__((always_inline)) {
       issue128A(s);
       issue128B(s);
+    };
+    // issue points of stage s+1's pieces inside stage s (RNNT_BK128_ISSUE >= 2): 0 top (after the
+    // barrier), 1 after half of the first k step, 2 after the first k step, 3 after half of the
+    // second.  2: A@0 B@2;  3: A0-1@0 A2-3@1 B0-1@2 B2-3@3;  4: A@0 B@1;  5: A0-1 B0-1@0 A2-3 B2-3@2
+    auto issue_at = [&](int pt, int s) __attribute__((always_inline)) {
+      constexpr int M = RNNT_BK128_ISSUE;
+      if (M == 2) { if (pt == 0) issue128A(s); if (pt == 2) issue128B(s); }
+      if (M == 3) {
+        if (pt == 0) issue128A(s, 0, 2);
+        if (pt == 1) issue128A(s, 2, 4);
+        if (pt == 2) issue128B(s, 0, 2);
+        if (pt == 3) issue128B(s, 2, 4);
+      }
+      if (M == 4) { if (pt == 0) issue128A(s); if (pt == 1) issue128B(s); }
+      if (M == 5) {
+        if (pt == 0) { issue128A(s, 0, 2); issue128B(s, 0, 2); }
+        if (pt == 2) { issue128A(s, 2, 4); issue128B(s, 2, 4); }
+      }
     };
     const int sw = col >> 1;  // (row >> 1) & 7 for rows 16i + col
     const int fa0 = (wm * 64 + col) * 128, fb0 = 32768 + (wn * 128 + col) * 128;
@@ -313,14 +334,54 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #endif
     for (int s = 0; s < nS; ++s) {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (RNNT_BK128_ISSUE == 2) {
-        if (s + 1 < nS) issue128A(s + 1);
+      if (RNNT_BK128_ISSUE >= 2) {
+        if (s + 1 < nS) issue_at(0, s + 1);
         else issue_c();
       } else if (!late) {
         if (s + 1 < nS) issue128(s + 1);
         else issue_c();
       }
       const int8_t* st = smem + ((s + roff) & 1) * 65536;
+#if RNNT_BK128_PRELOAD
+      // the second k step's fragments are read while the first one's MFMAs run: its A fragments
+      // into 4 extra registers up front, each B fragment into the register the first step's
+      // B fragment j frees once its 4 MFMAs are issued (column-major order)
+      {
+        const int cs0 = (q ^ sw) << 4, cs1 = ((4 + q) ^ sw) << 4;
+        v4i fra[4], frb[8], fna[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa0 + cs0 + i * 2048);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb0 + cs0 + j * 2048);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fna[i] = *(const v4i*)(st + fa0 + cs1 + i * 2048);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+          frb[j] = *(const v4i*)(st + fb0 + cs1 + j * 2048);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (RNNT_BK128_ISSUE >= 2 && s + 1 < nS) {
+          issue_at(1, s + 1);
+          issue_at(2, s + 1);
+          issue_at(3, s + 1);
+        }
+        if (late) {
+          if (s + 1 < nS) issue128(s + 1);
+          else issue_c();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fna[i], frb[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+#else
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int cs = ((kk * 4 + q) ^ sw) << 4;
@@ -332,14 +393,20 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+          if ((RNNT_BK128_ISSUE == 3 || (RNNT_BK128_ISSUE == 4 && kk == 0)) && i == 2 && s + 1 < nS) {
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            issue_at(2 * kk + 1, s + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
         }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
-        if (RNNT_BK128_ISSUE == 2 && kk == 0 && s + 1 < nS) {
-          __builtin_amdgcn_sched_barrier(0);
-          issue128B(s + 1);
+        if ((RNNT_BK128_ISSUE == 2 || RNNT_BK128_ISSUE == 3 || RNNT_BK128_ISSUE == 5) && kk == 0 && s + 1 < nS) {
+          issue_at(2, s + 1);
           __builtin_amdgcn_sched_barrier(0);
         }
         if (late && kk == 0) {
@@ -349,6 +416,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+#endif
     }
   }
 #elif RNNT_PINGPONG

@@ -46,6 +46,11 @@ for v in "$@"; do
     pp) build pp -DRNNT_BK128=0 -DRNNT_PINGPONG=1 ;;
     ph2) build ph2 -DRNNT_BK128=0 -DRNNT_PHASES=2 ;;
     bk64) build bk64 -DRNNT_BK128=0 ;;
+    pl) build pl -DRNNT_BK128_PRELOAD=1 ;;
+    is3) build is3 -DRNNT_BK128_ISSUE=3 ;;
+    is4) build is4 -DRNNT_BK128_ISSUE=4 ;;
+    is5) build is5 -DRNNT_BK128_ISSUE=5 ;;
+    pl_i0) build pl_i0 -DRNNT_BK128_PRELOAD=1 -DRNNT_BK128_ISSUE=0 ;;
     jt_old) build jt_old -DRNNT_JT_GEMM=0 ;;
     bk128_i1) build bk128_i1 -DRNNT_BK128_ISSUE=1 ;;
     stamps_bk64) build stamps_bk64 -DRNNT_DEV_STAMPS -DRNNT_BK128=0 ;;
