@@ -814,11 +814,35 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 // workgroups resident on an XCD share 4 weight tiles and ~8 activation tiles through its L2
 // (weights fetched from HBM/MALL 2x, activations 4x per tick, instead of 1x / 8x).
 // 2 waves per SIMD either way: one 8-wave workgroup per CU (ENC_WN 2) or two 4-wave ones (1)
+#ifndef RNNT_XCD_G  // gate tiles per XCD: 4 (x 1/2 of the batch tiles) or 8 (x 1/4)
+#define RNNT_XCD_G 4
+#endif
+constexpr int XG = RNNT_XCD_G;           // gate tiles per XCD
+constexpr int XGG = 16 / XG;             // gate groups
+constexpr int XP = 8 / XGG;              // batch parts
+static_assert(XG == 4 || XG == 8, "XCD tile map");
+// job tile k (0..) of XCD xcd -> (mt, nt); batch part p = tiles [p*nbt/XP, (p+1)*nbt/XP)
+__device__ __forceinline__ int xcd_pick(const EncTickArgs& args, int xcd, int k, int& mt, int& nt) {
+  const int gsel = xcd % XGG, psel = xcd / XGG;
+  for (int j = 0; j < args.njobs; ++j) {
+    const int nbt = args.nbt[j];
+    const int b0 = XG == 4 ? (psel ? (nbt + 1) >> 1 : 0) : psel * nbt / XP;
+    const int b1 = XG == 4 ? (psel ? nbt : (nbt + 1) >> 1) : (psel + 1) * nbt / XP;
+    const int cnt = XG * (b1 - b0);
+    if (k < cnt) {
+      mt = gsel * XG + (k % XG);
+      nt = b0 + k / XG;
+      return j;
+    }
+    k -= cnt;
+  }
+  return -1;
+}
 constexpr int WG_PER_CU = ENC_WN == 2 ? 1 : 2;
 constexpr int SLOTS_PER_XCD = 32 * WG_PER_CU;  // resident workgroups per XCD (32 CUs)
 __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(EncTickArgs args) {
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  const int xcd = blockIdx.x & 7, gg = xcd & 3, bg = xcd >> 2;
+  const int xcd = blockIdx.x & 7;
   unsigned long long st_t0 = 0ull;
   EST_MARK(st_t0);
 #pragma unroll
@@ -835,19 +859,7 @@ __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(Enc
   const int stride = RNNT_PERSIST ? (int)(gridDim.x >> 3) : 1 << 30;
 #if RNNT_PERSIST == 2
   static_assert(RNNT_BK128, "next-tile prefetch uses the 128-byte stage ring");
-  auto pick = [&](int k, int& mt, int& nt) -> int {
-    for (int j = 0; j < args.njobs; ++j) {
-      const int nbt = args.nbt[j], h0 = (nbt + 1) >> 1;
-      const int cnt = 4 * (bg ? nbt - h0 : h0);
-      if (k < cnt) {
-        mt = gg * 4 + (k & 3);
-        nt = (bg ? h0 : 0) + (k >> 2);
-        return j;
-      }
-      k -= cnt;
-    }
-    return -1;
-  };
+  auto pick = [&](int k, int& mt, int& nt) -> int { return xcd_pick(args, xcd, k, mt, nt); };
   int k0 = blockIdx.x >> 3, mt = 0, nt = 0;
   int jsel = pick(k0, mt, nt);
   int roff = 0;
@@ -871,18 +883,8 @@ __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(Enc
   return;
 #endif
   for (int k0 = blockIdx.x >> 3;; k0 += stride) {
-    int k = k0, jsel = -1, mt = 0, nt = 0;
-    for (int j = 0; j < args.njobs; ++j) {
-      const int nbt = args.nbt[j], h0 = (nbt + 1) >> 1;
-      const int cnt = 4 * (bg ? nbt - h0 : h0);
-      if (k < cnt) {
-        jsel = j;
-        mt = gg * 4 + (k & 3);
-        nt = (bg ? h0 : 0) + (k >> 2);
-        break;
-      }
-      k -= cnt;
-    }
+    int mt = 0, nt = 0;
+    const int jsel = xcd_pick(args, xcd, k0, mt, nt);
     if (jsel < 0) return;
     if (k0 != (int)(blockIdx.x >> 3)) __syncthreads();  // the previous tile's epilogue LDS reads are done
     // wave-uniform runtime index into the kernarg segment: the job's fields stay scalar loads
@@ -910,7 +912,7 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
     attr = true;
   }
   int per_xcd = 0;  // the batch-half-0 XCDs carry the larger half
-  for (int j = 0; j < a.njobs; ++j) per_xcd += 4 * ((a.nbt[j] + 1) >> 1);
+  for (int j = 0; j < a.njobs; ++j) per_xcd += XG * ((a.nbt[j] + XP - 1) / XP);  // the largest part
   if (per_xcd <= 0) return 0;
 #ifndef RNNT_PERSIST_FREE  // persistent grids: workgroup slots per XCD left to other streams
 #define RNNT_PERSIST_FREE 0

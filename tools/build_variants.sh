@@ -47,6 +47,7 @@ for v in "$@"; do
     ph2) build ph2 -DRNNT_BK128=0 -DRNNT_PHASES=2 ;;
     bk64) build bk64 -DRNNT_BK128=0 ;;
     pl) build pl -DRNNT_BK128_PRELOAD=1 ;;
+    xg8) build xg8 -DRNNT_XCD_G=8 ;;
     is3) build is3 -DRNNT_BK128_ISSUE=3 ;;
     is4) build is4 -DRNNT_BK128_ISSUE=4 ;;
     is5) build is5 -DRNNT_BK128_ISSUE=5 ;;
