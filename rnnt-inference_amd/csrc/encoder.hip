@@ -774,7 +774,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #ifdef RNNT_DEV_EPI_NOSTORE
   return;
 #endif
-  __syncthreads();
+  // the staged images are complete: LDS writes retired + barrier.  Not __syncthreads(): its
+  // fence waits vmcnt(0), i.e. for a next-tile prefetch (RNNT_PERSIST 2) still in flight
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   // copy-out: thread t moves 16-byte chunks; a wave instruction writes 8 (c, bf16 f) or 16 (h, y)
   // whole row segments
   const int um = m0 >> 2;
@@ -867,7 +869,9 @@ __global__ void __launch_bounds__(NWAVE * 64, WG_PER_CU) lstm_i8_tick_kernel(Enc
   while (jsel >= 0) {
     int nmt = 0, nnt = 0;
     const int jn = pick(k0 + stride, nmt, nnt);
-    if (k0 != (int)(blockIdx.x >> 3)) __syncthreads();  // the previous tile's epilogue LDS reads are done
+    // the previous tile's epilogue LDS reads are done (raw barrier: the prefetched stage 0 and
+    // the copy-out stores may stay in flight)
+    if (k0 != (int)(blockIdx.x >> 3)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const EncStepArgs& cur = args.job[__builtin_amdgcn_readfirstlane(jsel)];
     const bool pf = jn >= 0 && cur.mode != ENC_OUT_FINAL;
     lstm_i8_step(cur, __builtin_amdgcn_readfirstlane(mt), __builtin_amdgcn_readfirstlane(nt), smem, st_t0,

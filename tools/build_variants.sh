@@ -24,6 +24,7 @@ for v in "$@"; do
     stagger3) build stagger3 -DRNNT_STAGGER=1 -DRNNT_STAGGER_AT=3 ;;
     persist) build persist -DRNNT_PERSIST=1 ;;
     persist2) build persist2 -DRNNT_PERSIST=2 ;;
+    stamps_p2) build stamps_p2 -DRNNT_DEV_STAMPS -DRNNT_PERSIST=2 ;;
     persist2_f1) build persist2_f1 -DRNNT_PERSIST=2 -DRNNT_PERSIST_FREE=1 ;;
     persist2_f2) build persist2_f2 -DRNNT_PERSIST=2 -DRNNT_PERSIST_FREE=2 ;;
     epi_nobq) build epi_nobq -DRNNT_DEV_EPI_NOBQ ;;

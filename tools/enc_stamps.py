@@ -85,7 +85,17 @@ def main():
                 lag.append((t0[b] - t3[a]) / 100.0)
         first_round = idx[t0[idx] - s0 < 50]  # started within 0.5 us of the launch's first tile
         out.setdefault("first_round_tiles", []).append(int(len(first_round)))
+    # position of each tile in its CU's sequence within the launch (0 = first)
+    pos = np.zeros(n, np.int64)
+    for L in range(lid + 1):
+        idx = np.where(launch == L)[0]
+        for c in np.unique(cu[idx]):
+            ii = idx[cu[idx] == c]
+            pos[ii[np.argsort(t0[ii])]] = np.arange(len(ii))
     pro, main_, epi = (t1 - t0) / 100.0, (t2 - t1) / 100.0, (t3 - t2) / 100.0
+    for ps in (0, 1):
+        m = pos == ps
+        out[f"tile{ps}_prologue_main_epilogue_us_p50"] = [pct(pro[m], 50), pct(main_[m], 50), pct(epi[m], 50)]
     out.update({
         "launch_span_us": [round(v, 1) for v in per],
         "prologue_us_p10_p50_p90": [pct(pro, 10), pct(pro, 50), pct(pro, 90)],
