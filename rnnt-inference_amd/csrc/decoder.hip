@@ -263,6 +263,11 @@ __global__ void __launch_bounds__(512, 1) joint_trans_gemm_kernel(DecWeights w, 
 __device__ __forceinline__ float* hc_part(float* hc, int row, int slot, int part) {
   return hc + ((size_t)row * 2 + slot) * 4 * P + part * P;  // parts 0:h0 1:h1 2:c0 3:c1
 }
+// the h parts hold bf16 (the contract rounds h to bf16 where it is produced): 320 bf16 in the
+// first 640 bytes of the part, so the staging loads of the step kernels move half the bytes
+__device__ __forceinline__ uint16_t* h_bf(float* hc, int row, int slot, int layer) {
+  return (uint16_t*)hc_part(hc, row, slot, layer);
+}
 
 __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
@@ -365,9 +370,9 @@ __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int p
       uint4 v = uint4{0u, 0u, 0u, 0u};
       if (em >= 0) {
         const int r = entry_row(em), smm = entry_slot(em);
-        const float* src = LAYER == 0 ? hc_part(a.hc, r, smm, 0) + k
-                                      : (k < P ? hc_part(a.hc, r, smm ^ 1, 0) + k : hc_part(a.hc, r, smm, 1) + k - P);
-        v = pack8(*(const float4*)src, *(const float4*)(src + 4));
+        const uint16_t* src = LAYER == 0 ? h_bf(a.hc, r, smm, 0) + k
+                                         : (k < P ? h_bf(a.hc, r, smm ^ 1, 0) + k : h_bf(a.hc, r, smm, 1) + k - P);
+        v = *(const uint4*)src;
       }
       *(uint4*)&X[m][k] = v;
     }
@@ -401,7 +406,7 @@ __global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int p
           const float cn = fg * cp[st][tt] + ig * gg;
           const float hh = bf_round_ftz(og * det_tanh(cn));
           hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
-          hc_part(a.hc, row, sl ^ 1, LAYER)[u] = hh;
+          h_bf(a.hc, row, sl ^ 1, LAYER)[u] = (uint16_t)(__float_as_uint(hh) >> 16);  // hh is bf16-exact
         }
       }
     }
@@ -454,8 +459,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       const int m = i / (P / 8), k = (i % (P / 8)) * 8, em = ents[m];
       uint4 v = uint4{0u, 0u, 0u, 0u};
       if (em >= 0) {
-        const float* src = hc_part(a.hc, entry_row(em), entry_slot(em) ^ 1, 1) + k;
-        v = pack8(*(const float4*)src, *(const float4*)(src + 4));
+        v = *(const uint4*)(h_bf(a.hc, entry_row(em), entry_slot(em) ^ 1, 1) + k);
       }
       *(uint4*)&X[m][k] = v;
     }
