@@ -48,6 +48,10 @@ for v in "$@"; do
     ph2) build ph2 -DRNNT_BK128=0 -DRNNT_PHASES=2 ;;
     bk64) build bk64 -DRNNT_BK128=0 ;;
     pl) build pl -DRNNT_BK128_PRELOAD=1 ;;
+    pr96) build pr96 -DRNNT_PRED_RG=96 ;;
+    pr32) build pr32 -DRNNT_PRED_RG=32 ;;
+    jg1024) build jg1024 -DRNNT_JOINT_G=1024 ;;
+    gr192) build gr192 -DRNNT_G_RG=192 ;;
     xg8) build xg8 -DRNNT_XCD_G=8 ;;
     is3) build is3 -DRNNT_BK128_ISSUE=3 ;;
     is4) build is4 -DRNNT_BK128_ISSUE=4 ;;
