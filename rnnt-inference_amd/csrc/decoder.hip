@@ -310,11 +310,18 @@ constexpr int DEC_SUB = DEC_RT / 16;
 #define RNNT_JOINT_G 512
 #endif
 constexpr int PRED_ROW_GROUPS = RNNT_PRED_RG;
+#ifndef RNNT_PRED_WIDE_MIN  // live-row bound from which the prediction launches use 8-wave workgroups (0: never)
+#define RNNT_PRED_WIDE_MIN 0
+#endif
 constexpr int G_ROW_GROUPS = RNNT_G_RG;
 constexpr int JOINT_GROUPS = RNNT_JOINT_G;
 
-template <int LAYER>
-__global__ void __launch_bounds__(PRED_THREADS) dec_pred_kernel(DecArgs a, int parity) {
+// NW waves per workgroup (NW gate tiles): 4 by default; 8 while the emit lists are long (the
+// staged rows then feed twice the gate tiles, halving the row re-reads across column groups, at
+// the price of a 2x weight slice per launch -- which only the short tail steps notice)
+template <int LAYER, int NW>
+__global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity) {
+  constexpr int PRED_THREADS = NW * 64;
   constexpr int NT = 1;                  // gate tiles per wave
   constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
   constexpr int XP = KX + 8;             // bf16 pitch: +16 B per row (conflict-free b128 reads)
@@ -653,10 +660,15 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_joint = lt1 < JOINT_GROUPS ? lt1 : JOINT_GROUPS;
     for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      hipLaunchKernelGGL(dec_pred_kernel<0>, dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                         dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL(dec_pred_kernel<1>, dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                         dim3(PRED_THREADS), 0, st, a, p);
+      if (RNNT_PRED_WIDE_MIN > 0 && live_bound >= RNNT_PRED_WIDE_MIN) {
+        hipLaunchKernelGGL((dec_pred_kernel<0, 8>), dim3(xcd_grid_size(PG4 / (16 * 8), rg_pred)), dim3(512), 0, st, a, p);
+        hipLaunchKernelGGL((dec_pred_kernel<1, 8>), dim3(xcd_grid_size(PG4 / (16 * 8), rg_pred)), dim3(512), 0, st, a, p);
+      } else {
+        hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                           dim3(PRED_THREADS), 0, st, a, p);
+        hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                           dim3(PRED_THREADS), 0, st, a, p);
+      }
       hipLaunchKernelGGL(dec_g_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), rg_g)), dim3(G_THREADS), 0, st, a,
                          p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);

@@ -49,6 +49,9 @@ for v in "$@"; do
     bk64) build bk64 -DRNNT_BK128=0 ;;
     pl) build pl -DRNNT_BK128_PRELOAD=1 ;;
     pr96) build pr96 -DRNNT_PRED_RG=96 ;;
+    pw1024) build pw1024 -DRNNT_PRED_WIDE_MIN=1024 ;;
+    pw2048) build pw2048 -DRNNT_PRED_WIDE_MIN=2048 ;;
+    pw4096) build pw4096 -DRNNT_PRED_WIDE_MIN=4096 ;;
     pr32) build pr32 -DRNNT_PRED_RG=32 ;;
     jg1024) build jg1024 -DRNNT_JOINT_G=1024 ;;
     gr192) build gr192 -DRNNT_G_RG=192 ;;
