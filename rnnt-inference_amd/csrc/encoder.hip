@@ -68,23 +68,11 @@ constexpr int NWAVE = 4 * ENC_WN;            // 4 gate-row waves x ENC_WN batch-
 #ifndef RNNT_STAGGER
 #define RNNT_STAGGER 1
 #endif
-#ifndef RNNT_READAHEAD  // 1: fragments of the next k step read during this step's MFMAs
-#define RNNT_READAHEAD 0
-#endif
 #ifndef RNNT_BK128  // 1: 128-byte-row stages, two buffers (see the main loop); 0: 64-byte stages, 4 buffers
 #define RNNT_BK128 (ENC_WN == 2)
 #endif
-#ifndef RNNT_BK128_PRELOAD  // 1: a stage's second k step's fragments read during the first's MFMAs
-#define RNNT_BK128_PRELOAD 0
-#endif
 #ifndef RNNT_BK128_ISSUE  // 128-byte stages: 0 all pieces at the stage top; 1 waves 4-7 mid-stage; 2 A top, B mid
 #define RNNT_BK128_ISSUE 2
-#endif
-#ifndef RNNT_PHASES  // 2: two barrier-bracketed MFMA phases per k step (see the main loop)
-#define RNNT_PHASES 0
-#endif
-#ifndef RNNT_PINGPONG  // 1: the two wave groups alternate memory and MFMA phases (see the main loop)
-#define RNNT_PINGPONG 0
 #endif
 #ifndef RNNT_PRIO_MODE  // 0: MFMA clusters at priority 1; 1: + late waves at 1 throughout; 2: static, late waves only
 #define RNNT_PRIO_MODE 0
@@ -342,46 +330,6 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
         else issue_c();
       }
       const int8_t* st = smem + ((s + roff) & 1) * 65536;
-#if RNNT_BK128_PRELOAD
-      // the second k step's fragments are read while the first one's MFMAs run: its A fragments
-      // into 4 extra registers up front, each B fragment into the register the first step's
-      // B fragment j frees once its 4 MFMAs are issued (column-major order)
-      {
-        const int cs0 = (q ^ sw) << 4, cs1 = ((4 + q) ^ sw) << 4;
-        v4i fra[4], frb[8], fna[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa0 + cs0 + i * 2048);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb0 + cs0 + j * 2048);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fna[i] = *(const v4i*)(st + fa0 + cs1 + i * 2048);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
-          frb[j] = *(const v4i*)(st + fb0 + cs1 + j * 2048);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (RNNT_BK128_ISSUE >= 2 && s + 1 < nS) {
-          issue_at(1, s + 1);
-          issue_at(2, s + 1);
-          issue_at(3, s + 1);
-        }
-        if (late) {
-          if (s + 1 < nS) issue128(s + 1);
-          else issue_c();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fna[i], frb[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-#else
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int cs = ((kk * 4 + q) ^ sw) << 4;
@@ -416,173 +364,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#endif
     }
-  }
-#elif RNNT_PINGPONG
-  // Ping-pong main loop: waves 0-3 (group A) and 4-7 (group B, one per SIMD beside an A wave)
-  // run offset by one phase.  A wave alternates a memory phase (read k step ks's fragments from
-  // LDS, issue its LDS-DMA pieces of stage ks+3, retire the reads) and an MFMA phase (32 MFMAs
-  // on those fragments); with B one phase behind, every SIMD always has one wave in an MFMA
-  // phase while its partner does the memory work.  One raw barrier per phase.  Ordering (stage
-  // s in ring buffer s % 4): A reads stage s in phase 2s, B in 2s+1; A waits for its pieces of
-  // stage s in its MFMA phase 2s-1, B in its memory phase 2s-1, both before the barrier ending
-  // that phase (RAW).  Stage s+3 goes into the buffer of stage s-1 in phases 2s (A) / 2s+1 (B),
-  // after both groups retired their reads of it (lgkmcnt(0) before the barriers ending phases
-  // 2s-2 / 2s-1: WAR).  The cell state goes into the buffer of stage nK-4 as before.
-  static_assert(NSTAGE == 4, "ping-pong ring: stage s+3 refills the buffer of stage s-1");
-  auto vm_wait = [&](int n) __attribute__((always_inline)) {
-    switch (n) {
-#define RNNT_VW(v) \
-  case v: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(v) : "memory"); break;
-      RNNT_VW(0) RNNT_VW(4) RNNT_VW(8) RNNT_VW(12) RNNT_VW(16)
-#undef RNNT_VW
-      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-  };
-  static_assert(GLDS_PER_STAGE == 4 && C_GLDS == 4, "vm_wait immediates");
-#pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s) issue(s);
-  stage_barrier<2 * GLDS_PER_STAGE>();  // stage 0 landed for every wave
-  const int grp = wn;
-  v4i fra[4], frb[8];
-  for (int ph = 0; ph <= 2 * nK; ++ph) {
-    const int lp = ph - grp;
-    if (lp >= 0 && lp < 2 * nK) {
-      const int ks = lp >> 1;
-      if ((lp & 1) == 0) {  // memory phase of k step ks
-        if (grp == 1 && ks + 1 < nK)  // stage ks+1 landed (A reads it next phase)
-          vm_wait((ks + 2 < nK ? GLDS_PER_STAGE : 0) + (ks > nK - NSTAGE + 1 ? C_GLDS : 0));
-        const int8_t* st = smem + (ks % NSTAGE) * STAGE_BYTES;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa + i * 1024);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb + j * 1024);
-        if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
-        else if (ks + NSTAGE - 1 == nK) issue_c();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      } else {  // MFMA phase of k step ks
-        if (grp == 0 && ks + 1 < nK)  // stage ks+1 landed (read next phase)
-          vm_wait(((ks + 2 < nK) + (ks + 3 < nK)) * GLDS_PER_STAGE + (ks >= nK - NSTAGE + 1 ? C_GLDS : 0));
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    asm volatile("s_barrier" ::: "memory");
-  }
-#elif RNNT_READAHEAD
-  // Read-ahead main loop: the fragments of stage ks+1 are read from LDS while the MFMAs of stage
-  // ks run on fragments already in registers, so no wave waits on an LDS burst after the
-  // per-step barrier.  Stage j is read during step j-1 and consumed in step j; the barrier at
-  // the top of step ks (after this wave's DMA of stage ks+1 has landed) certifies every wave's
-  // reads of stage ks-1 done, so stage ks+NSTAGE-1 is DMA'd into that buffer; two stages stay in
-  // flight.  The cell state goes into the buffer of stage nK-NSTAGE at step nK-NSTAGE+1 as before.
-  static_assert(NSTAGE == 4, "read-ahead ring: 1 being read, 2 in flight, 1 being refilled");
-#pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s) issue(s);  // nK >= 20 for every layer
-  stage_barrier_n((NSTAGE - 2) * GLDS_PER_STAGE);  // stage 0 landed everywhere
-  v4i fra[4], frb[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(smem + fa + i * 1024);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(smem + fb + j * 1024);
-  for (int ks = 0; ks < nK; ++ks) {
-    const bool more = ks + 1 < nK;
-    const int8_t* st = smem + ((ks + 1) % NSTAGE) * STAGE_BYTES;
-    v4i fna[4];
-    if (more) {
-      // stage ks+1 landed: this wave may leave stage ks+2 (if issued) and the cell-state pieces
-      // (issued at step nK-NSTAGE+1) in flight
-      const int later = ks + 2 < nK ? 1 : 0;
-      stage_barrier_n(later * GLDS_PER_STAGE + (ks >= nK - NSTAGE + 2 ? C_GLDS : 0));
-      if (ks + NSTAGE - 1 < nK) issue(ks + NSTAGE - 1);
-      else if (ks + NSTAGE - 1 == nK) issue_c();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fna[i] = *(const v4i*)(st + fa + i * 1024);
-    }
-    __builtin_amdgcn_s_setprio(1);
-    // column-major MFMA order: once B fragment j has fed its 4 MFMAs its registers take the next
-    // stage's fragment j (register budget: 128 accumulators + 16 A + 16 next-A + 32 B)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
-      if (more) frb[j] = *(const v4i*)(st + fb + j * 1024);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fra[i] = fna[i];
-    }
-  }
-#elif RNNT_PHASES == 2
-  // Two barrier-bracketed phases per k step (the guide's 8-phase GEMM structure at this tile):
-  // each phase reads its fragments and issues half of this wave's pieces of stage ks+3, meets
-  // the other waves at a barrier, retires its reads and runs 16 MFMAs, and closes with a
-  // barrier, so every wave's MFMA cluster runs while the others' are running.  Stage ks+3
-  // refills the buffer of stage ks-1 (all reads of it retired before the barriers closing step
-  // ks-1); phase B waits for this wave's pieces of stage ks+1, so after its closing barrier
-  // stage ks+1 has landed everywhere.  The cell state goes into stage nK-4's buffer at ks = nK-3.
-  static_assert(NSTAGE == 4 && GLDS_PER_STAGE == 4 && C_GLDS == 4, "two-phase ring");
-#pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s) issue(s);
-  stage_barrier<2 * GLDS_PER_STAGE>();  // stage 0 landed for every wave
-  for (int ks = 0; ks < nK; ++ks) {
-    const int8_t* st = smem + (ks % NSTAGE) * STAGE_BYTES;
-    const int nxt = ks + NSTAGE - 1;
-    v4i fra[2], frb[8];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) fra[i] = *(const v4i*)(st + fa + i * 1024);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb + j * 1024);
-    if (nxt < nK) {
-      issue_piece(nxt, 0);
-      issue_piece(nxt, 1);
-    } else if (nxt == nK) {
-      issue_c();
-    }
-    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    v4i frc[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) frc[i] = *(const v4i*)(st + fa + (i + 2) * 1024);
-    if (nxt < nK) {
-      issue_piece(nxt, 2);
-      issue_piece(nxt, 3);
-    }
-    if (ks + 1 < nK) {
-      // pieces issued after stage ks+1's: stages ks+2, ks+3 (when they exist) and the cell state
-      const int n = 4 * (ks + 2 < nK) + 4 * (ks + 3 < nK) + 4 * (ks >= nK - 3);
-      if (n == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (n == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_barrier\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        acc[i + 2][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(frc[i], frb[j], acc[i + 2][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
   }
 #else
 #pragma unroll

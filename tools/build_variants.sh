@@ -43,11 +43,7 @@ for v in "$@"; do
     noload) build noload -DRNNT_DEV_NO_LOAD ;;
     ji1) build ji1 -DRNNT_JOINT_ITERS=1 ;;
     stamps) build stamps -DRNNT_DEV_STAMPS ;;
-    ra) build ra -DRNNT_BK128=0 -DRNNT_READAHEAD=1 ;;
-    pp) build pp -DRNNT_BK128=0 -DRNNT_PINGPONG=1 ;;
-    ph2) build ph2 -DRNNT_BK128=0 -DRNNT_PHASES=2 ;;
     bk64) build bk64 -DRNNT_BK128=0 ;;
-    pl) build pl -DRNNT_BK128_PRELOAD=1 ;;
     pr96) build pr96 -DRNNT_PRED_RG=96 ;;
     pw1024) build pw1024 -DRNNT_PRED_WIDE_MIN=1024 ;;
     pw2048) build pw2048 -DRNNT_PRED_WIDE_MIN=2048 ;;
@@ -59,17 +55,12 @@ for v in "$@"; do
     is3) build is3 -DRNNT_BK128_ISSUE=3 ;;
     is4) build is4 -DRNNT_BK128_ISSUE=4 ;;
     is5) build is5 -DRNNT_BK128_ISSUE=5 ;;
-    pl_i0) build pl_i0 -DRNNT_BK128_PRELOAD=1 -DRNNT_BK128_ISSUE=0 ;;
     jt_old) build jt_old -DRNNT_JT_GEMM=0 ;;
     bk128_i1) build bk128_i1 -DRNNT_BK128_ISSUE=1 ;;
     stamps_bk64) build stamps_bk64 -DRNNT_DEV_STAMPS -DRNNT_BK128=0 ;;
     bk128_i0) build bk128_i0 -DRNNT_BK128_ISSUE=0 ;;
     bk64_noepi) build bk64_noepi -DRNNT_BK128=0 -DRNNT_DEV_NO_EPI ;;
     tab16) build tab16 -DRNNT_TAB_COPIES=16 ;;
-    ph2_noepi) build ph2_noepi -DRNNT_BK128=0 -DRNNT_PHASES=2 -DRNNT_DEV_NO_EPI ;;
-    pp_noepi) build pp_noepi -DRNNT_BK128=0 -DRNNT_PINGPONG=1 -DRNNT_DEV_NO_EPI ;;
-    ra_noepi) build ra_noepi -DRNNT_BK128=0 -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_EPI ;;
-    ra_noload) build ra_noload -DRNNT_BK128=0 -DRNNT_READAHEAD=1 -DRNNT_DEV_NO_LOAD ;;
     rt64) build rt64 -DRNNT_DEC_RT=64 ;;
     ji3) build ji3 -DRNNT_JOINT_ITERS=3 ;;
     ji6) build ji6 -DRNNT_JOINT_ITERS=6 ;;
