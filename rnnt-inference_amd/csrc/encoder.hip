@@ -697,6 +697,11 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
       return -1;
     attr = true;
   }
+  // shapes the kernel's staging assumes (checked on the host: a mismatch would read out of bounds)
+  for (int j = 0; j < a.njobs; ++j) {
+    const int K = a.job[j].I + H;
+    if (a.job[j].I % (RNNT_BK128 ? 128 : BK) != 0 || K % (RNNT_BK128 ? 128 : BK) != 0 || a.nbt[j] < 0) return -1;
+  }
   int per_xcd = 0;  // the batch-half-0 XCDs carry the larger half
   for (int j = 0; j < a.njobs; ++j) per_xcd += XG * ((a.nbt[j] + XP - 1) / XP);  // the largest part
   if (per_xcd <= 0) return 0;
