@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--first", type=int, default=1, help="0: K1280, 1: K2048, 2: K3072")
     ap.add_argument("--T", type=int, default=4)
+    ap.add_argument("--encode", action="store_true",
+                    help="time a whole dense encode (every tick carries all its layer-steps) instead of one layer")
     args = ap.parse_args()
     pm, _ = weights.build_model()
     n_pad = pad_batch(args.n)
@@ -44,15 +46,24 @@ def main():
     rd.restype = C.c_int
     I = {0: 256, 1: 1024, 2: 2048}[args.first]
     T = args.T
-    x = (torch.randn((T, n_pad, 256), device="cuda") if args.first == 0 else
-         torch.randint(-128, 127, (T, n_pad, I), dtype=torch.int8, device="cuda"))
-    hx = torch.zeros((1, n_pad, 1024), dtype=torch.int8, device="cuda")
-    cx = torch.zeros((1, n_pad, 1024), dtype=torch.int16, device="cuda")
-    y = torch.empty((T, n_pad, 1024), dtype=torch.int8, device="cuda")
-    eng.lstm_int8(args.first, 1, x, hx, cx, y)  # warm
+    if args.encode:
+        T = max(T, 16)
+        feats = torch.randn((T, n_pad, 256), device="cuda")
+        lens_h = np.full(args.n, T, np.int32)
+        lens = torch.zeros(n_pad, dtype=torch.int32, device="cuda")
+        lens[: args.n] = T
+        run = lambda: eng.encode(feats, lens, lens_h, n=args.n)  # noqa: E731
+    else:
+        x = (torch.randn((T, n_pad, 256), device="cuda") if args.first == 0 else
+             torch.randint(-128, 127, (T, n_pad, I), dtype=torch.int8, device="cuda"))
+        hx = torch.zeros((1, n_pad, 1024), dtype=torch.int8, device="cuda")
+        cx = torch.zeros((1, n_pad, 1024), dtype=torch.int16, device="cuda")
+        y = torch.empty((T, n_pad, 1024), dtype=torch.int8, device="cuda")
+        run = lambda: eng.lstm_int8(args.first, 1, x, hx, cx, y)  # noqa: E731
+    run()  # warm
     torch.cuda.synchronize()
     rd(None, 0)
-    eng.lstm_int8(args.first, 1, x, hx, cx, y)
+    run()
     torch.cuda.synchronize()
     buf = np.zeros(8 * (1 << 19), np.uint64)
     n = rd(C.c_void_p(buf.ctypes.data), len(buf) // 8)
@@ -73,10 +84,16 @@ def main():
     out = {"tiles": int(n), "launches": int(lid + 1), "K": int(r[0, 0] & 0xFFFF)}
     per = []
     lag = []
+    util, gaps, prev_end = [], [], None
     for L in range(lid + 1):
         idx = np.where(launch == L)[0]
         s0, e1 = t0[idx].min(), t3[idx].max()
         per.append((e1 - s0) / 100.0)
+        # CU occupancy inside the launch (tile time / (CUs x span)) and the gap since the last one
+        util.append(float((t3[idx] - t0[idx]).sum()) / (256.0 * max(1, e1 - s0)))
+        if prev_end is not None:
+            gaps.append((s0 - prev_end) / 100.0)
+        prev_end = e1
         # dispatch lag: tiles that started after another tile ended on the same CU slot
         for c in np.unique(cu[idx]):
             ii = idx[cu[idx] == c]
@@ -97,7 +114,10 @@ def main():
         m = pos == ps
         out[f"tile{ps}_prologue_main_epilogue_us_p50"] = [pct(pro[m], 50), pct(main_[m], 50), pct(epi[m], 50)]
     out.update({
-        "launch_span_us": [round(v, 1) for v in per],
+        "launch_span_us_p50": pct(per, 50),
+        "launch_cu_occupancy_p10_p50_p90": [pct(util, 10), pct(util, 50), pct(util, 90)],
+        "gap_between_launches_us_p50": pct(gaps, 50) if gaps else None,
+        "launch_span_us": [round(v, 1) for v in per[:8]],
         "prologue_us_p10_p50_p90": [pct(pro, 10), pct(pro, 50), pct(pro, 90)],
         "main_us_p10_p50_p90": [pct(main_, 10), pct(main_, 50), pct(main_, 90)],
         "epilogue_us_p10_p50_p90": [pct(epi, 10), pct(epi, 50), pct(epi, 90)],
