@@ -33,6 +33,8 @@ from rnnt_amd.engine import Engine, PartitionedStream, cu_mask_words, pad_batch 
 
 METRIC = "MLPerf Offline utterances/sec at 1/2/4/8 MI355X; WER vs fp32 ref"
 INT8_DENSE_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 MFMA = 2x the ~2.5 PF dense bf16 rate
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+DECODE_OPS_PER_STEP = 4_682_752  # (2*2*4P*2P + 2*J*(H+P) + 2*K*J) per frame or emitted symbol
 
 
 def parse():
@@ -361,8 +363,15 @@ def main():
             traffic = json.load(open(args.traffic_json)).get("lstm_i8_step_bytes_per_launch")
         except Exception:
             traffic = None
+    # decode work: D = (T' + U) * 4,682,752 bf16 ops per utterance, summed over the query
+    dec_ops = float(enc_frames + emitted) * DECODE_OPS_PER_STEP
+    dec_ms = (st["greedy_ms"] + st["joint_trans_ms"]) / args.steps
+    dec_ms_iso = iso["greedy_ms"] + iso["joint_trans_ms"]
+    dec_ach = dec_ops / (dec_ms * 1e-3) / 1e12 if dec_ms > 0 else 0.0
+    dec_ach_iso = dec_ops / (dec_ms_iso * 1e-3) / 1e12 if dec_ms_iso > 0 else 0.0
+    ticks_q = st["step_launches"] / args.steps
     roofline = {
-        "bound": "mfma", "kernel": "lstm_i8_step_kernel (int8 encoder, all 5 layers)",
+        "bound": "mfma", "kernel": "lstm_i8_tick_kernel (int8 encoder, up to 5 layer-steps per launch)",
         "achieved": round(achieved, 2), "peak": INT8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
         "frac": round(achieved / INT8_DENSE_PEAK_TOPS, 4), "traffic": traffic,
         "measured_on": "HIP events around every encode call on its own stream, timed region (encode overlaps "
@@ -371,6 +380,15 @@ def main():
         "joint_trans_ms_per_query": round(st["joint_trans_ms"] / args.steps, 3),
         "greedy_ms_per_query": round(st["greedy_ms"] / args.steps, 3),
         "tick_launches_per_query": int(st["step_launches"] // args.steps),
+        "encode_us_per_tick_events": round(st["encode_ms"] / args.steps / ticks_q * 1e3, 2) if ticks_q else None,
+        "encode_us_per_tick_note": "event time per encode call / tick launches (includes the quantize kernel and "
+                                   "the gaps between ticks; rocprofv3 kernel stats give the kernel alone)",
+        "decode": {"kernels": "joint_trans_gemm_kernel + dec_pred/g/joint step kernels (bf16 MFMA)",
+                   "ops_per_query": dec_ops, "achieved": round(dec_ach, 2), "peak": BF16_DENSE_PEAK_TFLOPS,
+                   "unit": "TFLOP/s", "frac": round(dec_ach / BF16_DENSE_PEAK_TFLOPS, 4),
+                   "isolated_achieved": round(dec_ach_iso, 2),
+                   "isolated_frac": round(dec_ach_iso / BF16_DENSE_PEAK_TFLOPS, 4),
+                   "note": "latency-bound lock-step greedy loop; time = joint_trans + greedy event time"},
         "isolated": {"achieved": round(achieved_iso, 2), "frac": round(achieved_iso / INT8_DENSE_PEAK_TOPS, 4),
                      "encode_ms_per_query": round(iso["encode_ms"], 3),
                      "greedy_ms_per_query": round(iso["greedy_ms"], 3),
