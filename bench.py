@@ -146,7 +146,7 @@ def make_wav_batches(qsl, query, batch, sizes=None):
         bl = qsl["lens"][idx].astype(np.int32)
         wl = qsl["wav_lens"][idx].astype(np.int32)
         T = int(bl.max())
-        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, wav_lens_host=wl,
+        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, wav_lens_host=wl, idx=idx,
                         wav_lens=torch.from_numpy(wl).cuda(), wav_off=torch.from_numpy(qsl["wav_offs"][idx]).cuda(),
                         lens=torch.zeros(n_pad, dtype=torch.int32, device="cuda"),
                         x=torch.zeros((T, n_pad, 256), dtype=torch.float32, device="cuda")))
@@ -176,7 +176,7 @@ def make_batches(qsl, query, batch, sizes=None):
         valid = t < ln
         x = torch.zeros((T, n_pad, 256), dtype=torch.float32, device="cuda")
         x[:, :n, :240] = qsl["feats"][torch.where(valid, rows, 0)] * valid[..., None]
-        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, lens=torch.from_numpy(lp).cuda(), x=x))
+        out.append(dict(n=n, n_pad=n_pad, T=T, lens_host=bl, lens=torch.from_numpy(lp).cuda(), x=x, idx=idx))
     torch.cuda.synchronize()
     return out
 
@@ -221,24 +221,54 @@ def run_step(engines, streams, batches, featurizers=None, store=None, dec_stream
     return lens, toks
 
 
-def cpu_baseline(pm, lens, n_sample, seed):
+def sample_timed_rows(batches, n_sample, inflight):
+    """Rows of the timed query to re-check on the CPU: evenly spaced rows (first = longest,
+    last = shortest) of the first batch each engine ran and of the query's last batch, so the
+    sample spans every engine in flight and both ends of the length-sorted query."""
+    picks = sorted(set(list(range(min(inflight, len(batches)))) + [len(batches) - 1]))
+    per = max(2, -(-n_sample // len(picks)))
+    out = []
+    for b in picks:
+        n = batches[b]["n"]
+        rows = np.unique(np.linspace(0, n - 1, min(per, n)).round().astype(np.int64))
+        out += [(b, int(r)) for r in rows]
+    return out
+
+
+def cpu_baseline(pm, qsl, batches, timed_lens, timed_toks, n_sample, inflight):
     """The C restatement (oracle/, TEST INFRASTRUCTURE) timed on this host's cores on a bounded
-    sample of the same workload; also returns its tokens for a parity spot-check."""
+    sample of the timed query's own utterances, and the parity check of the tokens the GPU
+    produced for those rows INSIDE the timed region (last timed step) against it."""
     from oracle import oracle
-    rng = np.random.default_rng(seed)
-    idx = rng.choice(len(lens), size=min(n_sample, len(lens)), replace=False)
-    sl = np.sort(lens[idx])[::-1].astype(np.int32)
-    n_pad = pad_batch(len(sl))
-    lp = np.zeros(n_pad, np.int32)
-    lp[: len(sl)] = sl
-    x = synthetic.make_features(int(sl.max()), n_pad, seed=seed + 17, lens=lp)
+    picks = sample_timed_rows(batches, n_sample, inflight)
+    order = sorted(range(len(picks)), key=lambda i: -int(batches[picks[i][0]]["lens_host"][picks[i][1]]))
+    picks = [picks[i] for i in order]  # longest first, as the SUT sorts
+    qidx = np.array([batches[b]["idx"][r] for b, r in picks], np.int64)
+    sl = qsl["lens"][qidx].astype(np.int32)
+    n = len(sl)
+    T = int(sl.max())
+    x = np.zeros((T, n, 256), np.float32)
+    feats = qsl["feats"]
+    for i, q in enumerate(qidx):
+        o = int(qsl["offs"][q])
+        x[: sl[i], i, :240] = feats[o: o + int(sl[i])].cpu().numpy()
     oracle.lib()
     t0 = time.perf_counter()
-    f = oracle.encoder_i8(pm, x[:, : len(sl)], sl)
+    f = oracle.encoder_i8(pm, x, sl)
     res, rl, _ = oracle.greedy_decode(pm, f, (sl + 1) // 2, max_res=(500 // 2) * 30)
     dt = time.perf_counter() - t0
-    return dict(value=len(sl) / dt, seconds=dt, x=x, lens=lp, n=len(sl), sl=sl, res=res, rl=rl,
-                cores=oracle.lib().oracle_num_threads(), frames=int(sl.sum()))
+    mism = 0
+    gpu_res = np.full_like(res, -1)
+    gpu_rl = np.zeros_like(rl)
+    for i, (b, r) in enumerate(picks):
+        gl = int(timed_lens[b][r])
+        gpu_rl[i] = gl
+        gpu_res[i, :gl] = timed_toks[b][r, :gl].numpy()
+        if gl != int(rl[i]) or not np.array_equal(gpu_res[i, :gl], res[i, :gl]):
+            mism += 1
+    engines_hit = sorted({b % inflight for b, _ in picks})
+    return dict(value=n / dt, seconds=dt, n=n, sl=sl, x=x, res=res, rl=rl, cores=oracle.lib().oracle_num_threads(),
+                frames=int(sl.sum()), mismatches=mism, gpu_res=gpu_res, gpu_rl=gpu_rl, batches=sorted({b for b, _ in picks}), engines=engines_hit)
 
 
 def wer_vs_fp32(engine, ckpt, pm, cb, gpu_res, gpu_rl):
@@ -254,9 +284,13 @@ def wer_vs_fp32(engine, ckpt, pm, cb, gpu_res, gpu_rl):
     from rnnt_amd import accuracy
     sd = weights.migrate_state_dict(ckpt)
     engine.load_f32_encoder([weights.enc_layer_params(sd, l) for l in range(5)])
-    n, sl, x = cb["n"], cb["sl"], cb["x"]
-    T, n_pad = x.shape[0], x.shape[1]
-    xd, ld = torch.from_numpy(x).cuda(), torch.from_numpy(cb["lens"]).cuda()
+    n, sl = cb["n"], cb["sl"]
+    T, n_pad = cb["x"].shape[0], pad_batch(n)
+    x = np.zeros((T, n_pad, 256), np.float32)
+    x[:, :n] = cb["x"]
+    lp = np.zeros(n_pad, np.int32)
+    lp[:n] = sl
+    xd, ld = torch.from_numpy(x).cuda(), torch.from_numpy(lp).cuda()
     f32 = torch.empty(((T + 1) // 2, n_pad, 1024), dtype=torch.float32, device="cuda")
     fi8 = torch.empty_like(f32)
     engine.encode_f32(xd, ld, n, f32)
@@ -336,7 +370,7 @@ def main():
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lens_out, _ = run_step(engines, streams, batches, fzs, store, dec_streams, args.enc_concurrency)
+        lens_out, toks_out = run_step(engines, streams, batches, fzs, store, dec_streams, args.enc_concurrency)
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
@@ -412,21 +446,17 @@ def main():
                    "encoder_frames_per_query": enc_frames, "emitted_symbols_per_query": emitted},
         "roofline": roofline,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(pm, lens, args.cpu_sample, seed=99)
-        # parity spot-check of the same sample on the GPU
-        res = torch.empty((cb["n"], engine.max_res), dtype=torch.int32, device="cuda")
-        rl = torch.empty(cb["n"], dtype=torch.int32, device="cuda")
-        engine.infer(torch.from_numpy(cb["x"]).cuda(), torch.from_numpy(cb["lens"]).cuda(), cb["sl"], res, rl, n=cb["n"])
-        torch.cuda.synchronize()
-        same = bool(np.array_equal(rl.cpu().numpy(), cb["rl"]) and
-                    np.array_equal(res.cpu().numpy()[:, : cb["res"].shape[1]], cb["res"]))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.wav:
+        cb = cpu_baseline(pm, qsl, batches, lens_out, toks_out, args.cpu_sample, args.inflight)
         out["cpu_baseline"] = {"value": round(cb["value"], 3), "unit": "utterances/s", "cores": cb["cores"],
                                "kind": "port",
-                               "sample": f"{cb['n']} utterances ({cb['frames']} frames) drawn from the same QSL, "
-                                         f"int8 encoder + greedy decode, {cb['seconds']:.1f} s"}
-        out["parity_spot_check"] = {"utterances": cb["n"], "tokens_identical": same}
-        out["wer_vs_fp32"] = wer_vs_fp32(engine, ckpt, pm, cb, res.cpu().numpy(), rl.cpu().numpy())
+                               "sample": f"{cb['n']} utterances ({cb['frames']} frames) of the timed query (batches "
+                                         f"{cb['batches']}, longest to shortest rows), int8 encoder + greedy decode, "
+                                         f"{cb['seconds']:.1f} s"}
+        out["parity_spot_check"] = {"utterances": cb["n"], "source": "token rows produced inside the last timed step",
+                                    "batches": cb["batches"], "engines": cb["engines"],
+                                    "mismatched_rows": cb["mismatches"], "tokens_identical": cb["mismatches"] == 0}
+        out["wer_vs_fp32"] = wer_vs_fp32(engine, ckpt, pm, cb, cb["gpu_res"], cb["gpu_rl"])
     if rank == 0:
         print(json.dumps(out), flush=True)
     for e in engines:

@@ -696,26 +696,16 @@ int launch_joint_trans(const DecWeights& w, const uint16_t* fbf, const int32_t* 
 #define RNNT_JT_GEMM 1
 #endif
   if (RNNT_JT_GEMM && Npad % 256 == 0) {
-    static bool gattr = false;
-    if (!gattr) {
-      if (hipFuncSetAttribute((const void*)joint_trans_gemm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              JG_SMEM) != hipSuccess)
-        return -1;
-      gattr = true;
-    }
+    static std::atomic<uint64_t> gattr{0};
+    if (set_smem_attr_once((const void*)joint_trans_gemm_kernel, JG_SMEM, gattr)) return -1;
     const int nrt = Tp * Npad / 256;
     hipLaunchKernelGGL(joint_trans_gemm_kernel, dim3(16 * ((nrt + 7) / 8)), dim3(512), JG_SMEM, st, w, fbf, f_lens, F,
                        Npad, nrt);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
-  static bool attr = false;
+  static std::atomic<uint64_t> attr{0};
   const int smem = 64 * JT_PITCH * 2;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)joint_trans_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, smem) !=
-        hipSuccess)
-      return -1;
-    attr = true;
-  }
+  if (set_smem_attr_once((const void*)joint_trans_kernel, smem, attr)) return -1;
   const int nrows = Tp * Npad;
   hipLaunchKernelGGL(joint_trans_kernel, dim3(xcd_grid_size(J / 64, (nrows + JT_ROWS - 1) / JT_ROWS)), dim3(256), smem,
                      st, w, fbf, f_lens, F, Npad, nrows);

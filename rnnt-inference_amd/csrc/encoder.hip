@@ -690,13 +690,8 @@ int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStrea
 }
 
 int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute((const void*)lstm_i8_tick_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            SMEM_BYTES) != hipSuccess)
-      return -1;
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  if (set_smem_attr_once((const void*)lstm_i8_tick_kernel, SMEM_BYTES, attr)) return -1;
   // shapes the kernel's staging assumes (checked on the host: a mismatch would read out of bounds)
   for (int j = 0; j < a.njobs; ++j) {
     const int K = a.job[j].I + H;

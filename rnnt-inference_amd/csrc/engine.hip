@@ -30,6 +30,9 @@ static int fail(int code, const std::string& msg) {
   return code;
 }
 int rnnt_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
+#define DEVICE_SCOPE(dev)                                                                      \
+  DeviceScope dscope_(dev);                                                                    \
+  if (!dscope_.ok) return fail(RNNT_EDEVICE, "hipSetDevice failed")
 #define HIPCHK(x)                                                                              \
   do {                                                                                         \
     hipError_t e_ = (x);                                                                       \
@@ -61,6 +64,12 @@ struct rnnt_engine {
   hipEvent_t poll_ev[2] = {nullptr, nullptr};
   // last encoded batch
   int last_T = 0, last_n = 0, last_npad = 0;
+  // Stream ordering of the engine's own state (h/c, x0q, the encoder output, decode state):
+  // every call that touches it waits for the previous such call's completion event, on
+  // whatever stream that one ran, and records its own -- so encode -> decode -> next encode
+  // are ordered even when the caller puts them on different streams.
+  hipEvent_t state_ev = nullptr;
+  bool state_rec = false;
   // profiling
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_enc;
@@ -107,7 +116,7 @@ extern "C" const char* rnnt_last_error(void) { return g_err.c_str(); }
 // (an XCD with none is given all of its CUs by the runtime).
 extern "C" int rnnt_stream_create(int device, const uint32_t* cu_mask, int mask_words, void** out) {
   if (!out || (cu_mask && (mask_words <= 0 || mask_words > 16))) return fail(RNNT_EINVAL, "rnnt_stream_create: bad mask");
-  HIPCHK(hipSetDevice(device));
+  DEVICE_SCOPE(device);
   hipStream_t s = nullptr;
   if (cu_mask) {
     uint32_t per_xcd[8] = {0};
@@ -236,18 +245,24 @@ static int alloc_workspace(rnnt_engine* e) {
   for (int i = 0; i < 2 && !r; ++i)
     if (hipEventCreateWithFlags(&e->poll_ev[i], hipEventDisableTiming) != hipSuccess)
       r = fail(RNNT_EDEVICE, "hipEventCreate failed");
+  if (!r && hipEventCreateWithFlags(&e->state_ev, hipEventDisableTiming) != hipSuccess)
+    r = fail(RNNT_EDEVICE, "hipEventCreate failed");
   return r;
 }
 
 extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
   if (!e) return;
-  (void)hipSetDevice(e->device);
+  DeviceScope dscope(e->device);
   for (void* p : e->allocs) (void)hipFree(p);
   for (void* p : e->f32_ws) (void)hipFree(p);
   if (e->op_count_host) (void)hipHostFree(e->op_count_host);
   if (e->host_flags) (void)hipHostFree(e->host_flags);
   for (auto ev : e->poll_ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (e->state_ev) {
+    (void)hipEventSynchronize(e->state_ev);
+    (void)hipEventDestroy(e->state_ev);
+  }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -267,7 +282,8 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   e->np_max = (e->opts.max_batch + ENC_PAD - 1) / ENC_PAD * ENC_PAD;
   e->tp_max = (e->opts.max_frames + 1) / 2;
   int r = 0;
-  if (hipSetDevice(device) != hipSuccess) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
+  DeviceScope dscope(device);
+  if (!dscope.ok) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
   if (!r && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
   if (!r) r = pack_model(e, model);
@@ -298,6 +314,18 @@ __global__ void stack_time_kernel(const int8_t* x, const int32_t* lens, int T, i
 // `stream` is used as given: 0 is the legacy default (null) stream, which is what torch's
 // default stream is; the engine's own stream is only used by rnnt_engine_create.
 static hipStream_t pick(rnnt_engine*, void* s) { return (hipStream_t)s; }
+
+// state_ev protocol (see rnnt_engine::state_ev)
+static int state_acquire(rnnt_engine* e, hipStream_t st) {
+  if (e->state_rec && hipStreamWaitEvent(st, e->state_ev, 0) != hipSuccess)
+    return fail(RNNT_EDEVICE, "hipStreamWaitEvent failed");
+  return 0;
+}
+static int state_release(rnnt_engine* e, hipStream_t st) {
+  if (hipEventRecord(e->state_ev, st) != hipSuccess) return fail(RNNT_EDEVICE, "hipEventRecord failed");
+  e->state_rec = true;
+  return 0;
+}
 
 // number of leading 256-row tiles that hold a row with len > thr
 static int active_tiles(const std::vector<int>& tile_max, int thr) {
@@ -393,8 +421,9 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
   if (!e || !feats || !lens) return fail(RNNT_EINVAL, "null argument");
   int r = check_batch(e, T, n, n_pad);
   if (r) return r;
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
+  if ((r = state_acquire(e, st))) return r;
   const int Tp = (T + 1) / 2;
   const std::vector<int> tm = tile_maxima(lens_host, n, n_pad);
   for (int l = 0; l < 5; ++l) {
@@ -431,6 +460,7 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
   hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->flen, n_pad);
   HIPCHK(hipGetLastError());
   if (e->prof) e->ev_enc.push_back({ev0, new_event(st)});
+  if ((r = state_release(e, st))) return r;
   e->encode_calls++;
   e->last_T = T;
   e->last_n = n;
@@ -442,8 +472,10 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   if (!e || !res || !res_len) return fail(RNNT_EINVAL, "null argument");
   if (e->last_n <= 0) return fail(RNNT_EINVAL, "decode before encode");
   if (max_res <= 0) return fail(RNNT_EINVAL, "max_res must be positive");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
+  int r = state_acquire(e, st);
+  if (r) return r;
   const int Tp = (e->last_T + 1) / 2;
   hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
   if (launch_joint_trans(e->dw, e->fbf, e->flen, e->F, Tp, e->last_npad, st))
@@ -466,6 +498,7 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   if (steps < 0) return fail(RNNT_EDEVICE, "greedy launch failed");
   e->decode_steps += steps;
   if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
+  if ((r = state_release(e, st))) return r;
   e->decode_calls++;
   return 0;
 }
@@ -478,7 +511,7 @@ extern "C" int rnnt_engine_set_profiling(rnnt_engine* e, int on) {
 
 extern "C" int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset) {
   if (!e || !out) return fail(RNNT_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   memset(out, 0, sizeof(*out));
   for (auto& p : e->ev_enc) {
     float ms = 0;
@@ -522,8 +555,10 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
     return fail(RNNT_EINVAL, "T / n_pad out of range");
   if (first <= 1 && first + count > 2) return fail(RNNT_EINVAL, "a call covers pre_rnn or post_rnn, not both");
   if (first >= 2 && T > e->tp_max) return fail(RNNT_EINVAL, "post_rnn T exceeds ceil(max_frames/2)");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
+  int r0 = state_acquire(e, st);
+  if (r0) return r0;
   const int8_t* cur = (const int8_t*)x;
   if (first == 0) {
     if (launch_quantize((const float*)x, (int64_t)T * n_pad * FEAT, e->in_s[0], e->x0q, st))
@@ -547,14 +582,14 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
     HIPCHK(hipMemcpyAsync(cx + i * NH, e->c[l], NH * 2, hipMemcpyDeviceToDevice, st));
     cur = dst;
   }
-  return 0;
+  return state_release(e, st);
 }
 
 extern "C" int rnnt_op_stack_time(rnnt_engine* e, const int8_t* x, const int32_t* x_lens, int T, int n_pad, int C,
                                   int8_t* y, void* stream) {
   if (!e || !x || !x_lens || !y) return fail(RNNT_EINVAL, "null argument");
   if (T <= 0 || n_pad <= 0 || C <= 0 || C % 16) return fail(RNNT_EINVAL, "bad shape");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   hipLaunchKernelGGL(stack_time_kernel, dim3(n_pad, (T + 1) / 2), dim3(64), 0, pick(e, stream), x, x_lens, T, n_pad,
                      C, y);
   HIPCHK(hipGetLastError());
@@ -568,7 +603,7 @@ static const int F32_IP[5] = {256, 1024, 2048, 1024, 1024};  // padded to 32 (ch
 extern "C" int rnnt_engine_load_f32_encoder(rnnt_engine* e, const float* const* wih, const float* const* whh,
                                             const float* const* bih, const float* const* bhh) {
   if (!e || !wih || !whh || !bih || !bhh) return fail(RNNT_EINVAL, "null argument");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   for (int l = 0; l < 5; ++l) {
     if (!wih[l] || !whh[l] || !bih[l] || !bhh[l]) return fail(RNNT_EINVAL, "null fp32 encoder weight");
     const int I = F32_I[l], Ip = F32_IP[l];
@@ -659,7 +694,7 @@ extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const 
   if (!e->f32_loaded) return fail(RNNT_EINVAL, "fp32 encoder weights not loaded (rnnt_engine_load_f32_encoder)");
   if (T <= 0 || T > e->opts.max_frames || n <= 0 || n_pad < n || n_pad % 64)
     return fail(RNNT_EINVAL, "T / n / n_pad out of range (n_pad a multiple of 64)");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
   int r = f32_workspace(e, T, n_pad);
   if (r) return r;
@@ -684,7 +719,7 @@ extern "C" int rnnt_op_lstm_bf16(rnnt_engine* e, const uint16_t* x, const uint16
                                  float* cy, int n_pad, void* stream) {
   if (!e || !x || !hx || !cx || !hy || !cy) return fail(RNNT_EINVAL, "null argument");
   if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
   const size_t NP = (size_t)n_pad * P;
   if (launch_op_lstm_bf16(e->dw, 0, x, hx, cx, hy, cy, n_pad, st) ||
@@ -697,7 +732,7 @@ extern "C" int rnnt_op_joint_hidden(rnnt_engine* e, const float* f, const uint16
                                     void* stream) {
   if (!e || !f || !g || !y1) return fail(RNNT_EINVAL, "null argument");
   if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   if (launch_op_joint_hidden(e->dw, f, g, y1, n_pad, pick(e, stream))) return fail(RNNT_EDEVICE, "joint launch failed");
   return 0;
 }
@@ -705,7 +740,7 @@ extern "C" int rnnt_op_joint_hidden(rnnt_engine* e, const float* f, const uint16
 extern "C" int rnnt_op_joint_logits(rnnt_engine* e, const uint16_t* y1, float* logits, int n_pad, void* stream) {
   if (!e || !y1 || !logits) return fail(RNNT_EINVAL, "null argument");
   if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   if (launch_op_joint_logits(e->dw, y1, logits, n_pad, pick(e, stream))) return fail(RNNT_EDEVICE, "linear2 launch failed");
   return 0;
 }
@@ -723,13 +758,15 @@ extern "C" int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int
       !pre_cg || !hg || !cg || !finish)
     return fail(RNNT_EINVAL, "null argument");
   if (n <= 0 || n_pad < n || max_res <= 0) return fail(RNNT_EINVAL, "bad sizes");
-  HIPCHK(hipSetDevice(e->device));
+  DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
   if (!e->op_count) {
     int r = dev_alloc(e, &e->op_count, 4);
     if (r) return r;
     HIPCHK(hipHostMalloc((void**)&e->op_count_host, sizeof(int32_t)));
   }
+  int r = state_acquire(e, st);
+  if (r) return r;
   GreedyUpdateArgs a{symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg,
                      finish, e->op_count + 1, n, n_pad, max_res};
   if (launch_op_greedy_update(a, st)) return fail(RNNT_EDEVICE, "greedy_update launch failed");
@@ -737,6 +774,7 @@ extern "C" int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int
   hipLaunchKernelGGL(op_count_unfinished_kernel, dim3((n + 255) / 256), dim3(256), 0, st, finish, n, e->op_count);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(e->op_count_host, e->op_count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  if ((r = state_release(e, st))) return r;
   HIPCHK(hipStreamSynchronize(st));
   return *e->op_count_host == 0 ? 1 : 0;  // all(finish), the op's bool result
 }

@@ -31,6 +31,7 @@
 
 #include "../../include/rnnt_mi355x.h"
 #include "featurizer.hpp"
+#include "rnnt_device.hpp"
 
 namespace rnnt {
 namespace {
@@ -361,7 +362,8 @@ extern "C" int rnnt_featurizer_create(const rnnt_featurizer_config* cfg, const f
                                 "win 320, hop 160, 80 filters, splice 3, pad 256)");
   if (!(cfg->norm_eps >= 0.0f) || !(cfg->dither >= 0.0f) || !(cfg->log_guard >= 0.0f))
     return fz_fail(RNNT_EINVAL, "negative dither / log guard / eps");
-  FZCHK(hipSetDevice(device));
+  DeviceScope dscope(device);
+  if (!dscope.ok) return fz_fail(RNNT_EDEVICE, "hipSetDevice failed");
   // fb^T as MFMA B fragments per 16-filter column tile over the tile's non-zero bin span; column
   // tiles dealt to the 4 waves longest first (each wave projects its tiles for every chunk)
   std::vector<float> frag;
@@ -431,7 +433,7 @@ extern "C" int rnnt_featurizer_create(const rnnt_featurizer_config* cfg, const f
 
 extern "C" void rnnt_featurizer_destroy(rnnt_featurizer* f) {
   if (!f) return;
-  (void)hipSetDevice(f->device);
+  DeviceScope dscope(f->device);
   for (void* p : f->allocs) (void)hipFree(p);
   if (f->plan) (void)hipFree(f->plan);
   delete f;
@@ -450,7 +452,8 @@ extern "C" int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const i
     tmax = std::max(tmax, rnnt_featurizer_frames(wav_lens_host[i]));
   }
   if (tmax > T_out) return fz_fail(RNNT_EINVAL, "T_out smaller than the longest utterance's feature frames");
-  FZCHK(hipSetDevice(f->device));
+  DeviceScope dscope(f->device);
+  if (!dscope.ok) return fz_fail(RNNT_EDEVICE, "hipSetDevice failed");
   size_t chunks = 0;
   for (int i = 0; i < n; ++i)
     if (wav_lens_host[i] > 0) chunks += (size_t)(1 + wav_lens_host[i] / FZ_HOP + FZ_CHUNK - 1) / FZ_CHUNK;

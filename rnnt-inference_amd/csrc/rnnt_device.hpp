@@ -8,7 +8,42 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <mutex>
+
 namespace rnnt {
+
+// ---- host helpers shared by the launchers and the C ABI
+// Every entry point runs on its engine's device and gives the caller's current device back.
+struct DeviceScope {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
+// Raise a kernel's dynamic-LDS limit once per device, safely from concurrent host threads
+// (one engine per GPU, one host thread per engine: several threads may launch the first time
+// together).  `done` holds one bit per device id.
+static inline int set_smem_attr_once(const void* fn, int bytes, std::atomic<uint64_t>& done) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  const uint64_t bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return 0;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.load(std::memory_order_relaxed) & bit) return 0;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) return -1;
+  done.fetch_or(bit, std::memory_order_release);
+  return 0;
+}
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
