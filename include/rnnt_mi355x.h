@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RNNT_ABI_VERSION 4
+#define RNNT_ABI_VERSION 5
 
 #define RNNT_OK 0
 #define RNNT_EINVAL (-22)
@@ -106,11 +106,37 @@ int rnnt_engine_infer(rnnt_engine* e, const float* feats, const int32_t* lens, c
 int rnnt_engine_load_f32_encoder(rnnt_engine* e, const float* const* wih, const float* const* whh,
                                  const float* const* bih, const float* const* bhh);
 /* feats device fp32 [T][n_pad][256] (channels 240..255 ignored), lens device int32 [n_pad];
- * f_out device fp32 [ceil(T/2)][n_pad][1024].  n_pad a multiple of 64.  Arithmetic: k-ordered fp32
- * fma chains (b_ih + x.W_ih^T, b_hh + h.W_hh^T) on v_mfma_f32_16x16x4_f32, exact vs the CPU
- * restatement (oracle_encoder_f32). */
+ * f_out device fp32 [ceil(T/2)][n_pad][1024] or NULL.  n_pad a multiple of 64.  Arithmetic: k-ordered
+ * fp32 fma chains (b_ih + x.W_ih^T, b_hh + h.W_hh^T) on v_mfma_f32_16x16x4_f32, exact vs the CPU
+ * restatement (oracle_encoder_f32).  Keeps f for rnnt_engine_decode_f32 (the fp32 decoder) and, when
+ * n_pad <= max_batch (rounded up to 256), a bf16 copy for rnnt_engine_decode: the reference's
+ * run_mode="f32" + enable_bf16 path, which converts f to bf16 before the joint (decoder.py:121-122). */
 int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const int32_t* lens, int T, int n, int n_pad,
                            float* f_out, void* stream);
+
+/* ---- fp32 decoder (the run_mode="f32" Prediction / Joint with P.lstm and fp32 Linear layers,
+ * modeling_rnnt.py:183-205, 285-288, and GreedyDecoder.greedy_decode_f32, decoder.py:102-169).
+ * Natural layouts, fp32: embed [28][320], pred_w_ih/w_hh [2][1280][320] (gate order i,f,g,o),
+ * pred_b_ih/b_hh [2][1280], joint_w1t [512][1024], joint_w1p [512][320], joint_bt/bp [512]
+ * (bt = 0 after migrate_state_dict, utils.py:69), joint_w2 [29][512], joint_b2 [29]. */
+typedef struct {
+  const float* embed;
+  const float* pred_w_ih[2];
+  const float* pred_w_hh[2];
+  const float* pred_b_ih[2];
+  const float* pred_b_hh[2];
+  const float* joint_w1t;
+  const float* joint_w1p;
+  const float* joint_bt;
+  const float* joint_bp;
+  const float* joint_w2;
+  const float* joint_b2;
+} rnnt_f32_decoder_desc;
+int rnnt_engine_load_f32_decoder(rnnt_engine* e, const rnnt_f32_decoder_desc* d);
+/* Greedy decode of the last rnnt_engine_encode_f32 output in fp32 (k-ordered fp32 fma chains on
+ * v_mfma_f32_16x16x4_f32, exact vs oracle_greedy_decode with bf16 = 0); res / res_len as
+ * rnnt_engine_decode. */
+int rnnt_engine_decode_f32(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream);
 
 /* ---- in-run measurement (bench.py's roofline leg): HIP events recorded on the launch stream
  * around each call's encoder kernels and decoder kernels; rnnt_engine_get_stats synchronises

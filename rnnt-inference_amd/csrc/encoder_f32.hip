@@ -13,47 +13,9 @@
 // one layer x one timestep; workgroup = 4 waves x (16 gate rows) x 64 batch rows.
 #include "rnnt_device.hpp"
 #include "encoder_f32.hpp"
+#include "chain_f32.hpp"
 
 namespace rnnt {
-
-#define MFMA4(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
-
-// acc[j] += chain over k in [0, K) of A(row) . B_j, K a multiple of 16; a/b point at this
-// lane's first element (row base + 8q); blocks of 32 feed 8 MFMAs, a final half block 4.
-__device__ __forceinline__ void chain_rows(const float* __restrict__ a, const float* const* b, int K, v4f* acc) {
-  const int nb = K >> 5;
-  for (int blk = 0; blk < nb; ++blk) {
-    const float4 a0 = *(const float4*)(a + 32 * blk), a1 = *(const float4*)(a + 32 * blk + 4);
-    float4 b0[4], b1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      b0[j] = *(const float4*)(b[j] + 32 * blk);
-      b1[j] = *(const float4*)(b[j] + 32 * blk + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[j] = MFMA4(a0.x, b0[j].x, acc[j]);
-      acc[j] = MFMA4(a0.y, b0[j].y, acc[j]);
-      acc[j] = MFMA4(a0.z, b0[j].z, acc[j]);
-      acc[j] = MFMA4(a0.w, b0[j].w, acc[j]);
-      acc[j] = MFMA4(a1.x, b1[j].x, acc[j]);
-      acc[j] = MFMA4(a1.y, b1[j].y, acc[j]);
-      acc[j] = MFMA4(a1.z, b1[j].z, acc[j]);
-      acc[j] = MFMA4(a1.w, b1[j].w, acc[j]);
-    }
-  }
-  if (K & 16) {  // half block: instructions i = 0..3 (k = 32 nb + 4i + q)
-    const float4 a0 = *(const float4*)(a + 32 * nb);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 b0 = *(const float4*)(b[j] + 32 * nb);
-      acc[j] = MFMA4(a0.x, b0.x, acc[j]);
-      acc[j] = MFMA4(a0.y, b0.y, acc[j]);
-      acc[j] = MFMA4(a0.z, b0.z, acc[j]);
-      acc[j] = MFMA4(a0.w, b0.w, acc[j]);
-    }
-  }
-}
 
 __global__ void __launch_bounds__(256) lstm_f32_step_kernel(EncF32StepArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
@@ -100,7 +62,9 @@ __global__ void __launch_bounds__(256) lstm_f32_step_kernel(EncF32StepArgs a) {
       dst[a.half * H] = a.t < a.lens[n] ? hh : 0.0f;
       if (a.zero_next) dst[H] = 0.0f;
     } else {
-      a.y[(size_t)n * H + u] = hh;
+      if (a.y) a.y[(size_t)n * H + u] = hh;
+      if (a.y2) a.y2[(size_t)n * H + chain_pos(u)] = hh;
+      if (a.ybf) a.ybf[(size_t)n * H + u] = f2bf_ftz(hh);
     }
   }
 }

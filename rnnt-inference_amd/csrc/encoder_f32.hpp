@@ -18,6 +18,9 @@ struct EncF32StepArgs {
   float* c;             // [n_pad][1024] natural
   float* y;             // NEXT: [n_pad][1024] chain-permuted; STACKED: [n_pad][2048] chain-permuted;
                         // FINAL: [n_pad][1024] natural (f)
+  float* y2;            // FINAL: optional second copy of f, [n_pad][1024] chain-permuted (fp32 decoder input)
+  uint16_t* ybf;        // FINAL: optional bf16 copy of f, [n_pad][1024] natural, subnormals flushed
+                        // (the f32 + enable_bf16 decoder input, decoder.py:121-122)
   const int32_t* lens;  // STACKED masking
   int I, Ip;            // real / padded input width (240/256, 1024/1024, 2048/2048)
   int n;                // rows to compute (multiple-of-64 tiles launched; rows >= n skipped)

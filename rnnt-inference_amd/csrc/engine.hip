@@ -19,6 +19,7 @@
 #include "encoder.hpp"
 #include <hip/hip_ext.h>
 #include "encoder_f32.hpp"
+#include "decoder_f32.hpp"
 #include "rnnt_device.hpp"
 
 using namespace rnnt;
@@ -81,6 +82,13 @@ struct rnnt_engine {
   std::vector<void*> f32_ws;
   size_t f32_ws_T = 0, f32_ws_np = 0;
   float *f32_x = nullptr, *f32_ya = nullptr, *f32_xs = nullptr, *f32_yb = nullptr, *f32_h[2] = {}, *f32_c = nullptr;
+  // fp32 decoder (rnnt_engine_load_f32_decoder) and the last fp32 encode's outputs it decodes
+  bool f32_dec_loaded = false;
+  DecF32Weights dw32{};
+  float *f32_fc = nullptr, *f32_F = nullptr;
+  int32_t* f32_flen = nullptr;
+  DecF32State ds32{};
+  int last32_T = 0, last32_n = 0, last32_npad = 0;
   // operator-level decode: unfinished-row counter for greedy_decode_update's return value
   int32_t* op_count = nullptr;
   int32_t* op_count_host = nullptr;
@@ -638,7 +646,25 @@ static int f32_workspace(rnnt_engine* e, int T, int n_pad) {
     *p = (float*)q;
     return 0;
   };
+  auto ali = [&](int32_t** p, size_t count) -> int {
+    float* q = nullptr;
+    const int rr = al(&q, count);
+    *p = (int32_t*)q;
+    return rr;
+  };
+  const size_t NP = (size_t)n_pad * P;
   int r = al(&e->f32_x, (size_t)T * n_pad * FEAT);
+  if (!r) r = al(&e->f32_fc, Tp * NH);
+  if (!r) r = al(&e->f32_F, Tp * n_pad * J);
+  if (!r) r = ali(&e->f32_flen, n_pad);
+  if (!r) r = al(&e->ds32.ph, 2 * NP);
+  if (!r) r = al(&e->ds32.pc, 2 * NP);
+  if (!r) r = al(&e->ds32.gh, 2 * NP);
+  if (!r) r = al(&e->ds32.gc, 2 * NP);
+  int32_t** ints[] = {&e->ds32.time, &e->ds32.added, &e->ds32.idx, &e->ds32.preg, &e->ds32.fin};
+  for (auto pp : ints)
+    if (!r) r = ali(pp, n_pad);
+  if (!r) r = ali(&e->ds32.unfinished, 4);
   if (!r) r = al(&e->f32_ya, (size_t)T * NH);
   if (!r) r = al(&e->f32_xs, Tp * NH * 2);
   if (!r) r = al(&e->f32_yb, Tp * NH);
@@ -681,7 +707,11 @@ static int run_f32_layer(rnnt_engine* e, int l, int T, int n, int n_pad, const f
       a.half = t & 1;
       a.zero_next = ((t & 1) == 0 && t + 1 == stacked_T);
     } else {
-      a.y = y + (size_t)t * NH;
+      a.y = y ? y + (size_t)t * NH : nullptr;
+      if (mode == ENC_F32_FINAL) {  // the decoders' copies of f: chain-permuted fp32, and bf16
+        a.y2 = e->f32_fc + (size_t)t * NH;
+        a.ybf = e->fbf && n_pad <= e->np_max && t < e->tp_max ? e->fbf + (size_t)t * NH : nullptr;
+      }
     }
     if (launch_lstm_f32_step(a, st)) return fail(RNNT_EDEVICE, "fp32 lstm step launch failed");
   }
@@ -690,14 +720,15 @@ static int run_f32_layer(rnnt_engine* e, int l, int T, int n, int n_pad, const f
 
 extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const int32_t* lens, int T, int n, int n_pad,
                                       float* f_out, void* stream) {
-  if (!e || !feats || !lens || !f_out) return fail(RNNT_EINVAL, "null argument");
+  if (!e || !feats || !lens) return fail(RNNT_EINVAL, "null argument");
   if (!e->f32_loaded) return fail(RNNT_EINVAL, "fp32 encoder weights not loaded (rnnt_engine_load_f32_encoder)");
   if (T <= 0 || T > e->opts.max_frames || n <= 0 || n_pad < n || n_pad % 64)
     return fail(RNNT_EINVAL, "T / n / n_pad out of range (n_pad a multiple of 64)");
   DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
-  int r = f32_workspace(e, T, n_pad);
+  int r = state_acquire(e, st);
   if (r) return r;
+  if ((r = f32_workspace(e, T, n_pad))) return r;
   const int Tp = (T + 1) / 2;
   if (launch_permute_feats(feats, (int64_t)T * n_pad, e->f32_x, st)) return fail(RNNT_EDEVICE, "permute launch failed");
   // Transcription.forward (modeling_rnnt.py:116-144): pre_rnn 2 layers -> StackTime -> post_rnn 3 layers
@@ -706,7 +737,107 @@ extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const 
   if ((r = run_f32_layer(e, 2, Tp, n, n_pad, e->f32_xs, ENC_F32_NEXT, e->f32_yb, lens, Tp, st))) return r;
   if ((r = run_f32_layer(e, 3, Tp, n, n_pad, e->f32_yb, ENC_F32_NEXT, e->f32_ya, lens, Tp, st))) return r;
   if ((r = run_f32_layer(e, 4, Tp, n, n_pad, e->f32_ya, ENC_F32_FINAL, f_out, lens, Tp, st))) return r;
+  // f_lens = ceil(lens / 2) for both decoders; the bf16 copy of f (written when the batch fits
+  // the int8 workspace) lets rnnt_engine_decode run the f32 + enable_bf16 decoder on it
+  hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->f32_flen, n_pad);
+  HIPCHK(hipGetLastError());
+  e->last32_T = T;
+  e->last32_n = n;
+  e->last32_npad = n_pad;
+  if (n_pad <= e->np_max && Tp <= e->tp_max) {
+    hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->flen, n_pad);
+    HIPCHK(hipGetLastError());
+    e->last_T = T;
+    e->last_n = n;
+    e->last_npad = n_pad;
+  } else {
+    e->last_n = 0;  // no bf16 copy: rnnt_engine_decode refuses until the next encode
+  }
+  return state_release(e, st);
+}
+
+extern "C" int rnnt_engine_load_f32_decoder(rnnt_engine* e, const rnnt_f32_decoder_desc* m) {
+  if (!e || !m || !m->embed || !m->joint_w1t || !m->joint_w1p || !m->joint_bt || !m->joint_bp || !m->joint_w2 ||
+      !m->joint_b2)
+    return fail(RNNT_EINVAL, "null argument");
+  DEVICE_SCOPE(e->device);
+  std::vector<float> emb((size_t)29 * P, 0.0f);  // row 28: SOS (zero embedding)
+  for (int g = 0; g < 28; ++g)
+    for (int k = 0; k < P; ++k) emb[(size_t)g * P + chain_pos(k)] = m->embed[(size_t)g * P + k];
+  float* p = nullptr;
+  int r = upload(e, &p, emb);
+  if (r) return r;
+  e->dw32.emb = p;
+  for (int l = 0; l < 2; ++l) {
+    if (!m->pred_w_ih[l] || !m->pred_w_hh[l] || !m->pred_b_ih[l] || !m->pred_b_hh[l])
+      return fail(RNNT_EINVAL, "null fp32 prediction weight");
+    std::vector<float> wi((size_t)PG4 * P), wh((size_t)PG4 * P), bi(PG4), bh(PG4);
+    for (int g = 0; g < 4; ++g)
+      for (int u = 0; u < P; ++u) {
+        const int src = g * P + u, dst = 4 * u + g;  // gate-interleaved rows
+        for (int k = 0; k < P; ++k) {
+          wi[(size_t)dst * P + chain_pos(k)] = m->pred_w_ih[l][(size_t)src * P + k];
+          wh[(size_t)dst * P + chain_pos(k)] = m->pred_w_hh[l][(size_t)src * P + k];
+        }
+        bi[dst] = m->pred_b_ih[l][src];
+        bh[dst] = m->pred_b_hh[l][src];
+      }
+    float *a, *b, *c, *d;
+    if ((r = upload(e, &a, wi)) || (r = upload(e, &b, wh)) || (r = upload(e, &c, bi)) || (r = upload(e, &d, bh))) return r;
+    e->dw32.wih[l] = a;
+    e->dw32.whh[l] = b;
+    e->dw32.bih[l] = c;
+    e->dw32.bhh[l] = d;
+  }
+  auto chained = [](const float* src, int rows, int rows_pad, int K) {
+    std::vector<float> w((size_t)rows_pad * K, 0.0f);
+    for (int i = 0; i < rows; ++i)
+      for (int k = 0; k < K; ++k) w[(size_t)i * K + chain_pos(k)] = src[(size_t)i * K + k];
+    return w;
+  };
+  float *w1t, *w1p, *bt, *bp, *w2, *b2;
+  std::vector<float> b2v(NLAB_PAD, 0.0f);
+  std::copy(m->joint_b2, m->joint_b2 + NLAB, b2v.begin());
+  if ((r = upload(e, &w1t, chained(m->joint_w1t, J, J, H))) || (r = upload(e, &w1p, chained(m->joint_w1p, J, J, P))) ||
+      (r = upload(e, &w2, chained(m->joint_w2, NLAB, NLAB_PAD, J))) ||
+      (r = upload(e, &bt, std::vector<float>(m->joint_bt, m->joint_bt + J))) ||
+      (r = upload(e, &bp, std::vector<float>(m->joint_bp, m->joint_bp + J))) || (r = upload(e, &b2, b2v)))
+    return r;
+  e->dw32.w1t = w1t;
+  e->dw32.w1p = w1p;
+  e->dw32.bt = bt;
+  e->dw32.bp = bp;
+  e->dw32.w2 = w2;
+  e->dw32.b2 = b2;
+  e->f32_dec_loaded = true;
   return 0;
+}
+
+extern "C" int rnnt_engine_decode_f32(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream) {
+  if (!e || !res || !res_len) return fail(RNNT_EINVAL, "null argument");
+  if (!e->f32_dec_loaded) return fail(RNNT_EINVAL, "fp32 decoder weights not loaded (rnnt_engine_load_f32_decoder)");
+  if (e->last32_n <= 0) return fail(RNNT_EINVAL, "decode_f32 before encode_f32");
+  if (max_res <= 0) return fail(RNNT_EINVAL, "max_res must be positive");
+  DEVICE_SCOPE(e->device);
+  hipStream_t st = pick(e, stream);
+  int r = state_acquire(e, st);
+  if (r) return r;
+  const int Tp = (e->last32_T + 1) / 2;
+  if (launch_f32_joint_trans(e->dw32, e->f32_fc, e->f32_F, Tp, e->last32_npad, st))
+    return fail(RNNT_EDEVICE, "fp32 joint_trans launch failed");
+  DecF32Args a{};
+  a.w = e->dw32;
+  a.s = e->ds32;
+  a.F = e->f32_F;
+  a.f_lens = e->f32_flen;
+  a.res = res;
+  a.res_len = res_len;
+  a.N = e->last32_n;
+  a.Npad = e->last32_npad;
+  a.max_res = max_res;
+  a.max_iter = Tp * (MAXSYM + 1) + 2;
+  if (launch_greedy_decode_f32(a, e->host_flags, e->poll_ev, st) < 0) return fail(RNNT_EDEVICE, "fp32 greedy launch failed");
+  return state_release(e, st);
 }
 
 // ---------------------------------------------------------------- operator-level decode

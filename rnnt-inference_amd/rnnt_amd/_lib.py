@@ -39,6 +39,13 @@ class RnntStats(C.Structure):
                 ("step_launches", C.c_int64), ("decode_steps", C.c_int64), ("encode_calls", C.c_int64), ("decode_calls", C.c_int64)]
 
 
+class RnntF32DecoderDesc(C.Structure):
+    _fields_ = [("embed", C.c_void_p), ("pred_w_ih", C.c_void_p * 2), ("pred_w_hh", C.c_void_p * 2),
+                ("pred_b_ih", C.c_void_p * 2), ("pred_b_hh", C.c_void_p * 2), ("joint_w1t", C.c_void_p),
+                ("joint_w1p", C.c_void_p), ("joint_bt", C.c_void_p), ("joint_bp", C.c_void_p),
+                ("joint_w2", C.c_void_p), ("joint_b2", C.c_void_p)]
+
+
 class RnntFeaturizerConfig(C.Structure):
     _fields_ = [("sample_rate", C.c_int), ("n_fft", C.c_int), ("win_length", C.c_int), ("hop_length", C.c_int),
                 ("nfilt", C.c_int), ("frame_splicing", C.c_int), ("pad_out_feat", C.c_int),
@@ -71,6 +78,8 @@ _SIGS = {
                                                C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "rnnt_engine_encode_f32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                          C.c_void_p]),
+    "rnnt_engine_load_f32_decoder": (C.c_int, [C.c_void_p, C.POINTER(RnntF32DecoderDesc)]),
+    "rnnt_engine_decode_f32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "rnnt_engine_infer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "rnnt_op_lstm_int8": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,

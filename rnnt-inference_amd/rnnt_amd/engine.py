@@ -35,7 +35,8 @@ def _ptr(t):
 class Engine:
     def __init__(self, pm: PreparedModel, device=0, max_batch=1024, max_frames=R.MAX_FEA_LEN, max_res=None):
         if not pm.bf16:
-            raise ValueError("the engine runs the int8 encoder + bf16 prediction/joint path (enable_bf16)")
+            raise ValueError("the engine is created from the int8 + bf16 model (enable_bf16); the fp32 path is "
+                             "loaded on top with load_f32_encoder / load_f32_decoder")
         lib = _lib.lib()
         self.device = device
         self.max_frames = max_frames
@@ -110,11 +111,42 @@ class Engine:
         arrs = [(C.c_void_p * 5)(*[a.ctypes.data for a in col]) for col in keep]
         _lib.check(self._lib.rnnt_engine_load_f32_encoder(self._h, *arrs), "rnnt_engine_load_f32_encoder")
 
-    def encode_f32(self, feats, lens, n, f_out, stream=None):
+    def load_f32_decoder(self, pm32):
+        """fp32 prediction / joint weights (a PreparedModel built with bf16=False, natural
+        layouts) for decode_f32 -- the run_mode="f32" decoder without enable_bf16."""
+        if pm32.bf16:
+            raise ValueError("load_f32_decoder takes the fp32 PreparedModel (prepare_model(..., bf16=False))")
+        keep = []
+
+        def arr(a):
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            keep.append(a)
+            return a.ctypes.data
+
+        d = _lib.RnntF32DecoderDesc()
+        d.embed = arr(pm32.embed)
+        for l in range(2):
+            d.pred_w_ih[l] = arr(pm32.pred_wih[l])
+            d.pred_w_hh[l] = arr(pm32.pred_whh[l])
+            d.pred_b_ih[l] = arr(pm32.pred_bih[l])
+            d.pred_b_hh[l] = arr(pm32.pred_bhh[l])
+        d.joint_w1t, d.joint_w1p = arr(pm32.w1t), arr(pm32.w1p)
+        d.joint_bt, d.joint_bp = arr(pm32.bt), arr(pm32.bp)
+        d.joint_w2, d.joint_b2 = arr(pm32.w2), arr(pm32.b2)
+        _lib.check(self._lib.rnnt_engine_load_f32_decoder(self._h, C.byref(d)), "rnnt_engine_load_f32_decoder")
+
+    def decode_f32(self, res, res_len, stream=None):
+        """fp32 greedy decode of the last encode_f32 output: res cuda int32 [n, max_res], res_len [n]."""
+        rc = self._lib.rnnt_engine_decode_f32(self._h, _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_decode_f32")
+
+    def encode_f32(self, feats, lens, n, f_out=None, stream=None):
         """Transcription in fp32 (config 2): feats cuda fp32 [T, n_pad, 256], lens cuda int32
-        [n_pad] -> f_out cuda fp32 [ceil(T/2), n_pad, 1024]."""
+        [n_pad] -> f_out cuda fp32 [ceil(T/2), n_pad, 1024] (optional).  The engine keeps f for
+        decode_f32 and, when n_pad fits the int8 workspace, a bf16 copy for decode (the
+        f32 + enable_bf16 decoder)."""
         T, n_pad, ch = feats.shape
-        assert ch == R.PADDED_INPUT_SIZE and feats.is_contiguous() and f_out.is_contiguous()
+        assert ch == R.PADDED_INPUT_SIZE and feats.is_contiguous() and (f_out is None or f_out.is_contiguous())
         rc = self._lib.rnnt_engine_encode_f32(self._h, _ptr(feats), _ptr(lens), T, n, n_pad, _ptr(f_out),
                                               _stream_handle(stream))
         _lib.check(rc, "rnnt_engine_encode_f32")
