@@ -1,0 +1,118 @@
+"""The north_star accuracy criteria on the GPU:
+
+* "joint logits within a stated fp tolerance": teacher-forced, the bf16 decoder (the engine's
+  lstm_amx_bf16 / amx_linear_bf16_accum_relu / amx_linear_i16o32 operators) and the fp32
+  decoder (CPU restatement, fp32 weights) see the same int8 encoder frame and the same emitted
+  history at every step.  Stated tolerance:
+      max_j |L_bf16[j] - L_fp32[j]| <= 0.1 + 0.01 * max_j |L_fp32[j]|    at every step,
+  and the argmax agrees wherever the fp32 top-2 margin exceeds twice that tolerance.
+  Checked on the throughput model and on the well-conditioned planted model.
+* "WER within 1 % of fp32": on the planted model (rnnt_amd.planted: contractive encoder,
+  confident joint -- a trained model's regime), int8 encoder + bf16 decoder vs fp32 encoder +
+  fp32 decoder, both on the GPU, WER <= 1 %.
+"""
+import numpy as np
+import pytest
+import torch
+
+from rnnt_amd import accuracy, planted, synthetic, weights
+
+pytestmark = pytest.mark.gpu
+
+TOL_ABS, TOL_REL = 0.1, 0.01
+
+
+@pytest.fixture(scope="module")
+def planted_model():
+    ckpt, task = planted.make_planted_checkpoint()
+    lens = np.minimum(synthetic.devclean_lengths(8, seed=91), 300)
+    feats, _ = planted.planted_features(task, lens, seed=92)
+    x = np.zeros((int(lens.max()), 8, 240), np.float32)
+    for i, fe in enumerate(feats):
+        x[: len(fe), i] = fe
+    amax = weights.calibrate_amax(weights.migrate_state_dict(ckpt), x, lens)
+    return ckpt, task, amax
+
+
+def _encode_i8(e, x, lens, n_pad=256):
+    n = x.shape[1]
+    xp = np.zeros((x.shape[0], n_pad, 256), np.float32)
+    xp[:, :n, : x.shape[2]] = x
+    lp = np.zeros(n_pad, np.int32)
+    lp[:n] = lens
+    f = torch.empty(((x.shape[0] + 1) // 2, n_pad, 1024), dtype=torch.float32, device="cuda")
+    e.encode(torch.from_numpy(xp).cuda(), torch.from_numpy(lp).cuda(), lens, n=n, f_out=f)
+    torch.cuda.synchronize()
+    return f.cpu().numpy()[:, :n]
+
+
+def _check_tolerance(L16, L32):
+    d = np.abs(L16 - L32).max(1)
+    tol = TOL_ABS + TOL_REL * np.abs(L32).max(1)
+    assert (d <= tol).all(), f"{int((d > tol).sum())} of {len(d)} steps exceed the logit tolerance (max {d.max():.4f})"
+    s = np.sort(L32, 1)
+    clear = (s[:, -1] - s[:, -2]) > 2 * tol
+    agree = L16.argmax(1) == L32.argmax(1)
+    assert agree[clear].all(), "argmax differs at a step with a clear fp32 margin"
+    return float(agree.mean()), float(clear.mean())
+
+
+def _teacher_forced(pm, ckpt, x, lens):
+    from rnnt_amd.engine import Engine
+    from tools.joint_tolerance import teacher_forced
+    pm32 = weights.prepare_model(ckpt, pm.amax, bf16=False)
+    e = Engine(pm, device=0, max_batch=256, max_frames=int(lens.max()))
+    try:
+        f = _encode_i8(e, x, lens)
+        return teacher_forced(e, pm, pm32, f, lens)
+    finally:
+        e.close()
+
+
+def test_joint_logits_within_tolerance_throughput_model(pm_golden, ckpt):
+    lens = np.minimum(synthetic.devclean_lengths(16, seed=31), 200).astype(np.int32)
+    x = synthetic.make_features(int(lens.max()), 16, seed=32, lens=lens)
+    r = _teacher_forced(pm_golden, ckpt, x, lens)
+    agree, clear = _check_tolerance(r["L16"], r["L32"])
+    assert len(r["L16"]) > 1000 and agree > 0.98
+
+
+def test_joint_logits_within_tolerance_planted_model(planted_model):
+    ckpt, task, amax = planted_model
+    pm = weights.prepare_model(ckpt, amax, bf16=True)
+    lens = np.minimum(synthetic.devclean_lengths(16, seed=33), 240).astype(np.int32)
+    feats, _ = planted.planted_features(task, lens, seed=34)
+    x = np.zeros((int(lens.max()), 16, 240), np.float32)
+    for i, fe in enumerate(feats):
+        x[: len(fe), i] = fe
+    r = _teacher_forced(pm, ckpt, x, lens)
+    agree, clear = _check_tolerance(r["L16"], r["L32"])
+    assert len(r["L16"]) > 500 and clear > 0.95 and agree > 0.99
+
+
+def test_wer_int8_bf16_vs_fp32_planted_model(planted_model):
+    """The north_star's 'WER within 1 % of fp32 reference' on the well-conditioned model."""
+    from rnnt_amd.decoder import GreedyDecoder
+    from rnnt_amd.model import RNNT
+    ckpt, task, amax = planted_model
+    n = 128
+    lens = synthetic.devclean_lengths(n, seed=35)
+    feats, truth = planted.planted_features(task, lens, seed=36)
+    x = np.zeros((int(lens.max()), n, 240), np.float32)
+    for i, fe in enumerate(feats):
+        x[: len(fe), i] = fe
+    xd, ld = torch.from_numpy(x).cuda(), torch.from_numpy(lens)
+    hyp = {}
+    for mode in ("quant", "f32"):
+        m = RNNT(ckpt, mode, enable_bf16=(mode == "quant"), amax=amax)
+        dec = GreedyDecoder(m, mode, mode == "quant", batch_size=n)
+        res, rl = dec(xd, ld)
+        res, rl = res.cpu().numpy(), rl.cpu().numpy()
+        hyp[mode] = [accuracy.seq_to_sen(res[i], rl[i]) for i in range(n)]
+        dec.close()
+    ref_truth = ["".join(accuracy.LABELS[c] for c in t) for t in truth]
+    wer, errs, words = accuracy.word_error_rate(hyp["quant"], hyp["f32"])
+    wer_truth, _, _ = accuracy.word_error_rate(hyp["f32"], ref_truth)
+    assert words > 300
+    assert wer_truth < 0.05, f"the planted fp32 model should transcribe its own task ({wer_truth:.3f})"
+    assert wer <= 0.01, f"int8+bf16 vs fp32 WER {wer:.4f} ({errs}/{words})"
