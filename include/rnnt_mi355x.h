@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RNNT_ABI_VERSION 5
+#define RNNT_ABI_VERSION 6
 
 #define RNNT_OK 0
 #define RNNT_EINVAL (-22)
@@ -78,9 +78,31 @@ const char* rnnt_last_error(void);
 int rnnt_stream_create(int device, const uint32_t* cu_mask, int mask_words, void** out);
 int rnnt_stream_destroy(void* stream);
 
-/* Packs the model into the engine's device layouts on `device` and sizes the workspace. */
+/* Packs the model into the engine's device layouts on `device` and sizes the workspace.
+ * model == NULL gives an engine without weights: its components are loaded with the
+ * rnnt_engine_load_* calls below (the operator library does this from the tensors the
+ * TorchScript graph passes); a compute call whose component is missing fails with RNNT_EINVAL. */
 int rnnt_engine_create(const rnnt_model_desc* model, int device, const rnnt_opts* opts, rnnt_engine** out);
 void rnnt_engine_destroy(rnnt_engine* e);
+
+/* The packed model file written by tools/export_model.py (rnnt_amd.weights.save_engine_file):
+ * the rnnt_model_desc arrays in a flat little-endian container -- magic "RNNTMI01", u32 version 1,
+ * u32 entry count, then per entry {char name[48]; u32 dtype (0 int8, 1 fp32, 2 bf16 bits);
+ * u32 ndim; u64 shape[4]; u64 offset; u64 nbytes}, data 64-byte aligned.  Replaces the
+ * reference's torch::jit::load of the calibrated TorchScript model (csrc/rnnt_model.hpp:41-54). */
+int rnnt_engine_create_from_file(const char* path, int device, const rnnt_opts* opts, rnnt_engine** out);
+
+/* Component loaders (natural layouts as in rnnt_model_desc); a reload overwrites the component in
+ * place after synchronising the device.  Encoder layers [first, first + count): w[i], bq[i],
+ * rb[i], in_s[i], out_s[i] for layer first + i (iLSTM.weights / rb_scale / in_scale / out_scale,
+ * quant_lstm.py:92-101).  Prediction: embed may be NULL (operator-level use; the fused decode
+ * needs it).  Joint: linear1 (w1t, w1p, bt, bp) and linear2 (w2 [29][512], b2 [29]). */
+int rnnt_engine_load_encoder_layers(rnnt_engine* e, int first, int count, const int8_t* const* w,
+                                    const float* const* bq, const float* rb, const float* in_s, const float* out_s);
+int rnnt_engine_load_prediction(rnnt_engine* e, const uint16_t* embed, const uint16_t* const* w_ih,
+                                const uint16_t* const* w_hh, const float* const* b_ih, const float* const* b_hh);
+int rnnt_engine_load_joint(rnnt_engine* e, const uint16_t* w1t, const uint16_t* w1p, const float* bt, const float* bp);
+int rnnt_engine_load_joint_out(rnnt_engine* e, const uint16_t* w2, const float* b2);
 
 /* Encoder: feats device fp32 [T][n_pad][256] (the QSL's AssembleSamples layout, rnnt_qsl.cpp:150-188,
  * zero past lens and in channels 240..255), lens device int32 [n_pad] (0 for batch padding), lens_host
@@ -181,15 +203,19 @@ int rnnt_op_joint_hidden(rnnt_engine* e, const float* f, const uint16_t* g, uint
 /* amx_linear_i16o32 (modeling_rnnt.py:280-283): y1 bf16 [n_pad][512] -> logits fp32 [n_pad][32]
  * (labels 29..31 are zero padding, as the reference's padded linear2). */
 int rnnt_op_joint_logits(rnnt_engine* e, const uint16_t* y1, float* logits, int n_pad, void* stream);
-/* greedy_decode_update (modeling_rnnt.py:331-365; spec decoder.py:125-167), in place on the
- * device state; `finish` int32 [n] is the spec's self.finish (decoder.py:106).  f fp32
- * [T'][n_pad][1024], fi fp32 [n_pad][1024], pre_hg/hg bf16 and pre_cg/cg fp32 [2][n_pad][320],
- * res int32 [n][max_res].  Synchronises the stream; returns 1 when every row has finished, 0
- * otherwise, or a negative error code. */
-int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int32_t* symbols_added, int32_t* res,
-                          int32_t* res_idx, const float* f, const int32_t* f_lens, int32_t* time_idx, float* fi,
-                          int32_t* pre_g, uint16_t* pre_hg, float* pre_cg, const uint16_t* hg, const float* cg,
-                          int32_t* finish, int n, int n_pad, int max_res, void* stream);
+/* greedy_decode_update (modeling_rnnt.py:331-365; spec decoder.py:125-167), in place, on the
+ * reference's own operands (the C++ decode loop's tensors, rnnt_model.hpp:92-124): symbols [n]
+ * (int64 from torch.argmax when symbols_i64, else int32), symbols_added / res_idx / time_idx /
+ * pre_g int32 [n], res int32 [n][max_res], f fp32 [Tp][f_batch][1024], f_lens int32 [n], fi fp32
+ * [n][1024], pre_hg[l] / hg[l] bf16 [n][320], pre_cg[l] / cg[l] fp32 [n][320] (l = 0, 1).  The
+ * spec's per-row `finish` (decoder.py:106) is carried in time_idx: a row is finished once
+ * time_idx >= f_lens (left unclamped when it finishes; fi is gathered at min(time, f_len - 1)).
+ * Synchronises the stream; returns 1 when every row has finished (the op's bool), 0 otherwise, or
+ * a negative error code. */
+int rnnt_op_greedy_update(rnnt_engine* e, const void* symbols, int symbols_i64, int32_t* symbols_added, int32_t* res,
+                          int32_t* res_idx, const float* f, int f_batch, const int32_t* f_lens, int32_t* time_idx,
+                          float* fi, int32_t* pre_g, uint16_t* const* pre_hg, float* const* pre_cg,
+                          const uint16_t* const* hg, const float* const* cg, int n, int max_res, void* stream);
 
 /* ---- audio front end (the reference's AudioProcessor / FilterbankFeatures.forward,
  * datasets/parts/features.py:185-252, csrc/rnnt_processor.hpp:29-48; used when WAV=true,

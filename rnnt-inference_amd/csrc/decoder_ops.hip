@@ -127,12 +127,14 @@ __global__ void __launch_bounds__(256) op_joint_logits_kernel(DecWeights w, cons
   }
 }
 
-// greedy_decode_update (spec: decoder.py:125-167), one thread per row.
+// greedy_decode_update (spec: decoder.py:125-167), one thread per row; finished = time_idx >=
+// f_lens (see GreedyUpdateArgs).
 __global__ void op_greedy_update_kernel(GreedyUpdateArgs a) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= a.n) return;
-  if (a.finish[n]) return;
-  const int sym = a.symbols[n];
+  const int fl = a.f_lens[n];
+  if (a.time_idx[n] >= fl) return;  // finished
+  const int sym = a.sym64 ? (int)((const int64_t*)a.symbols)[n] : ((const int32_t*)a.symbols)[n];
   if (sym != BLANK && a.symbols_added[n] != MAXSYM) {  // 4. emit
     const int id = ++a.res_idx[n];
     if (id < a.max_res) a.res[(size_t)n * a.max_res + id] = sym;
@@ -140,21 +142,15 @@ __global__ void op_greedy_update_kernel(GreedyUpdateArgs a) {
     a.pre_g[n] = sym;
     for (int l = 0; l < 2; ++l)
       for (int k = 0; k < P; ++k) {
-        const size_t o = ((size_t)l * a.n_pad + n) * P + k;
-        a.pre_hg[o] = a.hg[o];
-        a.pre_cg[o] = a.cg[o];
+        const size_t o = (size_t)n * P + k;
+        a.pre_hg[l][o] = a.hg[l][o];
+        a.pre_cg[l][o] = a.cg[l][o];
       }
   } else {  // 5. advance
-    const int fl = a.f_lens[n];
-    int t = a.time_idx[n] + 1;
-    if (t >= fl) {
-      a.finish[n] = 1;
-      atomicSub(a.unfinished, 1);
-    }
-    const int eos = fl > 0 ? fl - 1 : 0;
-    if (t > eos) t = eos;
-    a.time_idx[n] = t;
-    for (int k = 0; k < H; ++k) a.fi[(size_t)n * H + k] = a.f[((size_t)t * a.n_pad + n) * H + k];
+    const int t = a.time_idx[n] + 1;
+    a.time_idx[n] = t;  // t >= fl: finished (the spec's finish |= time >= f_lens)
+    const int tf = t < fl ? t : fl - 1;  // the spec clamps time to eos before the gather
+    for (int k = 0; k < H; ++k) a.fi[(size_t)n * H + k] = a.f[((size_t)tf * a.f_batch + n) * H + k];
     a.symbols_added[n] = 0;
   }
 }

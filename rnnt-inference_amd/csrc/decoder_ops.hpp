@@ -7,23 +7,28 @@
 
 namespace rnnt {
 
+// greedy_decode_update's operands in the reference's own shapes (modeling_rnnt.py:351-365,
+// rnnt_model.hpp:92-124): per-layer state tensors, f [Tp][f_batch][1024].  The spec's per-row
+// `finish` flag (decoder.py:106) is not an operand of the reference op; it is carried in
+// time_idx: a row is finished once time_idx >= f_lens (time_idx is left unclamped when the row
+// finishes, so f_lens == 0 rows are finished from the start, as decoder.py:106 has it).
 struct GreedyUpdateArgs {
-  const int32_t* symbols;  // [n] argmax of the joint
+  const void* symbols;     // [n] argmax of the joint (int64 from torch.argmax, or int32)
+  bool sym64;
   int32_t* symbols_added;  // [n]
   int32_t* res;            // [n][max_res]
   int32_t* res_idx;        // [n]
-  const float* f;          // [Tp][n_pad][1024] encoder output
+  const float* f;          // [Tp][f_batch][1024] encoder output
+  int f_batch;
   const int32_t* f_lens;   // [n]
   int32_t* time_idx;       // [n]
-  float* fi;               // [n_pad][1024] current frame rows
+  float* fi;               // [n][1024] current frame rows
   int32_t* pre_g;          // [n]
-  uint16_t* pre_hg;        // bf16 [2][n_pad][320]
-  float* pre_cg;           // [2][n_pad][320]
-  const uint16_t* hg;      // bf16 [2][n_pad][320] candidate state
-  const float* cg;         // [2][n_pad][320]
-  int32_t* finish;         // [n] (decoder.py:106 `self.finish`)
-  int32_t* unfinished;     // device counter of rows not finished (decremented here)
-  int n, n_pad, max_res;
+  uint16_t* pre_hg[2];     // bf16 [n][320] per layer
+  float* pre_cg[2];        // [n][320]
+  const uint16_t* hg[2];   // bf16 [n][320] candidate state
+  const float* cg[2];      // [n][320]
+  int n, max_res;
 };
 
 int launch_op_lstm_bf16(const DecWeights& w, int layer, const uint16_t* x, const uint16_t* h_in, const float* c_in,

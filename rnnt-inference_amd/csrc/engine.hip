@@ -92,6 +92,9 @@ struct rnnt_engine {
   // operator-level decode: unfinished-row counter for greedy_decode_update's return value
   int32_t* op_count = nullptr;
   int32_t* op_count_host = nullptr;
+  // which model components are on the device (rnnt_engine_create with a model loads all)
+  int enc_loaded = 0;  // bit l: encoder layer l
+  bool pred_loaded = false, xtab_ok = false, joint1_loaded = false, joint2_loaded = false;
 };
 
 static hipEvent_t new_event(hipStream_t st) {
@@ -144,84 +147,142 @@ extern "C" int rnnt_stream_destroy(void* stream) {
   return RNNT_OK;
 }
 
-// ---- packing (natural layouts -> device layouts; see DESIGN.md "Data layout in HBM")
-static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
-  for (int l = 0; l < 5; ++l) {
-    if (!m->enc_w[l] || !m->enc_bq[l]) return fail(RNNT_EINVAL, "null encoder weight");
+// ---- packing (natural layouts -> device layouts; see DESIGN.md "Data layout in HBM").
+// Each model component has a fixed-size device buffer, allocated on its first load and
+// overwritten in place by a reload (the operator library reloads a component when the weight
+// tensors it is called with change; the device is synchronised first so no kernel still reads
+// the old copy).
+template <class T>
+static int load_buf(rnnt_engine* e, T** p, const std::vector<T>& host) {
+  if (!*p) return upload(e, p, host);
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(*p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+extern "C" int rnnt_engine_load_encoder_layers(rnnt_engine* e, int first, int count, const int8_t* const* w,
+                                               const float* const* bq, const float* rb, const float* in_s,
+                                               const float* out_s) {
+  if (!e || !w || !bq || !rb || !in_s || !out_s) return fail(RNNT_EINVAL, "null argument");
+  if (first < 0 || count <= 0 || first + count > 5) return fail(RNNT_EINVAL, "bad encoder layer range");
+  DEVICE_SCOPE(e->device);
+  for (int i = 0; i < count; ++i) {
+    const int l = first + i;
+    if (!w[i] || !bq[i]) return fail(RNNT_EINVAL, "null encoder weight");
     const int K = ENC_I[l] + H;
-    std::vector<int8_t> w((size_t)G4 * K);
+    std::vector<int8_t> wp((size_t)G4 * K);
     std::vector<float> b(G4);
     for (int g = 0; g < 4; ++g)
       for (int u = 0; u < H; ++u) {
         const int pr = enc_packed_row(u, g);
-        memcpy(&w[(size_t)pr * K], m->enc_w[l] + (size_t)(g * H + u) * K, K);
-        {  // the cell's folded bias term, as oracle_enc_bias: (bq rb) * (g == 2 ? 8 : 4) + 64
-          const float bqr = m->enc_bq[l][g * H + u] * m->enc_rb[l];
-          b[pr] = g == 2 ? bqr * 8.0f + 64.0f : bqr * 4.0f + 64.0f;
-        }
+        memcpy(&wp[(size_t)pr * K], w[i] + (size_t)(g * H + u) * K, K);
+        // the cell's folded bias term, as oracle_enc_bias: (bq rb) * (g == 2 ? 8 : 4) + 64
+        const float bqr = bq[i][g * H + u] * rb[i];
+        b[pr] = g == 2 ? bqr * 8.0f + 64.0f : bqr * 4.0f + 64.0f;
       }
-    int r = upload(e, &e->enc_w[l], w);
-    if (!r) r = upload(e, &e->enc_bq[l], b);
+    int r = load_buf(e, &e->enc_w[l], wp);
+    if (!r) r = load_buf(e, &e->enc_bq[l], b);
     if (r) return r;
-    e->rb[l] = m->enc_rb[l];
-    e->in_s[l] = m->enc_in_s[l];
-    e->out_s[l] = m->enc_out_s[l];
+    e->rb[l] = rb[i];
+    e->in_s[l] = in_s[i];
+    e->out_s[l] = out_s[i];
+    e->enc_loaded |= 1 << l;
   }
-  // prediction LSTM: rows gate-interleaved, k = [W_ih | W_hh] natural, biases separate
-  // (the two chains b_ih + x.W_ih and b_hh + h.W_hh are summed after, oracle pred_row)
+  return 0;
+}
+
+// prediction LSTM: rows gate-interleaved, k = [W_ih | W_hh] natural, biases separate (the two
+// chains b_ih + x.W_ih and b_hh + h.W_hh are summed after, oracle pred_row).  embed may be NULL
+// (operator-level use: the caller embeds); the fused decode needs it for its layer-0 table.
+extern "C" int rnnt_engine_load_prediction(rnnt_engine* e, const uint16_t* embed, const uint16_t* const* w_ih,
+                                           const uint16_t* const* w_hh, const float* const* b_ih,
+                                           const float* const* b_hh) {
+  if (!e || !w_ih || !w_hh || !b_ih || !b_hh) return fail(RNNT_EINVAL, "null argument");
+  DEVICE_SCOPE(e->device);
   for (int l = 0; l < 2; ++l) {
-    if (!m->pred_w_ih[l] || !m->pred_w_hh[l] || !m->pred_b_ih[l] || !m->pred_b_hh[l])
-      return fail(RNNT_EINVAL, "null prediction weight");
+    if (!w_ih[l] || !w_hh[l] || !b_ih[l] || !b_hh[l]) return fail(RNNT_EINVAL, "null prediction weight");
     std::vector<uint16_t> w((size_t)PG4 * 640);
     std::vector<float> b(2 * PG4);
     for (int g = 0; g < 4; ++g)
       for (int u = 0; u < P; ++u) {
         const int src = g * P + u, dst = 4 * u + g;
         for (int k = 0; k < 640; ++k)
-          w[(size_t)dst * 640 + k] =
-              k < P ? m->pred_w_ih[l][(size_t)src * P + k] : m->pred_w_hh[l][(size_t)src * P + k - P];
-        b[dst] = m->pred_b_ih[l][src];
-        b[PG4 + dst] = m->pred_b_hh[l][src];
+          w[(size_t)dst * 640 + k] = k < P ? w_ih[l][(size_t)src * P + k] : w_hh[l][(size_t)src * P + k - P];
+        b[dst] = b_ih[l][src];
+        b[PG4 + dst] = b_hh[l][src];
       }
-    uint16_t* dwp;
-    float* dbp;
-    int r = upload(e, &dwp, w);
-    if (!r) r = upload(e, &dbp, b);
+    uint16_t* dwp = const_cast<uint16_t*>(e->dw.wp[l]);
+    float* dbp = const_cast<float*>(e->dw.bih_p[l]);
+    int r = load_buf(e, &dwp, w);
+    if (!r) r = load_buf(e, &dbp, b);
     if (r) return r;
     e->dw.wp[l] = dwp;
     e->dw.bih_p[l] = dbp;
     e->dw.bhh_p[l] = dbp + PG4;
   }
-  auto pad_rows = [](const uint16_t* src, int rows, int rows_pad, int K) {
-    std::vector<uint16_t> w((size_t)rows_pad * K, 0);
-    std::copy(src, src + (size_t)rows * K, w.begin());
-    return w;
-  };
+  e->pred_loaded = true;
+  e->xtab_ok = false;
+  if (embed) {
+    uint16_t* emb = const_cast<uint16_t*>(e->dw.embed);
+    int r = load_buf(e, &emb, std::vector<uint16_t>(embed, embed + 28 * P));
+    if (r) return r;
+    e->dw.embed = emb;
+    // layer-0 input table (b_ih + emb[g].W_ih^T per label, same MFMA chain as the step kernels)
+    float* xtab = const_cast<float*>(e->dw.xtab);
+    if (!xtab && (r = dev_alloc(e, &xtab, (size_t)29 * PG4))) return r;
+    DecWeights w = e->dw;
+    if (launch_dec_xtab(w, xtab, e->stream)) return fail(RNNT_EDEVICE, "xtab launch failed");
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->dw.xtab = xtab;
+    e->xtab_ok = true;
+  }
+  return 0;
+}
+
+// joint first layer: linear1_trans (w1t [512][1024], bt) and linear1_pred (w1p [512][320], bp)
+extern "C" int rnnt_engine_load_joint(rnnt_engine* e, const uint16_t* w1t, const uint16_t* w1p, const float* bt,
+                                      const float* bp) {
+  if (!e || !w1t || !w1p || !bt || !bp) return fail(RNNT_EINVAL, "null argument");
+  DEVICE_SCOPE(e->device);
+  uint16_t *dt = const_cast<uint16_t*>(e->dw.w1t), *dp = const_cast<uint16_t*>(e->dw.w1p);
+  float *dbt = const_cast<float*>(e->dw.bt), *dbp = const_cast<float*>(e->dw.bp);
+  int r = load_buf(e, &dt, std::vector<uint16_t>(w1t, w1t + (size_t)J * H));
+  if (!r) r = load_buf(e, &dp, std::vector<uint16_t>(w1p, w1p + (size_t)J * P));
+  if (!r) r = load_buf(e, &dbt, std::vector<float>(bt, bt + J));
+  if (!r) r = load_buf(e, &dbp, std::vector<float>(bp, bp + J));
+  if (r) return r;
+  e->dw.w1t = dt; e->dw.w1p = dp; e->dw.bt = dbt; e->dw.bp = dbp;
+  e->joint1_loaded = true;
+  return 0;
+}
+
+// joint output layer: linear2 (w2 [29][512], b2 [29]), zero-padded to 32 labels
+extern "C" int rnnt_engine_load_joint_out(rnnt_engine* e, const uint16_t* w2, const float* b2) {
+  if (!e || !w2 || !b2) return fail(RNNT_EINVAL, "null argument");
+  DEVICE_SCOPE(e->device);
+  std::vector<uint16_t> w((size_t)NLAB_PAD * J, 0);
+  std::copy(w2, w2 + (size_t)NLAB * J, w.begin());
+  std::vector<float> b(NLAB_PAD, 0.0f);
+  std::copy(b2, b2 + NLAB, b.begin());
+  uint16_t* dw2 = const_cast<uint16_t*>(e->dw.w2);
+  float* db2 = const_cast<float*>(e->dw.b2);
+  int r = load_buf(e, &dw2, w);
+  if (!r) r = load_buf(e, &db2, b);
+  if (r) return r;
+  e->dw.w2 = dw2;
+  e->dw.b2 = db2;
+  e->joint2_loaded = true;
+  return 0;
+}
+
+static int pack_model(rnnt_engine* e, const rnnt_model_desc* m) {
   if (!m->embed || !m->joint_w1t || !m->joint_w1p || !m->joint_w2 || !m->joint_bt || !m->joint_bp || !m->joint_b2)
     return fail(RNNT_EINVAL, "null joint/embedding weight");
-  uint16_t *emb, *w1t, *w1p, *w2;
-  float *bt, *bp, *b2;
-  int r = upload(e, &emb, std::vector<uint16_t>(m->embed, m->embed + 28 * P));
-  if (!r) r = upload(e, &w1t, pad_rows(m->joint_w1t, J, J, H));
-  if (!r) r = upload(e, &w1p, pad_rows(m->joint_w1p, J, J, P));
-  if (!r) r = upload(e, &w2, pad_rows(m->joint_w2, NLAB, NLAB_PAD, J));
-  if (!r) r = upload(e, &bt, std::vector<float>(m->joint_bt, m->joint_bt + J));
-  if (!r) r = upload(e, &bp, std::vector<float>(m->joint_bp, m->joint_bp + J));
-  if (!r) {
-    std::vector<float> b(NLAB_PAD, 0.0f);
-    std::copy(m->joint_b2, m->joint_b2 + NLAB, b.begin());
-    r = upload(e, &b2, b);
-  }
-  if (r) return r;
-  e->dw.embed = emb; e->dw.w1t = w1t; e->dw.w1p = w1p; e->dw.w2 = w2;
-  e->dw.bt = bt; e->dw.bp = bp; e->dw.b2 = b2;
-  // layer-0 input table (b_ih + emb[g].W_ih^T per label, same MFMA chain as the step kernels)
-  float* xtab;
-  if ((r = dev_alloc(e, &xtab, (size_t)29 * PG4))) return r;
-  if (launch_dec_xtab(e->dw, xtab, e->stream)) return fail(RNNT_EDEVICE, "xtab launch failed");
-  HIPCHK(hipStreamSynchronize(e->stream));
-  e->dw.xtab = xtab;
-  return 0;
+  int r = rnnt_engine_load_encoder_layers(e, 0, 5, m->enc_w, m->enc_bq, m->enc_rb, m->enc_in_s, m->enc_out_s);
+  if (!r) r = rnnt_engine_load_prediction(e, m->embed, m->pred_w_ih, m->pred_w_hh, m->pred_b_ih, m->pred_b_hh);
+  if (!r) r = rnnt_engine_load_joint(e, m->joint_w1t, m->joint_w1p, m->joint_bt, m->joint_bp);
+  if (!r) r = rnnt_engine_load_joint_out(e, m->joint_w2, m->joint_b2);
+  return r;
 }
 
 static int alloc_workspace(rnnt_engine* e) {
@@ -277,7 +338,7 @@ extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
 
 extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, const rnnt_opts* opts,
                                   rnnt_engine** out) {
-  if (!model || !out) return fail(RNNT_EINVAL, "null argument");
+  if (!out) return fail(RNNT_EINVAL, "null argument");
   *out = nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(RNNT_EDEVICE, "no HIP device");
@@ -294,7 +355,7 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   if (!dscope.ok) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
   if (!r && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
-  if (!r) r = pack_model(e, model);
+  if (!r && model) r = pack_model(e, model);
   if (!r) r = alloc_workspace(e);
   if (r) {
     rnnt_engine_destroy(e);
@@ -302,6 +363,91 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   }
   *out = e;
   return 0;
+}
+
+// ---- packed model file (include/rnnt_mi355x.h: rnnt_engine_create_from_file)
+namespace {
+struct PkEntry {
+  char name[48];
+  uint32_t dtype, ndim;
+  uint64_t shape[4];
+  uint64_t offset, nbytes;
+};
+static_assert(sizeof(PkEntry) == 48 + 8 + 32 + 16, "packed entry layout");
+}  // namespace
+
+extern "C" int rnnt_engine_create_from_file(const char* path, int device, const rnnt_opts* opts, rnnt_engine** out) {
+  if (!path || !out) return fail(RNNT_EINVAL, "null argument");
+  *out = nullptr;
+  FILE* fp = fopen(path, "rb");
+  if (!fp) return fail(RNNT_EINVAL, std::string("cannot open ") + path);
+  std::vector<char> buf;
+  {
+    char tmp[1 << 16];
+    size_t k;
+    while ((k = fread(tmp, 1, sizeof(tmp), fp)) > 0) buf.insert(buf.end(), tmp, tmp + k);
+    fclose(fp);
+  }
+  const std::string where = std::string(path) + ": ";
+  if (buf.size() < 16 || memcmp(buf.data(), "RNNTMI01", 8) != 0) return fail(RNNT_EINVAL, where + "not an RNNTMI01 file");
+  uint32_t version = 0, count = 0;
+  memcpy(&version, buf.data() + 8, 4);
+  memcpy(&count, buf.data() + 12, 4);
+  if (version != 1 || count > 256 || 16 + (size_t)count * sizeof(PkEntry) > buf.size())
+    return fail(RNNT_EINVAL, where + "bad header");
+  std::vector<PkEntry> ents(count);
+  memcpy(ents.data(), buf.data() + 16, count * sizeof(PkEntry));
+  // name -> (data, dtype, element count), every entry checked against the file size
+  auto find = [&](const std::string& name, uint32_t dtype, uint64_t elems, const void** ptr) -> int {
+    for (const PkEntry& en : ents) {
+      if (strncmp(en.name, name.c_str(), sizeof(en.name)) != 0) continue;
+      uint64_t n = 1;
+      for (uint32_t d = 0; d < en.ndim && d < 4; ++d) n *= en.shape[d];
+      const uint64_t esz = dtype == 0 ? 1 : dtype == 1 ? 4 : 2;
+      if (en.dtype != dtype || en.ndim > 4 || n != elems || en.nbytes != n * esz || en.offset % 64 ||
+          en.offset > buf.size() || en.nbytes > buf.size() - en.offset)
+        return fail(RNNT_EINVAL, where + "entry " + name + " has the wrong type, shape or extent");
+      *ptr = buf.data() + en.offset;
+      return 0;
+    }
+    return fail(RNNT_EINVAL, where + "missing entry " + name);
+  };
+  rnnt_model_desc d{};
+  int r = 0;
+  const void* p = nullptr;
+  const float* rb = nullptr;
+  const float* ins = nullptr;
+  const float* outs = nullptr;
+  for (int l = 0; l < 5 && !r; ++l) {
+    if (!(r = find("enc_w." + std::to_string(l), 0, (uint64_t)G4 * (ENC_I[l] + H), &p))) d.enc_w[l] = (const int8_t*)p;
+    if (!r && !(r = find("enc_bq." + std::to_string(l), 1, G4, &p))) d.enc_bq[l] = (const float*)p;
+  }
+  if (!r && !(r = find("enc_rb", 1, 5, &p))) rb = (const float*)p;
+  if (!r && !(r = find("enc_in_s", 1, 5, &p))) ins = (const float*)p;
+  if (!r && !(r = find("enc_out_s", 1, 5, &p))) outs = (const float*)p;
+  if (!r) {
+    memcpy(d.enc_rb, rb, sizeof(d.enc_rb));
+    memcpy(d.enc_in_s, ins, sizeof(d.enc_in_s));
+    memcpy(d.enc_out_s, outs, sizeof(d.enc_out_s));
+  }
+  if (!r && !(r = find("embed", 2, (uint64_t)28 * P, &p))) d.embed = (const uint16_t*)p;
+  for (int l = 0; l < 2 && !r; ++l) {
+    const std::string s = "." + std::to_string(l);
+    if (!(r = find("pred_wih" + s, 2, (uint64_t)PG4 * P, &p))) d.pred_w_ih[l] = (const uint16_t*)p;
+    if (!r && !(r = find("pred_whh" + s, 2, (uint64_t)PG4 * P, &p))) d.pred_w_hh[l] = (const uint16_t*)p;
+    if (!r && !(r = find("pred_bih" + s, 1, PG4, &p))) d.pred_b_ih[l] = (const float*)p;
+    if (!r && !(r = find("pred_bhh" + s, 1, PG4, &p))) d.pred_b_hh[l] = (const float*)p;
+  }
+  if (!r && !(r = find("w1t", 2, (uint64_t)J * H, &p))) d.joint_w1t = (const uint16_t*)p;
+  if (!r && !(r = find("w1p", 2, (uint64_t)J * P, &p))) d.joint_w1p = (const uint16_t*)p;
+  if (!r && !(r = find("bt", 1, J, &p))) d.joint_bt = (const float*)p;
+  if (!r && !(r = find("bp", 1, J, &p))) d.joint_bp = (const float*)p;
+  if (!r && !(r = find("w2", 2, (uint64_t)NLAB * J, &p))) d.joint_w2 = (const uint16_t*)p;
+  if (!r && !(r = find("b2", 1, NLAB, &p))) d.joint_b2 = (const float*)p;
+  if (r) return r;
+  // typed pointers into the image are aligned: the vector's storage comes from operator new
+  // (>= 16-byte aligned) and every entry offset is a multiple of 64
+  return rnnt_engine_create(&d, device, opts, out);
 }
 
 // ---- small utility kernels
@@ -427,6 +573,7 @@ static std::vector<int> tile_maxima(const int32_t* lens_host, int n, int n_pad) 
 extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
                                   int T, int n, int n_pad, float* f_out, void* stream) {
   if (!e || !feats || !lens) return fail(RNNT_EINVAL, "null argument");
+  if (e->enc_loaded != 0x1f) return fail(RNNT_EINVAL, "encoder weights not loaded");
   int r = check_batch(e, T, n, n_pad);
   if (r) return r;
   DEVICE_SCOPE(e->device);
@@ -479,6 +626,8 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
 extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream) {
   if (!e || !res || !res_len) return fail(RNNT_EINVAL, "null argument");
   if (e->last_n <= 0) return fail(RNNT_EINVAL, "decode before encode");
+  if (!e->xtab_ok || !e->joint1_loaded || !e->joint2_loaded)
+    return fail(RNNT_EINVAL, "prediction (with embedding) / joint weights not loaded");
   if (max_res <= 0) return fail(RNNT_EINVAL, "max_res must be positive");
   DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
@@ -562,6 +711,8 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
   if (T <= 0 || T > e->opts.max_frames || n_pad <= 0 || n_pad % ENC_PAD || n_pad > e->np_max)
     return fail(RNNT_EINVAL, "T / n_pad out of range");
   if (first <= 1 && first + count > 2) return fail(RNNT_EINVAL, "a call covers pre_rnn or post_rnn, not both");
+  for (int l = first; l < first + count; ++l)
+    if (!(e->enc_loaded >> l & 1)) return fail(RNNT_EINVAL, "encoder layer weights not loaded");
   if (first >= 2 && T > e->tp_max) return fail(RNNT_EINVAL, "post_rnn T exceeds ceil(max_frames/2)");
   DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
@@ -850,6 +1001,7 @@ extern "C" int rnnt_op_lstm_bf16(rnnt_engine* e, const uint16_t* x, const uint16
                                  float* cy, int n_pad, void* stream) {
   if (!e || !x || !hx || !cx || !hy || !cy) return fail(RNNT_EINVAL, "null argument");
   if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
+  if (!e->pred_loaded) return fail(RNNT_EINVAL, "prediction weights not loaded");
   DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
   const size_t NP = (size_t)n_pad * P;
@@ -863,6 +1015,7 @@ extern "C" int rnnt_op_joint_hidden(rnnt_engine* e, const float* f, const uint16
                                     void* stream) {
   if (!e || !f || !g || !y1) return fail(RNNT_EINVAL, "null argument");
   if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
+  if (!e->joint1_loaded) return fail(RNNT_EINVAL, "joint linear1 weights not loaded");
   DEVICE_SCOPE(e->device);
   if (launch_op_joint_hidden(e->dw, f, g, y1, n_pad, pick(e, stream))) return fail(RNNT_EDEVICE, "joint launch failed");
   return 0;
@@ -871,24 +1024,28 @@ extern "C" int rnnt_op_joint_hidden(rnnt_engine* e, const float* f, const uint16
 extern "C" int rnnt_op_joint_logits(rnnt_engine* e, const uint16_t* y1, float* logits, int n_pad, void* stream) {
   if (!e || !y1 || !logits) return fail(RNNT_EINVAL, "null argument");
   if (!check_rows(n_pad)) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 16");
+  if (!e->joint2_loaded) return fail(RNNT_EINVAL, "joint linear2 weights not loaded");
   DEVICE_SCOPE(e->device);
   if (launch_op_joint_logits(e->dw, y1, logits, n_pad, pick(e, stream))) return fail(RNNT_EDEVICE, "linear2 launch failed");
   return 0;
 }
 
-__global__ void op_count_unfinished_kernel(const int32_t* finish, int n, int32_t* count) {
+__global__ void op_count_unfinished_kernel(const int32_t* time_idx, const int32_t* f_lens, int n, int32_t* count) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && !finish[i]) atomicAdd(count, 1);
+  if (i < n && time_idx[i] < f_lens[i]) atomicAdd(count, 1);
 }
 
-extern "C" int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int32_t* symbols_added, int32_t* res,
-                                     int32_t* res_idx, const float* f, const int32_t* f_lens, int32_t* time_idx,
-                                     float* fi, int32_t* pre_g, uint16_t* pre_hg, float* pre_cg, const uint16_t* hg,
-                                     const float* cg, int32_t* finish, int n, int n_pad, int max_res, void* stream) {
+extern "C" int rnnt_op_greedy_update(rnnt_engine* e, const void* symbols, int symbols_i64, int32_t* symbols_added,
+                                     int32_t* res, int32_t* res_idx, const float* f, int f_batch, const int32_t* f_lens,
+                                     int32_t* time_idx, float* fi, int32_t* pre_g, uint16_t* const* pre_hg,
+                                     float* const* pre_cg, const uint16_t* const* hg, const float* const* cg, int n,
+                                     int max_res, void* stream) {
   if (!e || !symbols || !symbols_added || !res || !res_idx || !f || !f_lens || !time_idx || !fi || !pre_g || !pre_hg ||
-      !pre_cg || !hg || !cg || !finish)
+      !pre_cg || !hg || !cg)
     return fail(RNNT_EINVAL, "null argument");
-  if (n <= 0 || n_pad < n || max_res <= 0) return fail(RNNT_EINVAL, "bad sizes");
+  for (int l = 0; l < 2; ++l)
+    if (!pre_hg[l] || !pre_cg[l] || !hg[l] || !cg[l]) return fail(RNNT_EINVAL, "null state tensor");
+  if (n <= 0 || f_batch < n || max_res <= 0) return fail(RNNT_EINVAL, "bad sizes");
   DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
   if (!e->op_count) {
@@ -898,11 +1055,29 @@ extern "C" int rnnt_op_greedy_update(rnnt_engine* e, const int32_t* symbols, int
   }
   int r = state_acquire(e, st);
   if (r) return r;
-  GreedyUpdateArgs a{symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg,
-                     finish, e->op_count + 1, n, n_pad, max_res};
+  GreedyUpdateArgs a{};
+  a.symbols = symbols;
+  a.sym64 = symbols_i64 != 0;
+  a.symbols_added = symbols_added;
+  a.res = res;
+  a.res_idx = res_idx;
+  a.f = f;
+  a.f_batch = f_batch;
+  a.f_lens = f_lens;
+  a.time_idx = time_idx;
+  a.fi = fi;
+  a.pre_g = pre_g;
+  for (int l = 0; l < 2; ++l) {
+    a.pre_hg[l] = pre_hg[l];
+    a.pre_cg[l] = pre_cg[l];
+    a.hg[l] = hg[l];
+    a.cg[l] = cg[l];
+  }
+  a.n = n;
+  a.max_res = max_res;
   if (launch_op_greedy_update(a, st)) return fail(RNNT_EDEVICE, "greedy_update launch failed");
   HIPCHK(hipMemsetAsync(e->op_count, 0, sizeof(int32_t), st));
-  hipLaunchKernelGGL(op_count_unfinished_kernel, dim3((n + 255) / 256), dim3(256), 0, st, finish, n, e->op_count);
+  hipLaunchKernelGGL(op_count_unfinished_kernel, dim3((n + 255) / 256), dim3(256), 0, st, time_idx, f_lens, n, e->op_count);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(e->op_count_host, e->op_count, sizeof(int32_t), hipMemcpyDeviceToHost, st));
   if ((r = state_release(e, st))) return r;

@@ -1,0 +1,424 @@
+// torch_ops.cpp -- the reference's operator library, torch.ops.intel_mlperf.*, on the MI355X engine.
+//
+// The reference's TorchScript graph binds its hot-path ops from a loaded library
+// (models/_C.py:9-51: torch.ops.load_library(".../libmlperf_plugins.so")) and the C++ SUT runs
+// that graph through torch::jit::load (csrc/rnnt_model.hpp:41-54).  This library registers the
+// same namespace and schemas -- the ones the call sites imply (quant_lstm.py:92-101,
+// modeling_rnnt.py:202, 269-283, 326-328, 351-365) -- so the graph binds unchanged:
+//
+//   lstm_amx_int8(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights, Tensor rb_scale,
+//                 Tensor in_scale, Tensor out_scale, bool skip_quant_y) -> (Tensor, Tensor[], Tensor[])
+//   stack_time(Tensor x, Tensor x_lens, int factor) -> Tensor
+//   lstm_amx_bf16(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights) -> (Tensor, Tensor[], Tensor[])
+//   amx_linear_bf16_accum_relu(Tensor f, Tensor w1_trans, Tensor g, Tensor w1_pred, Tensor bias) -> Tensor
+//   amx_linear_i16o32(Tensor y, Tensor w2, Tensor b2) -> Tensor
+//   greedy_decode_update(Tensor symbols, Tensor symbols_added, Tensor res, Tensor res_idx, Tensor f,
+//                        Tensor f_lens, Tensor time_idx, Tensor fi, Tensor pre_g, Tensor[] pre_hg,
+//                        Tensor[] pre_cg, Tensor[] hg, Tensor[] cg) -> bool
+//   prepack_lstm_weights(Tensor w_ih, Tensor w_hh) -> (Tensor, Tensor)   (identity: the engine packs)
+//   prepack_linear_weight(Tensor w) -> Tensor                           (identity)
+//
+// Activations live on the GPU (CUDA dispatch key); weights may be host or device tensors.  The
+// ops compute with the weights they are passed: each distinct weight set (keyed by the tensors'
+// storage pointers, version counters and shapes) is unpacked -- from the reference's AMX tile
+// layouts (quant_modules.py:158-193 transpose_tile_weight[_bf16]) or natural layouts -- and
+// loaded into a per-device engine (rnnt_engine_load_*) the first time it is seen; a changed
+// weight tensor reloads that component.  All arithmetic is the engine's (librnnt_mi355x.so).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rnnt_mi355x.h"
+
+namespace {
+
+constexpr int H = 1024, P = 320, J = 512, NLAB = 29;
+const int ENC_I[5] = {256, 1024, 2048, 1024, 1024};
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc >= 0, "intel_mlperf::", what, " (MI355X engine): ", rnnt_last_error());
+}
+
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// identity of a set of weight tensors
+using Key = std::vector<int64_t>;
+void key_add(Key& k, const at::Tensor& t) {
+  k.push_back((int64_t)(intptr_t)t.data_ptr());
+  k.push_back((int64_t)t._version());
+  k.push_back(t.numel());
+  k.push_back((int64_t)t.scalar_type());
+  for (auto s : t.sizes()) k.push_back(s);
+}
+
+struct OpEngine {
+  rnnt_engine* e = nullptr;
+  int max_batch = 0, max_frames = 0;
+  Key enc[5], pred, joint1, joint2;
+};
+std::mutex g_mu;
+std::map<int, OpEngine> g_eng;
+
+// The device's engine with room for n_pad rows and `frames` feature frames (recreated larger on
+// demand; its components then reload from the next call's weights).
+OpEngine& engine_for(int dev, int64_t n_pad, int64_t frames) {
+  OpEngine& oe = g_eng[dev];
+  if (oe.e && n_pad <= oe.max_batch && frames <= oe.max_frames) return oe;
+  if (oe.e) rnnt_engine_destroy(oe.e);
+  oe = OpEngine{};
+  rnnt_opts o{};
+  o.max_batch = (int)std::max<int64_t>(round_up(n_pad, 256), 256);
+  o.max_frames = (int)std::max<int64_t>(frames, 500);
+  o.max_res = (o.max_frames / 2) * 30;
+  check_rc(rnnt_engine_create(nullptr, dev, &o, &oe.e), "engine create");
+  oe.max_batch = o.max_batch;
+  oe.max_frames = o.max_frames;
+  return oe;
+}
+
+void* stream_of(const at::Tensor& t) { return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+template <class T>
+std::vector<T> host_vec(const at::Tensor& t, at::ScalarType st) {
+  at::Tensor c = t.detach().to(at::kCPU).to(st).contiguous();
+  std::vector<T> v(c.numel());
+  std::memcpy(v.data(), c.data_ptr(), v.size() * sizeof(T));
+  return v;
+}
+
+// int8 weight of a gate matrix W_q [4096][I] (natural), from the reference's AMX tiles of W_q^T
+// ([col_step][4][col_tile][16][64], transpose_tile_weight: element (k, o) of W^T at
+// [o/64][(o%64)/16][k/64][(k%64)/4][4(o%16) + k%4]) or a natural [4096][I'] tensor; I >= I'.
+std::vector<int8_t> enc_weight(const at::Tensor& t, int I) {
+  at::Tensor c = t.detach().to(at::kCPU).contiguous();
+  TORCH_CHECK(c.scalar_type() == at::kChar, "lstm_amx_int8: int8 weights expected");
+  std::vector<int8_t> w((size_t)4 * H * I, 0);
+  const int8_t* p = c.data_ptr<int8_t>();
+  if (c.dim() == 5) {
+    const int64_t cs = c.size(0), ct = c.size(2);
+    TORCH_CHECK(c.size(1) == 4 && c.size(3) == 16 && c.size(4) == 64 && cs * 64 == 4 * H && ct * 64 <= I + 63,
+                "lstm_amx_int8: AMX tile shape ", c.sizes());
+    const int K = (int)std::min<int64_t>(ct * 64, I);
+    for (int o = 0; o < 4 * H; ++o)
+      for (int k = 0; k < K; ++k)
+        w[(size_t)o * I + k] =
+            p[(((((size_t)(o / 64) * 4 + (o % 64) / 16) * ct + k / 64) * 16 + (k % 64) / 4) * 64) + 4 * (o % 16) + k % 4];
+  } else {
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == 4 * H && c.size(1) <= I, "lstm_amx_int8: weight shape ", c.sizes());
+    for (int o = 0; o < 4 * H; ++o) std::memcpy(&w[(size_t)o * I], p + (size_t)o * c.size(1), c.size(1));
+  }
+  return w;
+}
+
+// bf16 weight W [O][K] (bit patterns, natural) from transpose_tile_weight_bf16 tiles of W^T
+// ([col_step][2][col_tile][16][32]: element (k, o) at [o/32][(o%32)/16][k/32][(k%32)/2][2(o%16) + k%2])
+// or a natural [O'][K] tensor (O' <= O rows, the rest zero).
+std::vector<uint16_t> bf16_weight(const at::Tensor& t, int O, int K, const char* op) {
+  at::Tensor c = t.detach().to(at::kCPU).contiguous();
+  TORCH_CHECK(c.scalar_type() == at::kBFloat16, op, ": bf16 weights expected");
+  std::vector<uint16_t> w((size_t)O * K, 0);
+  const uint16_t* p = (const uint16_t*)c.data_ptr();
+  if (c.dim() == 5) {
+    const int64_t cs = c.size(0), ct = c.size(2);
+    TORCH_CHECK(c.size(1) == 2 && c.size(3) == 16 && c.size(4) == 32 && ct * 32 == K && cs * 32 >= O, op,
+                ": bf16 tile shape ", c.sizes());
+    for (int o = 0; o < O; ++o)
+      for (int k = 0; k < K; ++k)
+        w[(size_t)o * K + k] =
+            p[(((((size_t)(o / 32) * 2 + (o % 32) / 16) * ct + k / 32) * 16 + (k % 32) / 2) * 32) + 2 * (o % 16) + k % 2];
+  } else {
+    TORCH_CHECK(c.dim() == 2 && c.size(1) == K && c.size(0) <= O, op, ": weight shape ", c.sizes());
+    std::memcpy(w.data(), p, (size_t)c.size(0) * K * 2);
+  }
+  return w;
+}
+
+// ---------------------------------------------------------------- lstm_amx_int8
+std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_amx_int8(
+    const at::Tensor& x, at::TensorList hx, at::TensorList cx, const c10::List<c10::List<at::Tensor>>& weights,
+    const at::Tensor& rb_scale, const at::Tensor& in_scale, const at::Tensor& out_scale, bool skip_quant_y) {
+  const int L = (int)weights.size();
+  TORCH_CHECK(x.is_cuda(), "lstm_amx_int8: activations must be on the GPU");
+  TORCH_CHECK(x.dim() == 3, "lstm_amx_int8: x [T, N, C]");
+  const bool pre = x.scalar_type() == at::kFloat;
+  const int first = pre ? 0 : 2;
+  TORCH_CHECK((pre && L == 2) || (!pre && L == 3 && x.scalar_type() == at::kChar),
+              "lstm_amx_int8: pre_rnn (fp32 x, 2 layers) or post_rnn (int8 x, 3 layers)");
+  TORCH_CHECK((int)hx.size() == L && (int)cx.size() == L, "lstm_amx_int8: one hx / cx tensor per layer");
+  TORCH_CHECK(skip_quant_y == (first + L == 5), "lstm_amx_int8: skip_quant_y is set exactly for post_rnn");
+  const int64_t T = x.size(0), N = x.size(1), n_pad = round_up(N, 256);
+  const int dev = x.device().index();
+  std::lock_guard<std::mutex> lock(g_mu);
+  OpEngine& oe = engine_for(dev, n_pad, pre ? T : 2 * T);
+  const std::vector<float> rb = host_vec<float>(rb_scale, at::kFloat), ins = host_vec<float>(in_scale, at::kFloat),
+                           outs = host_vec<float>(out_scale, at::kFloat);
+  TORCH_CHECK((int)rb.size() >= L && (int)ins.size() >= L && (int)outs.size() >= L, "lstm_amx_int8: scale tensors");
+  for (int i = 0; i < L; ++i) {
+    const int l = first + i;
+    const c10::List<at::Tensor> wl = weights.get(i);
+    TORCH_CHECK(wl.size() == 4, "lstm_amx_int8: weights[l] = [w_ih, w_hh, b_ih, b_q]");
+    Key k;
+    for (int j : {0, 1, 3}) key_add(k, wl.get(j));
+    key_add(k, rb_scale);
+    key_add(k, in_scale);
+    key_add(k, out_scale);
+    if (k == oe.enc[l]) continue;
+    const int I = ENC_I[l];
+    const std::vector<int8_t> wi = enc_weight(wl.get(0), I), wh = enc_weight(wl.get(1), H);
+    std::vector<int8_t> w((size_t)4 * H * (I + H));
+    for (int o = 0; o < 4 * H; ++o) {
+      std::memcpy(&w[(size_t)o * (I + H)], &wi[(size_t)o * I], I);
+      std::memcpy(&w[(size_t)o * (I + H) + I], &wh[(size_t)o * H], H);
+    }
+    const std::vector<float> bq = host_vec<float>(wl.get(3), at::kFloat);
+    TORCH_CHECK((int)bq.size() == 4 * H, "lstm_amx_int8: fused bias [4096]");
+    const int8_t* wp = w.data();
+    const float* bp = bq.data();
+    check_rc(rnnt_engine_load_encoder_layers(oe.e, l, 1, &wp, &bp, &rb[i], &ins[i], &outs[i]), "lstm_amx_int8 load");
+    oe.enc[l] = k;
+  }
+  const auto opt = x.options();
+  at::Tensor xin;
+  if (pre) {
+    xin = at::zeros({T, n_pad, 256}, opt.dtype(at::kFloat));
+    xin.narrow(1, 0, N).narrow(2, 0, x.size(2)).copy_(x);
+  } else {
+    TORCH_CHECK(x.size(2) == 2 * H, "lstm_amx_int8: post_rnn x int8 [T, N, 2048]");
+    xin = at::zeros({T, n_pad, 2 * H}, opt.dtype(at::kChar));
+    xin.narrow(1, 0, N).copy_(x);
+  }
+  at::Tensor h = at::zeros({L, n_pad, H}, opt.dtype(at::kChar));
+  at::Tensor c = at::zeros({L, n_pad, H}, opt.dtype(at::kHalf));
+  for (int i = 0; i < L; ++i) {
+    h[i].narrow(0, 0, N).copy_(hx[i]);
+    c[i].narrow(0, 0, N).copy_(cx[i]);
+  }
+  at::Tensor y = at::empty({T, n_pad, H}, opt.dtype(skip_quant_y ? at::kFloat : at::kChar));
+  check_rc(rnnt_op_lstm_int8(oe.e, first, L, xin.data_ptr(), (int)T, (int)n_pad, (int8_t*)h.data_ptr(),
+                             (uint16_t*)c.data_ptr(), y.data_ptr(), stream_of(x)),
+           "lstm_amx_int8");
+  std::vector<at::Tensor> ho, co;
+  for (int i = 0; i < L; ++i) {
+    ho.push_back(h[i].narrow(0, 0, N));
+    co.push_back(c[i].narrow(0, 0, N));
+  }
+  return {N == n_pad ? y : y.narrow(1, 0, N).contiguous(), ho, co};
+}
+
+// ---------------------------------------------------------------- stack_time
+at::Tensor stack_time(const at::Tensor& x, const at::Tensor& x_lens, int64_t factor) {
+  TORCH_CHECK(factor == 2, "stack_time: factor 2");
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kChar && x.dim() == 3, "stack_time: int8 [T, N, C] on the GPU");
+  const int64_t T = x.size(0), N = x.size(1), C = x.size(2), n_pad = round_up(N, 16);
+  at::Tensor xin = at::zeros({T, n_pad, C}, x.options());
+  xin.narrow(1, 0, N).copy_(x);
+  at::Tensor lens = at::zeros({n_pad}, x.options().dtype(at::kInt));
+  lens.narrow(0, 0, N).copy_(x_lens);
+  at::Tensor y = at::empty({(T + 1) / 2, n_pad, 2 * C}, x.options());
+  std::lock_guard<std::mutex> lock(g_mu);
+  OpEngine& oe = engine_for(x.device().index(), 256, 500);
+  check_rc(rnnt_op_stack_time(oe.e, (const int8_t*)xin.data_ptr(), lens.data_ptr<int32_t>(), (int)T, (int)n_pad, (int)C,
+                              (int8_t*)y.data_ptr(), stream_of(x)),
+           "stack_time");
+  return N == n_pad ? y : y.narrow(1, 0, N).contiguous();
+}
+
+// ---------------------------------------------------------------- lstm_amx_bf16
+// weights[l] = [w_ih, w_hh, b_ih, b_hh + b_ih] (Prediction.prepack_weights, modeling_rnnt.py:161-181);
+// the engine's contract keeps the two chains' biases apart (b_ih + x.W_ih, b_hh + h.W_hh), so
+// b_hh is recovered as fp32(slot 3 - slot 2).
+std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_amx_bf16(
+    const at::Tensor& x, at::TensorList hx, at::TensorList cx, const c10::List<c10::List<at::Tensor>>& weights) {
+  TORCH_CHECK(x.is_cuda(), "lstm_amx_bf16: activations must be on the GPU");
+  TORCH_CHECK(weights.size() == 2 && hx.size() == 2 && cx.size() == 2, "lstm_amx_bf16: 2 layers");
+  const at::Tensor x2 = x.reshape({-1, P});
+  const int64_t N = x2.size(0), n_pad = round_up(N, 16);
+  std::lock_guard<std::mutex> lock(g_mu);
+  OpEngine& oe = engine_for(x.device().index(), n_pad, 500);
+  Key k;
+  for (int l = 0; l < 2; ++l)
+    for (int j = 0; j < 4; ++j) key_add(k, weights.get(l).get(j));
+  if (k != oe.pred) {
+    std::vector<uint16_t> wi[2], wh[2];
+    std::vector<float> bi[2], bh[2];
+    const uint16_t *pwi[2], *pwh[2];
+    const float *pbi[2], *pbh[2];
+    for (int l = 0; l < 2; ++l) {
+      const c10::List<at::Tensor> wl = weights.get(l);
+      TORCH_CHECK(wl.size() == 4, "lstm_amx_bf16: weights[l] = [w_ih, w_hh, b_ih, b_hh + b_ih]");
+      wi[l] = bf16_weight(wl.get(0), 4 * P, P, "lstm_amx_bf16");
+      wh[l] = bf16_weight(wl.get(1), 4 * P, P, "lstm_amx_bf16");
+      bi[l] = host_vec<float>(wl.get(2), at::kFloat);
+      const std::vector<float> bf = host_vec<float>(wl.get(3), at::kFloat);
+      TORCH_CHECK(bi[l].size() == 4 * P && bf.size() == 4 * P, "lstm_amx_bf16: biases [1280]");
+      bh[l].resize(4 * P);
+      for (int r = 0; r < 4 * P; ++r) bh[l][r] = bf[r] - bi[l][r];
+      pwi[l] = wi[l].data();
+      pwh[l] = wh[l].data();
+      pbi[l] = bi[l].data();
+      pbh[l] = bh[l].data();
+    }
+    check_rc(rnnt_engine_load_prediction(oe.e, nullptr, pwi, pwh, pbi, pbh), "lstm_amx_bf16 load");
+    oe.pred = k;
+  }
+  const auto opt = x.options();
+  at::Tensor xb = at::zeros({n_pad, P}, opt.dtype(at::kBFloat16));
+  xb.narrow(0, 0, N).copy_(x2);
+  at::Tensor h = at::zeros({2, n_pad, P}, opt.dtype(at::kBFloat16));
+  at::Tensor c = at::zeros({2, n_pad, P}, opt.dtype(at::kFloat));
+  for (int l = 0; l < 2; ++l) {
+    h[l].narrow(0, 0, N).copy_(hx[l]);
+    c[l].narrow(0, 0, N).copy_(cx[l]);
+  }
+  at::Tensor hy = at::empty_like(h), cy = at::empty_like(c);
+  check_rc(rnnt_op_lstm_bf16(oe.e, (const uint16_t*)xb.data_ptr(), (const uint16_t*)h.data_ptr(), c.data_ptr<float>(),
+                             (uint16_t*)hy.data_ptr(), cy.data_ptr<float>(), (int)n_pad, stream_of(x)),
+           "lstm_amx_bf16");
+  std::vector<at::Tensor> ho{hy[0].narrow(0, 0, N), hy[1].narrow(0, 0, N)};
+  std::vector<at::Tensor> co{cy[0].narrow(0, 0, N), cy[1].narrow(0, 0, N)};
+  return {ho[1].unsqueeze(0), ho, co};
+}
+
+// ---------------------------------------------------------------- joint
+// linear1: bias = linear1_trans.bias + linear1_pred.bias (modeling_rnnt.py:225-227); the trans
+// bias is zero after migrate_state_dict (utils.py:69), so the engine's F chain starts from 0 and
+// the G chain from `bias`.
+at::Tensor amx_linear_bf16_accum_relu(const at::Tensor& f, const at::Tensor& w1_trans, const at::Tensor& g,
+                                      const at::Tensor& w1_pred, const at::Tensor& bias) {
+  TORCH_CHECK(f.is_cuda() && g.is_cuda(), "amx_linear_bf16_accum_relu: activations must be on the GPU");
+  const at::Tensor f2 = f.reshape({-1, H}), g2 = g.reshape({-1, P});
+  const int64_t N = f2.size(0), n_pad = round_up(N, 16);
+  TORCH_CHECK(g2.size(0) == N, "amx_linear_bf16_accum_relu: f / g rows");
+  std::lock_guard<std::mutex> lock(g_mu);
+  OpEngine& oe = engine_for(f.device().index(), n_pad, 500);
+  Key k;
+  key_add(k, w1_trans);
+  key_add(k, w1_pred);
+  key_add(k, bias);
+  if (k != oe.joint1) {
+    const std::vector<uint16_t> wt = bf16_weight(w1_trans, J, H, "amx_linear_bf16_accum_relu");
+    const std::vector<uint16_t> wp = bf16_weight(w1_pred, J, P, "amx_linear_bf16_accum_relu");
+    const std::vector<float> bp = host_vec<float>(bias, at::kFloat), bt(J, 0.0f);
+    TORCH_CHECK((int)bp.size() == J, "amx_linear_bf16_accum_relu: bias [512]");
+    check_rc(rnnt_engine_load_joint(oe.e, wt.data(), wp.data(), bt.data(), bp.data()), "amx_linear_bf16_accum_relu load");
+    oe.joint1 = k;
+  }
+  at::Tensor fp = at::zeros({n_pad, H}, f.options().dtype(at::kFloat));
+  fp.narrow(0, 0, N).copy_(f2);
+  at::Tensor gp = at::zeros({n_pad, P}, g.options().dtype(at::kBFloat16));
+  gp.narrow(0, 0, N).copy_(g2);
+  at::Tensor y1 = at::empty({n_pad, J}, g.options().dtype(at::kBFloat16));
+  check_rc(rnnt_op_joint_hidden(oe.e, fp.data_ptr<float>(), (const uint16_t*)gp.data_ptr(), (uint16_t*)y1.data_ptr(),
+                                (int)n_pad, stream_of(f)),
+           "amx_linear_bf16_accum_relu");
+  return y1.narrow(0, 0, N);
+}
+
+at::Tensor amx_linear_i16o32(const at::Tensor& y, const at::Tensor& w2, const at::Tensor& b2) {
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.size(1) == J, "amx_linear_i16o32: y bf16 [N, 512] on the GPU");
+  const int64_t N = y.size(0), n_pad = round_up(N, 16);
+  std::lock_guard<std::mutex> lock(g_mu);
+  OpEngine& oe = engine_for(y.device().index(), n_pad, 500);
+  Key k;
+  key_add(k, w2);
+  key_add(k, b2);
+  if (k != oe.joint2) {
+    const std::vector<uint16_t> w = bf16_weight(w2, 32, J, "amx_linear_i16o32");  // 29 labels, zero-padded to 32
+    std::vector<float> b = host_vec<float>(b2, at::kFloat);
+    TORCH_CHECK(b.size() == NLAB || b.size() == 32, "amx_linear_i16o32: bias [29] or [32]");
+    check_rc(rnnt_engine_load_joint_out(oe.e, w.data(), b.data()), "amx_linear_i16o32 load");
+    oe.joint2 = k;
+  }
+  at::Tensor yp = at::zeros({n_pad, J}, y.options().dtype(at::kBFloat16));
+  yp.narrow(0, 0, N).copy_(y);
+  at::Tensor logits = at::empty({n_pad, 32}, y.options().dtype(at::kFloat));
+  check_rc(rnnt_op_joint_logits(oe.e, (const uint16_t*)yp.data_ptr(), logits.data_ptr<float>(), (int)n_pad,
+                                stream_of(y)),
+           "amx_linear_i16o32");
+  return logits.narrow(0, 0, N);
+}
+
+// ---------------------------------------------------------------- greedy_decode_update
+bool greedy_decode_update(const at::Tensor& symbols, const at::Tensor& symbols_added, const at::Tensor& res,
+                          const at::Tensor& res_idx, const at::Tensor& f, const at::Tensor& f_lens,
+                          const at::Tensor& time_idx, const at::Tensor& fi, const at::Tensor& pre_g,
+                          at::TensorList pre_hg, at::TensorList pre_cg, at::TensorList hg, at::TensorList cg) {
+  const int64_t N = symbols.numel();
+  TORCH_CHECK(symbols.is_cuda(), "greedy_decode_update: state must be on the GPU");
+  TORCH_CHECK(symbols.scalar_type() == at::kLong || symbols.scalar_type() == at::kInt, "symbols int64 / int32");
+  for (const at::Tensor* t : {&symbols_added, &res_idx, &time_idx, &f_lens, &pre_g})
+    TORCH_CHECK(t->scalar_type() == at::kInt && t->numel() == N && t->is_contiguous(), "greedy_decode_update: int32 [N] state");
+  TORCH_CHECK(res.scalar_type() == at::kInt && res.dim() == 2 && res.size(0) == N && res.is_contiguous(), "res int32 [N, max_res]");
+  TORCH_CHECK(f.scalar_type() == at::kFloat && f.dim() == 3 && f.size(2) == H && f.is_contiguous() && f.size(1) >= N,
+              "f fp32 [T, N, 1024]");
+  TORCH_CHECK(fi.scalar_type() == at::kFloat && fi.numel() == N * H && fi.is_contiguous(), "fi fp32 [N, 1024]");
+  TORCH_CHECK(pre_hg.size() == 2 && pre_cg.size() == 2 && hg.size() == 2 && cg.size() == 2, "2-layer state");
+  uint16_t* phg[2];
+  float* pcg[2];
+  const uint16_t* chg[2];
+  const float* ccg[2];
+  for (int l = 0; l < 2; ++l) {
+    TORCH_CHECK(pre_hg[l].scalar_type() == at::kBFloat16 && hg[l].scalar_type() == at::kBFloat16 &&
+                    pre_cg[l].scalar_type() == at::kFloat && cg[l].scalar_type() == at::kFloat,
+                "greedy_decode_update: h bf16, c fp32");
+    for (const at::Tensor* t : {&pre_hg[l], &pre_cg[l], &hg[l], &cg[l]})
+      TORCH_CHECK(t->numel() == N * P && t->is_contiguous(), "greedy_decode_update: [N, 320] contiguous state");
+    phg[l] = (uint16_t*)pre_hg[l].data_ptr();
+    pcg[l] = pre_cg[l].data_ptr<float>();
+    chg[l] = (const uint16_t*)hg[l].data_ptr();
+    ccg[l] = cg[l].data_ptr<float>();
+  }
+  std::lock_guard<std::mutex> lock(g_mu);
+  OpEngine& oe = engine_for(symbols.device().index(), 256, 500);
+  const int rc = rnnt_op_greedy_update(oe.e, symbols.data_ptr(), symbols.scalar_type() == at::kLong,
+                                       symbols_added.data_ptr<int32_t>(), res.data_ptr<int32_t>(),
+                                       res_idx.data_ptr<int32_t>(), f.data_ptr<float>(), (int)f.size(1),
+                                       f_lens.data_ptr<int32_t>(), time_idx.data_ptr<int32_t>(), fi.data_ptr<float>(),
+                                       pre_g.data_ptr<int32_t>(), phg, pcg, chg, ccg, (int)N, (int)res.size(1),
+                                       stream_of(symbols));
+  check_rc(rc, "greedy_decode_update");
+  return rc == 1;
+}
+
+// build-time ops of the reference graph: the engine packs its own layouts, so these hand the
+// natural tensors through (the compute ops accept natural as well as AMX-tiled weights)
+std::tuple<at::Tensor, at::Tensor> prepack_lstm_weights(const at::Tensor& w_ih, const at::Tensor& w_hh) {
+  return {w_ih, w_hh};
+}
+at::Tensor prepack_linear_weight(const at::Tensor& w) { return w; }
+
+}  // namespace
+
+TORCH_LIBRARY(intel_mlperf, m) {
+  m.def("lstm_amx_int8(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights, Tensor rb_scale, Tensor in_scale, "
+        "Tensor out_scale, bool skip_quant_y) -> (Tensor, Tensor[], Tensor[])");
+  m.def("stack_time(Tensor x, Tensor x_lens, int factor) -> Tensor");
+  m.def("lstm_amx_bf16(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights) -> (Tensor, Tensor[], Tensor[])");
+  m.def("amx_linear_bf16_accum_relu(Tensor f, Tensor w1_trans, Tensor g, Tensor w1_pred, Tensor bias) -> Tensor");
+  m.def("amx_linear_i16o32(Tensor y, Tensor w2, Tensor b2) -> Tensor");
+  m.def("greedy_decode_update(Tensor symbols, Tensor(b!) symbols_added, Tensor(c!) res, Tensor(d!) res_idx, "
+        "Tensor f, Tensor f_lens, Tensor(e!) time_idx, Tensor(f!) fi, Tensor(g!) pre_g, Tensor(h!)[] pre_hg, "
+        "Tensor(i!)[] pre_cg, Tensor[] hg, Tensor[] cg) -> bool");
+  m.def("prepack_lstm_weights(Tensor w_ih, Tensor w_hh) -> (Tensor, Tensor)");
+  m.def("prepack_linear_weight(Tensor w) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(intel_mlperf, CUDA, m) {
+  m.impl("lstm_amx_int8", lstm_amx_int8);
+  m.impl("stack_time", stack_time);
+  m.impl("lstm_amx_bf16", lstm_amx_bf16);
+  m.impl("amx_linear_bf16_accum_relu", amx_linear_bf16_accum_relu);
+  m.impl("amx_linear_i16o32", amx_linear_i16o32);
+  m.impl("greedy_decode_update", greedy_decode_update);
+}
+
+TORCH_LIBRARY_IMPL(intel_mlperf, CompositeExplicitAutograd, m) {
+  m.impl("prepack_lstm_weights", prepack_lstm_weights);
+  m.impl("prepack_linear_weight", prepack_linear_weight);
+}

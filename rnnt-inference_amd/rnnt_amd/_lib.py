@@ -73,7 +73,14 @@ _SIGS = {
     "rnnt_op_lstm_bf16": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_void_p]),
     "rnnt_op_joint_hidden": (C.c_int, [C.c_void_p] * 4 + [C.c_int, C.c_void_p]),
     "rnnt_op_joint_logits": (C.c_int, [C.c_void_p] * 3 + [C.c_int, C.c_void_p]),
-    "rnnt_op_greedy_update": (C.c_int, [C.c_void_p] * 15 + [C.c_int, C.c_int, C.c_int, C.c_void_p]),
+    "rnnt_op_greedy_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    "rnnt_engine_create_from_file": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(RnntOpts), C.POINTER(C.c_void_p)]),
+    "rnnt_engine_load_encoder_layers": (C.c_int, [C.c_void_p, C.c_int, C.c_int] + [C.c_void_p] * 5),
+    "rnnt_engine_load_prediction": (C.c_int, [C.c_void_p] * 6),
+    "rnnt_engine_load_joint": (C.c_int, [C.c_void_p] * 5),
+    "rnnt_engine_load_joint_out": (C.c_int, [C.c_void_p] * 3),
     "rnnt_engine_load_f32_encoder": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                                C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     "rnnt_engine_encode_f32": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,

@@ -33,8 +33,9 @@ def _ptr(t):
 
 
 class Engine:
-    def __init__(self, pm: PreparedModel, device=0, max_batch=1024, max_frames=R.MAX_FEA_LEN, max_res=None):
-        if not pm.bf16:
+    def __init__(self, pm: PreparedModel, device=0, max_batch=1024, max_frames=R.MAX_FEA_LEN, max_res=None,
+                 _path=None):
+        if pm is not None and not pm.bf16:
             raise ValueError("the engine is created from the int8 + bf16 model (enable_bf16); the fp32 path is "
                              "loaded on top with load_f32_encoder / load_f32_decoder")
         lib = _lib.lib()
@@ -52,6 +53,14 @@ class Engine:
         def bf(a):
             return arr(f32_to_bf16_bits(np.asarray(a, np.float32)), np.uint16)
 
+        opts = _lib.RnntOpts(self.max_batch, max_frames, self.max_res)
+        h = C.c_void_p()
+        self._lib = lib
+        if _path is not None:  # C-side loader (rnnt_engine_create_from_file)
+            _lib.check(lib.rnnt_engine_create_from_file(str(_path).encode(), device, C.byref(opts), C.byref(h)),
+                       "rnnt_engine_create_from_file")
+            self._h = h
+            return
         d = _lib.RnntModelDesc()
         for l in range(5):
             d.enc_w[l] = arr(pm.enc_w[l], np.int8)
@@ -71,11 +80,14 @@ class Engine:
         d.joint_bp = arr(pm.bp, np.float32)
         d.joint_w2 = bf(pm.w2)
         d.joint_b2 = arr(pm.b2, np.float32)
-        opts = _lib.RnntOpts(self.max_batch, max_frames, self.max_res)
-        h = C.c_void_p()
         _lib.check(lib.rnnt_engine_create(C.byref(d), device, C.byref(opts), C.byref(h)), "rnnt_engine_create")
         self._h = h
-        self._lib = lib
+
+    @classmethod
+    def from_file(cls, path, device=0, max_batch=1024, max_frames=R.MAX_FEA_LEN, max_res=None):
+        """An engine loaded by the C ABI from an engine model file (weights.save_engine_file /
+        tools/export_model.py --engine-file): the path a C++ SUT takes."""
+        return cls(None, device=device, max_batch=max_batch, max_frames=max_frames, max_res=max_res, _path=path)
 
     # ---------------------------------------------------------------- batch API
     def encode(self, feats, lens, lens_host=None, n=None, f_out=None, stream=None):
@@ -188,11 +200,20 @@ class Engine:
         _lib.check(rc, "rnnt_op_joint_logits")
 
     def op_greedy_update(self, symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg,
-                         hg, cg, finish, n, stream=None):
-        rc = self._lib.rnnt_op_greedy_update(self._h, *[_ptr(t) for t in (symbols, symbols_added, res, res_idx, f, f_lens,
-                                                                           time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg,
-                                                                           finish)],
-                                             n, fi.shape[0], res.shape[1], _stream_handle(stream))
+                         hg, cg, stream=None):
+        """greedy_decode_update on the reference's operands (rnnt_op_greedy_update): symbols int64
+        or int32 [n]; pre_hg / hg lists of 2 bf16 [n, 320]; pre_cg / cg lists of 2 fp32 [n, 320];
+        f [Tp, f_batch, 1024].  Returns all(finished)."""
+        import torch
+        n = symbols.shape[0]
+
+        def arr2(ts):
+            return (C.c_void_p * 2)(*[t.data_ptr() for t in ts])
+
+        rc = self._lib.rnnt_op_greedy_update(self._h, _ptr(symbols), int(symbols.dtype == torch.int64),
+                                             _ptr(symbols_added), _ptr(res), _ptr(res_idx), _ptr(f), f.shape[1],
+                                             _ptr(f_lens), _ptr(time_idx), _ptr(fi), _ptr(pre_g), arr2(pre_hg),
+                                             arr2(pre_cg), arr2(hg), arr2(cg), n, res.shape[1], _stream_handle(stream))
         if rc < 0:
             _lib.check(rc, "rnnt_op_greedy_update")
         return rc == 1

@@ -1,33 +1,155 @@
-"""The ``torch.ops.intel_mlperf`` operator surface of the hot path, backed by the HIP engine.
+"""The ``torch.ops.intel_mlperf`` operator surface of the hot path.
 
-Mirrors reference ``models/_C.py:15-51`` for the ops the RNN-T graph calls on its quantised
-path, with the argument meaning the reference call sites give them:
+The reference's graph binds its ops from a loaded library (models/_C.py:9-51); this package
+builds the MI355X one, ``libintel_mlperf_mi355x.so`` (csrc/torch_ops.cpp), which registers the
+same namespace and the schemas the call sites imply (quant_lstm.py:92-101, modeling_rnnt.py:202,
+269-283, 326-328, 351-365).  ``load_library()`` makes ``torch.ops.intel_mlperf.*`` available to
+Python and TorchScript (torch.jit.script / torch.jit.load graphs bind to it unchanged); the
+module-level functions below are those ops, so ``from rnnt_amd import ops as P`` can stand in
+for the reference's ``import _C as P``.
 
-  lstm_amx_int8(x, hx, cx, weights, rb_scale, in_scale, out_scale, skip_quant_y)
-        quant_lstm.py:92-101 -- one whole iLSTM stack (pre_rnn: 2 layers, post_rnn: 3)
-  stack_time(x, x_lens, factor)           modeling_rnnt.py:327
-  greedy_decode(...) / transcription      the fused hot loop behind TorchModel::encode/decode
-
-Weight layout: the reference pre-packs int8 weights into AMX tiles
-(quant_modules.transpose_tile_weight); the engine packs its own MFMA layout from the
-*natural* int8 matrices iLSTMLayer._quant_parameters computes (quant_lstm.py:193-215), so the
-``weights`` argument here is [[W_ih_q, W_hh_q, b_ih, b_q], ...] in natural [4H, I] layout.
-The kernels run on the weights bound at ``bind(engine, model)`` (the engine is the device-side
-owner of the packed model, like the TorchScript module owns the reference's packed tensors);
-the passed tensors are checked for shape and against the bound model.
+The ops compute with the weights they are passed, in the reference's prepacked layouts
+(``reference_weights`` builds them from a PreparedModel exactly as the reference's model build
+does) or natural layouts.  ``transcription`` / ``greedy_decode`` are the fused engine paths
+behind TorchModel::encode / decode (bound with ``bind``), used by GreedyDecoder.
 
 Errors follow the reference's TORCH_CHECK convention: invalid arguments raise RuntimeError.
 """
+import os
+
 import numpy as np
 
-from .config import ENC_INPUT_SIZES, RNNTParam as R
+from .config import RNNTParam as R
 from .engine import pad_batch
 
+_HERE = os.path.dirname(os.path.abspath(__file__))
+OPS_LIB = os.path.join(_HERE, "libintel_mlperf_mi355x.so")
+_loaded = False
 _bound = {"engine": None, "model": None}
 
 
+def load_library(path=OPS_LIB):
+    """torch.ops.load_library of the operator library (no fallback: a missing library raises)."""
+    global _loaded
+    if not _loaded:
+        import torch
+        from . import _lib
+        if not os.path.exists(path):
+            raise RuntimeError(f"operator library missing: {path} (build with `make -C {_lib.CSRC}`)")
+        _lib.lib()  # the engine first: torch's HIP runtime, one per process
+        torch.ops.load_library(path)
+        _loaded = True
+    import torch
+    return torch.ops.intel_mlperf
+
+
+def lstm_amx_int8(x, hx, cx, weights, rb_scale, in_scale, out_scale, skip_quant_y):
+    """quant_lstm.py:92-101: one iLSTM stack (pre_rnn 2 layers on fp32 x, post_rnn 3 on int8)."""
+    return load_library().lstm_amx_int8(x, hx, cx, weights, rb_scale, in_scale, out_scale, skip_quant_y)
+
+
+def stack_time(x, x_lens, factor):
+    """modeling_rnnt.py:326-328."""
+    return load_library().stack_time(x, x_lens, factor)
+
+
+def lstm_amx_bf16(x, hx, cx, weights):
+    """modeling_rnnt.py:202."""
+    return load_library().lstm_amx_bf16(x, hx, cx, weights)
+
+
+def amx_linear_bf16_accum_relu(f, w1_trans, g, w1_pred, bias):
+    """modeling_rnnt.py:269-275."""
+    return load_library().amx_linear_bf16_accum_relu(f, w1_trans, g, w1_pred, bias)
+
+
+def amx_linear_i16o32(y, w2, b2):
+    """modeling_rnnt.py:280-283: logits fp32 [N, 32] (29 labels + zero padding)."""
+    return load_library().amx_linear_i16o32(y, w2, b2)
+
+
+def greedy_decode_update(symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg):
+    """modeling_rnnt.py:331-365, in place; returns all(finished)."""
+    return load_library().greedy_decode_update(symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g,
+                                               pre_hg, pre_cg, hg, cg)
+
+
+# ---------------------------------------------------------------- reference-format weights
+def amx_tiles_int8(wt):
+    """transpose_tile_weight (quant_modules.py:175-191, padding=True) of W^T [K, O] int8:
+    tiles [O/64][4][ceil(K/64)][16][64], element (k, o) at [o/64][(o%64)/16][k/64][(k%64)/4][4(o%16)+k%4]."""
+    wt = np.asarray(wt, np.int8)
+    K, O = wt.shape
+    ct, cs = (K + 63) // 64, (O + 63) // 64
+    w = np.zeros((ct * 64, cs * 64), np.int8)
+    w[:K, :O] = wt
+    # k = 64 kt + 4 r + kk, o = 64 s + 16 j + oo  ->  [s][j][kt][r][4 oo + kk]
+    return np.ascontiguousarray(w.reshape(ct, 16, 4, cs, 4, 16).transpose(3, 4, 0, 1, 5, 2).reshape(cs, 4, ct, 16, 64))
+
+
+def amx_tiles_bf16(wt_bits):
+    """transpose_tile_weight_bf16 (quant_modules.py:158-172, padding=True) of W^T [K, O] (bf16 bits):
+    tiles [ceil(O/32)][2][K/32][16][32], element (k, o) at [o/32][(o%32)/16][k/32][(k%32)/2][2(o%16)+k%2]."""
+    wt = np.asarray(wt_bits, np.uint16)
+    K, O = wt.shape
+    ct, cs = (K + 31) // 32, (O + 31) // 32
+    w = np.zeros((ct * 32, cs * 32), np.uint16)
+    w[:K, :O] = wt
+    # k = 32 kt + 2 r + kk, o = 32 s + 16 j + oo  ->  [s][j][kt][r][2 oo + kk]
+    return np.ascontiguousarray(w.reshape(ct, 16, 2, cs, 2, 16).transpose(3, 4, 0, 1, 5, 2).reshape(cs, 2, ct, 16, 32))
+
+
+def reference_weights(pm, device="cpu"):
+    """The weight tensors the reference graph hands the ops, built from a PreparedModel the way
+    the reference's model build lays them out: iLSTM.weights = [[tiles(W_ih_q^T), tiles(W_hh_q^T),
+    b_ih, b_q]] + rb/in/out scale tensors (quant_lstm.py:193-215), Prediction weights =
+    [[tiles(W_ih^T), tiles(W_hh^T), b_ih, b_hh + b_ih]] (modeling_rnnt.py:161-181), joint
+    tiles + linear1 bias = b_trans + b_pred + zero-padded linear2 (:223-257)."""
+    import torch
+    from .weights import f32_to_bf16_bits
+    H = R.trans_hidden_size
+
+    def bft(a_bits):
+        return torch.from_numpy(a_bits.view(np.int16)).view(torch.bfloat16).to(device)
+
+    def f32(a):
+        return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(device)
+
+    enc = []
+    for l in range(5):
+        w = pm.enc_w[l]
+        I = w.shape[1] - H
+        wih = w[:, :I] if l else w[:, :R.trans_input_size]  # first layer: 240 real columns, padded by the tiling
+        enc.append([torch.from_numpy(amx_tiles_int8(wih.T)).to(device), torch.from_numpy(amx_tiles_int8(w[:, I:].T)).to(device),
+                    f32(np.zeros(4 * H)), f32(pm.enc_bq[l])])
+    scales = {k: f32(getattr(pm, "enc_" + k)) for k in ("rb", "in_s", "out_s")}
+    pred = []
+    for l in range(R.pred_num_layers):
+        pred.append([bft(amx_tiles_bf16(f32_to_bf16_bits(pm.pred_wih[l]).T)),
+                     bft(amx_tiles_bf16(f32_to_bf16_bits(pm.pred_whh[l]).T)),
+                     f32(pm.pred_bih[l]), f32(np.asarray(pm.pred_bhh[l], np.float32) + np.asarray(pm.pred_bih[l], np.float32))])
+    joint = dict(w1_trans=bft(amx_tiles_bf16(f32_to_bf16_bits(pm.w1t).T)),
+                 w1_pred=bft(amx_tiles_bf16(f32_to_bf16_bits(pm.w1p).T)),
+                 bias=f32(np.asarray(pm.bt, np.float32) + np.asarray(pm.bp, np.float32)),
+                 w2=bft(amx_tiles_bf16(f32_to_bf16_bits(pm.w2).T)), b2=f32(np.pad(pm.b2, (0, 3))))
+    embed = bft(f32_to_bf16_bits(pm.embed))
+    return dict(pre=enc[:2], post=enc[2:], pre_scales=[scales[k][:2] for k in ("rb", "in_s", "out_s")],
+                post_scales=[scales[k][2:] for k in ("rb", "in_s", "out_s")], pred=pred, embed=embed, **joint)
+
+
+def op_model(pm):
+    """The PreparedModel the op path is numerically equivalent to: prediction b_hh recovered from
+    the reference's fused slot as fp32((b_hh + b_ih) - b_ih) (csrc/torch_ops.cpp lstm_amx_bf16)."""
+    import copy
+    m = copy.copy(pm)
+    m.pred_bhh = [((np.asarray(bh, np.float32) + np.asarray(bi, np.float32)) - np.asarray(bi, np.float32)).astype(np.float32)
+                  for bh, bi in zip(pm.pred_bhh, pm.pred_bih)]
+    return m
+
+
+# ---------------------------------------------------------------- fused engine paths
 def bind(engine, model):
-    """Register the engine (and its PreparedModel) the ops dispatch to."""
+    """Register the engine (and its PreparedModel) the fused transcription / greedy_decode use."""
     _bound["engine"], _bound["model"] = engine, model
 
 
@@ -36,75 +158,6 @@ def _engine():
     if e is None:
         raise RuntimeError("rnnt_amd.ops: no engine bound (call ops.bind(engine, model))")
     return e
-
-
-def _check(cond, msg):
-    if not cond:
-        raise RuntimeError(msg)
-
-
-def _pad_rows(t, n_pad, dim=1):
-    import torch
-    n = t.shape[dim]
-    if n == n_pad:
-        return t.contiguous()
-    shape = list(t.shape)
-    shape[dim] = n_pad
-    out = torch.zeros(shape, dtype=t.dtype, device=t.device)
-    out.narrow(dim, 0, n).copy_(t)
-    return out
-
-
-def lstm_amx_int8(x, hx, cx, weights, rb_scale, in_scale, out_scale, skip_quant_y):
-    """quant_lstm.py:80-102.  pre_rnn: x fp32 [T, N, 240|256] (quantised with in_scale[0]),
-    post_rnn: x int8 [T, N, 2048]; hx: list of int8 [N, 1024]; cx: list of fp16 [N, 1024].
-    Returns (y, hx', cx'): y int8 [T, N, 1024], or fp32 when skip_quant_y (post_rnn)."""
-    import torch
-    e = _engine()
-    pm = _bound["model"]
-    L = len(weights)
-    _check(L in (R.pre_num_layers, R.post_num_layers), "lstm_amx_int8: expected 2 (pre_rnn) or 3 (post_rnn) layers")
-    first = 0 if L == R.pre_num_layers and x.dtype == torch.float32 else R.pre_num_layers
-    _check(len(hx) == L and len(cx) == L, "lstm_amx_int8: hx/cx must have one tensor per layer")
-    _check(bool(skip_quant_y) == (first + L == 5), "lstm_amx_int8: skip_quant_y is set exactly for post_rnn")
-    for i, w in enumerate(weights):
-        l = first + i
-        K = ENC_INPUT_SIZES[l] + R.trans_hidden_size
-        wih, whh = w[0], w[1]
-        _check(tuple(wih.shape)[0] == 4 * R.trans_hidden_size and wih.shape[1] + whh.shape[1] in (K, K - 16),
-               f"lstm_amx_int8: layer {i} weight shape {tuple(wih.shape)} / {tuple(whh.shape)}")
-        if pm is not None:
-            _check(float(rb_scale[i]) == float(pm.enc_rb[l]) and float(in_scale[i]) == float(pm.enc_in_s[l]),
-                   "lstm_amx_int8: scales differ from the bound model")
-    T, N = x.shape[0], x.shape[1]
-    n_pad = pad_batch(N)
-    if first == 0:
-        xin = torch.zeros((T, n_pad, R.PADDED_INPUT_SIZE), dtype=torch.float32, device=x.device)
-        xin[:, :N, : x.shape[2]] = x
-    else:
-        _check(x.dtype == torch.int8 and x.shape[2] == 2 * R.trans_hidden_size, "lstm_amx_int8: post_rnn x int8 [T,N,2048]")
-        xin = _pad_rows(x, n_pad)
-    h = torch.stack([_pad_rows(t, n_pad, 0) for t in hx]).contiguous()
-    c = torch.stack([_pad_rows(t.view(torch.int16), n_pad, 0) for t in cx]).contiguous()
-    ydt = torch.float32 if skip_quant_y else torch.int8
-    y = torch.empty((T, n_pad, R.trans_hidden_size), dtype=ydt, device=x.device)
-    e.lstm_int8(first, L, xin, h, c, y)
-    return (y[:, :N], [h[i, :N] for i in range(L)], [c[i, :N].view(torch.float16) for i in range(L)])
-
-
-def stack_time(x, x_lens, factor):
-    """modeling_rnnt.py:326-328: int8 [T, N, C] -> [ceil(T/2), N, 2C], frames >= x_lens zeroed."""
-    import torch
-    _check(factor == R.stack_time_factor, "stack_time: factor must be 2")
-    _check(x.dtype == torch.int8, "stack_time: int8 input")
-    T, N, C = x.shape
-    n_pad = pad_batch(N)
-    xin = _pad_rows(x, n_pad)
-    lens = torch.zeros(n_pad, dtype=torch.int32, device=x.device)
-    lens[:N] = x_lens.to(torch.int32)
-    y = torch.empty(((T + 1) // 2, n_pad, 2 * C), dtype=torch.int8, device=x.device)
-    _engine().stack_time(xin, lens, y)
-    return y[:, :N]
 
 
 def transcription(x, x_lens, f_out=True):
@@ -136,75 +189,3 @@ def greedy_decode(n, max_res=None):
     rl = torch.empty(n, dtype=torch.int32, device="cuda")
     e.decode(res, rl)
     return res, rl
-
-
-# ---------------------------------------------------------------- decode operators
-# The reference's op-by-op greedy loop (models/decoder.py:171-212) calls these four; tensors use
-# torch's bfloat16 / float32 / int32 dtypes and the reference's shapes.  Weight arguments are
-# accepted for signature compatibility and checked against the bound model's shapes; the
-# engine computes with its own packed copy (as for lstm_amx_int8).
-
-def _bits(t):
-    import torch
-    return t.contiguous().view(torch.int16)
-
-
-def lstm_amx_bf16(x, hx, cx, weights=None):
-    """modeling_rnnt.py:202: x bf16 [1, N, 320]; hx: 2 x bf16 [N, 320]; cx: 2 x fp32 [N, 320]
-    -> (g bf16 [1, N, 320], hy, cy)."""
-    import torch
-    e = _engine()
-    N = x.shape[-2]
-    _check(x.shape[-1] == R.pred_hidden_size and len(hx) == 2 and len(cx) == 2, "lstm_amx_bf16: bad shapes")
-    n_pad = (N + 15) // 16 * 16
-    xb = torch.zeros((n_pad, R.pred_hidden_size), dtype=torch.bfloat16, device=x.device)
-    xb[:N] = x.reshape(N, -1)
-    h = torch.zeros((2, n_pad, R.pred_hidden_size), dtype=torch.bfloat16, device=x.device)
-    c = torch.zeros((2, n_pad, R.pred_hidden_size), dtype=torch.float32, device=x.device)
-    for l in range(2):
-        h[l, :N] = hx[l]
-        c[l, :N] = cx[l]
-    hy, cy = torch.empty_like(h), torch.empty_like(c)
-    e.op_lstm_bf16(_bits(xb), _bits(h), c, _bits(hy).view(torch.int16), cy)
-    return hy[1, :N].unsqueeze(0), [hy[0, :N], hy[1, :N]], [cy[0, :N], cy[1, :N]]
-
-
-def amx_linear_bf16_accum_relu(f, w1_trans=None, g=None, w1_pred=None, bias=None):
-    """modeling_rnnt.py:269-275: f [N, 1024] (fp32 or bf16), g bf16 [N, 320] -> y1 bf16 [N, 512]."""
-    import torch
-    e = _engine()
-    N = f.shape[0]
-    n_pad = (N + 15) // 16 * 16
-    fp = torch.zeros((n_pad, R.trans_hidden_size), dtype=torch.float32, device=f.device)
-    fp[:N] = f.float()
-    gp = torch.zeros((n_pad, R.pred_hidden_size), dtype=torch.bfloat16, device=f.device)
-    gp[:N] = g.reshape(N, -1)
-    y1 = torch.empty((n_pad, R.joint_hidden_size), dtype=torch.bfloat16, device=f.device)
-    e.op_joint_hidden(fp, _bits(gp), y1.view(torch.int16))
-    return y1[:N]
-
-
-def amx_linear_i16o32(y, w2=None, b2=None):
-    """modeling_rnnt.py:280-283: y1 bf16 [N, 512] -> logits fp32 [N, 32] (29 labels + zero pad)."""
-    import torch
-    e = _engine()
-    N = y.shape[0]
-    n_pad = (N + 15) // 16 * 16
-    yp = torch.zeros((n_pad, R.joint_hidden_size), dtype=torch.bfloat16, device=y.device)
-    yp[:N] = y
-    logits = torch.empty((n_pad, 32), dtype=torch.float32, device=y.device)
-    e.op_joint_logits(yp.view(torch.int16), logits)
-    return logits[:N]
-
-
-def greedy_decode_update(symbols, symbols_added, res, res_idx, f, f_lens, time_idx, fi, pre_g, pre_hg, pre_cg, hg, cg,
-                         finish):
-    """modeling_rnnt.py:331-365 (spec decoder.py:125-167), in place.  Device tensors: symbols,
-    symbols_added, res_idx, f_lens, time_idx, finish int32 [N]; res int32 [N, max_res]; f fp32
-    [T', n_pad, 1024]; fi fp32 [n_pad, 1024]; pre_g int32 [N]; pre_hg / hg bf16 [2, n_pad, 320];
-    pre_cg / cg fp32 [2, n_pad, 320].  Returns all(finish)."""
-    import torch
-    e = _engine()
-    N = symbols.shape[0]
-    return e.op_greedy_update(symbols.to(torch.int32).contiguous(), symbols_added, res, res_idx, f, f_lens, time_idx, fi,
-                              pre_g, pre_hg.view(torch.int16), pre_cg, hg.view(torch.int16), cg, finish, N)

