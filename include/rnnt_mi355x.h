@@ -113,6 +113,14 @@ int rnnt_engine_load_joint_out(rnnt_engine* e, const uint16_t* w2, const float* 
 int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
                        int T, int n, int n_pad, float* f_out, void* stream);
 
+/* encode with AssembleSamples (rnnt_qsl.cpp:150-188) fused into the input quantizer: the batch is
+ * gathered straight from the QSL's ragged sample store -- store device fp32 [rows][240] (each
+ * sample's [T_i][240] frames back to back, LoadSamplesToRam), offsets device int64 [n] (first
+ * row of batch row i's sample), lens device int32 [n_pad] / lens_host int32 [n] (required; every
+ * length <= T).  No assembled [T][n_pad][256] copy is made. */
+int rnnt_engine_encode_gather(rnnt_engine* e, const float* store, const int64_t* offsets, const int32_t* lens,
+                              const int32_t* lens_host, int T, int n, int n_pad, float* f_out, void* stream);
+
 /* Greedy decode of the last encoded batch: res device int32 [n][max_res] (filled with -1 first),
  * res_len device int32 [n]. */
 int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream);

@@ -49,6 +49,27 @@ __global__ void __launch_bounds__(256) quantize_kernel(const float4* __restrict_
   }
 }
 
+// AssembleSamples (rnnt_qsl.cpp:150-188) fused with the quantizer: one thread per 4 output
+// channels, a wave covers one (frame, row) pair's 256 channels as 64 x 4 B (the 240 real
+// channels are one contiguous 960-byte run of the sample's stored frame).
+__global__ void __launch_bounds__(256) quantize_gather_kernel(const float* __restrict__ store,
+                                                              const int64_t* __restrict__ offsets,
+                                                              const int32_t* __restrict__ lens, int n, int n_pad,
+                                                              int64_t words, float s, uint32_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i & 63);
+    const int64_t rt = i >> 6;  // t * n_pad + row
+    const int row = (int)(rt % n_pad), t = (int)(rt / n_pad);
+    uint32_t v = 0;
+    if (row < n && c4 < 60 && t < lens[row]) {
+      const float4 x = *(const float4*)(store + (offsets[row] + t) * 240 + 4 * c4);
+      v = (uint32_t)(uint8_t)q8(x.x * s) | ((uint32_t)(uint8_t)q8(x.y * s) << 8) |
+          ((uint32_t)(uint8_t)q8(x.z * s) << 16) | ((uint32_t)(uint8_t)q8(x.w * s) << 24);
+    }
+    out[i] = v;
+  }
+}
+
 // ---------------------------------------------------------------- LSTM step
 // Workgroup tile: 256 packed gate rows (64 units) x 256 batch rows, K swept in 64-byte
 // steps.  8 waves as 4 (gate) x 2 (batch); each wave owns 64 gate rows x 128 batch rows =
@@ -686,6 +707,17 @@ int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStrea
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(quantize_kernel, dim3(grid), dim3(256), 0, st, (const float4*)feat, n4, s, (uint32_t*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_quantize_gather(const float* store, const int64_t* offsets, const int32_t* lens, int T, int n, int n_pad,
+                           float s, int8_t* out, hipStream_t st) {
+  const int64_t words = (int64_t)T * n_pad * 64;
+  int grid = (int)((words + 255) / 256);
+  if (grid > 16384) grid = 16384;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(quantize_gather_kernel, dim3(grid), dim3(256), 0, st, store, offsets, lens, n, n_pad, words, s,
+                     (uint32_t*)out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -54,6 +54,11 @@ struct EncTickArgs {
 };
 
 int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStream_t st);
+// AssembleSamples + the layer-0 input quantizer in one pass: row i of the batch is the QSL sample
+// stored at store[offsets[i] * 240 ...] (LoadSamplesToRam's [T_i][240] fp32 rows, ragged), frames
+// t < lens[i]; out int8 [T][n_pad][256], zero past the length, in channels 240..255 and rows >= n.
+int launch_quantize_gather(const float* store, const int64_t* offsets, const int32_t* lens, int T, int n, int n_pad,
+                           float s, int8_t* out, hipStream_t st);
 int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st);
 
 }  // namespace rnnt

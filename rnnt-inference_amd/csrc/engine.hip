@@ -570,9 +570,17 @@ static std::vector<int> tile_maxima(const int32_t* lens_host, int n, int n_pad) 
   return tm;
 }
 
-extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
-                                  int T, int n, int n_pad, float* f_out, void* stream) {
-  if (!e || !feats || !lens) return fail(RNNT_EINVAL, "null argument");
+// The input of encode: an assembled [T][n_pad][256] fp32 batch, or the QSL's ragged sample store
+// gathered in the quantize pass (store != nullptr).
+struct EncInput {
+  const float* feats = nullptr;
+  const float* store = nullptr;
+  const int64_t* offsets = nullptr;
+};
+
+static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, const int32_t* lens_host, int T, int n,
+                       int n_pad, float* f_out, void* stream) {
+  if (!e || !lens || !(in.feats || (in.store && in.offsets))) return fail(RNNT_EINVAL, "null argument");
   if (e->enc_loaded != 0x1f) return fail(RNNT_EINVAL, "encoder weights not loaded");
   int r = check_batch(e, T, n, n_pad);
   if (r) return r;
@@ -586,7 +594,8 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
     HIPCHK(hipMemsetAsync(e->c[l], 0, (size_t)n_pad * H * 2, st));
   }
   hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
-  if (launch_quantize(feats, (int64_t)T * n_pad * FEAT, e->in_s[0], e->x0q, st))
+  if (in.store ? launch_quantize_gather(in.store, in.offsets, lens, T, n, n_pad, e->in_s[0], e->x0q, st)
+               : launch_quantize(in.feats, (int64_t)T * n_pad * FEAT, e->in_s[0], e->x0q, st))
     return fail(RNNT_EDEVICE, "quantize launch failed");
   // Wavefront schedule: tick tau runs layer 0 at frame tau, layer 1 at frame tau-1, and the
   // post_rnn layers 2/3/4 at stacked frame t' on ticks 2t'+3 / 2t'+4 / 2t'+5, i.e. as soon as
@@ -621,6 +630,25 @@ extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int3
   e->last_n = n;
   e->last_npad = n_pad;
   return 0;
+}
+
+extern "C" int rnnt_engine_encode(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host,
+                                  int T, int n, int n_pad, float* f_out, void* stream) {
+  EncInput in;
+  in.feats = feats;
+  return encode_impl(e, in, lens, lens_host, T, n, n_pad, f_out, stream);
+}
+
+extern "C" int rnnt_engine_encode_gather(rnnt_engine* e, const float* store, const int64_t* offsets,
+                                         const int32_t* lens, const int32_t* lens_host, int T, int n, int n_pad,
+                                         float* f_out, void* stream) {
+  if (!lens_host) return fail(RNNT_EINVAL, "encode_gather needs the host lengths");
+  for (int i = 0; i < n; ++i)
+    if (lens_host[i] < 0 || lens_host[i] > T) return fail(RNNT_EINVAL, "a length exceeds T");
+  EncInput in;
+  in.store = store;
+  in.offsets = offsets;
+  return encode_impl(e, in, lens, lens_host, T, n, n_pad, f_out, stream);
 }
 
 extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream) {

@@ -69,6 +69,8 @@ _SIGS = {
     "rnnt_engine_destroy": (None, [C.c_void_p]),
     "rnnt_engine_encode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                      C.c_void_p, C.c_void_p]),
+    "rnnt_engine_encode_gather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                            C.c_int, C.c_void_p, C.c_void_p]),
     "rnnt_engine_decode": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "rnnt_op_lstm_bf16": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_void_p]),
     "rnnt_op_joint_hidden": (C.c_int, [C.c_void_p] * 4 + [C.c_int, C.c_void_p]),

@@ -102,6 +102,15 @@ class Engine:
                                           T, n, n_pad, _ptr(f_out), _stream_handle(stream))
         _lib.check(rc, "rnnt_engine_encode")
 
+    def encode_gather(self, store, offsets, lens, lens_host, T, n, n_pad, f_out=None, stream=None):
+        """encode with AssembleSamples fused into the quantizer: store cuda fp32 [rows, 240] (the
+        QSL's ragged samples), offsets cuda int64 [n], lens cuda int32 [n_pad], lens_host [n]."""
+        assert store.is_contiguous() and store.shape[1] == R.trans_input_size and offsets.dtype.itemsize == 8
+        lh = np.ascontiguousarray(lens_host, np.int32)
+        rc = self._lib.rnnt_engine_encode_gather(self._h, _ptr(store), _ptr(offsets), _ptr(lens), lh.ctypes.data, T, n,
+                                                 n_pad, _ptr(f_out), _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_encode_gather")
+
     def decode(self, res, res_len, stream=None):
         """res: cuda int32 [n, max_res]; res_len: cuda int32 [n]."""
         rc = self._lib.rnnt_engine_decode(self._h, _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))

@@ -2,21 +2,22 @@
 
 Mirrors the reference's LoadGen-facing surface (the real MLPerf LoadGen is not installable
 offline, so the query / response types are plain Python):
-  * ``RNNTQSL``   csrc/rnnt_qsl.{hpp,cpp} / models/rnnt_qsl.py: holds per-sample features
-                  [T_i, 240] and lengths; ``sort`` is the length-descending bucket sort
-                  (rnnt_qsl.cpp:104-133); ``assemble`` pads a batch to [T_max, n_pad, 256]
-                  (AssembleSamples, rnnt_qsl.cpp:150-188).
-  * ``OfflineSUT`` csrc/torch_sut.cpp:88-236 / models/pytorch_sut.py:58-118: issue_queries
-                  sorts, takes <= batch_size samples per batch, runs encode+decode on its GPU
-                  and completes each sample with its int32 token row (res_len*4 bytes,
-                  QuerySamplesComplete, torch_sut.cpp:221-236).
-Multi-GPU: one process per GPU, each with its own engine(s); a query's sorted samples are
-dealt to ranks in batch-sized chunks (snake order, so every rank gets the same length mix).
-There is no data-path collective: results are completed per rank.  Within a GPU, several
-engines (each with its own HIP stream and host thread, like the reference's INTER worker
-threads, torch_sut.cpp:143-182) keep batches in flight; encoders take turns so one batch's
-latency-bound greedy decode overlaps the next batch's encoder.
+  * QSLs (csrc/rnnt_qsl.{hpp,cpp} / models/rnnt_qsl.py): per-sample features and lengths;
+    ``sort`` is the length-descending bucket sort (rnnt_qsl.cpp:104-133); ``batch_inputs`` is
+    AssembleSamples (rnnt_qsl.cpp:150-188) -- for the HBM-resident ``GpuQSL`` it hands the engine
+    the ragged store and the batch's row offsets, which the engine gathers inside its quantize pass.
+  * ``OfflineSUT`` (csrc/torch_sut.cpp:88-236 / models/pytorch_sut.py:58-118): issue_queries sorts
+    the query, splits it into batches and runs them through its engines -- one host thread per
+    engine pulling batches from one shared work list (the reference's INTER worker threads pulling
+    from one queue, torch_sut.cpp:143-182) -- and completes every sample with its int32 token row
+    (QuerySamplesComplete, torch_sut.cpp:221-236) through one completion point.  Engines may sit on
+    several GPUs of the process (one stream per engine on its own device; encoders on one device
+    take turns, so each batch's latency-bound greedy decode overlaps the next batch's encoder).
+Multi-process (one process per GPU, bench.py / rnnt_amd.dist): every rank sorts the same query,
+``dist.shard_query`` deals the batches to ranks (snake order), each rank runs its share through
+its OfflineSUT, and the responses are gathered to rank 0's host (``dist.gather_responses``).
 """
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -31,7 +32,25 @@ class QuerySample:
     index: int
 
 
-class RNNTQSL:
+class _SortedQSL:
+    def __len__(self):
+        return self.count
+
+    def sort_indices(self, indices):
+        """Positions of `indices` in longest-first order, stable (the bucket sort's order)."""
+        return np.argsort(-self.lengths[np.asarray(indices, np.int64)], kind="stable")
+
+    def sort(self, samples, reverse=True):
+        """Bucket sort by feature length, longest first (rnnt_qsl.cpp:104-133)."""
+        lmin, lmax = int(self.lengths.min()), int(self.lengths.max())
+        buckets = [[] for _ in range(lmax - lmin + 1)]
+        for s in samples:
+            L = int(self.lengths[s.index])
+            buckets[(lmax - L) if reverse else (L - lmin)].append(s)
+        return [s for b in buckets for s in b]
+
+
+class RNNTQSL(_SortedQSL):
     def __init__(self, features, lengths):
         """features: list of [T_i, 240] float32 arrays (or None for synthetic on-demand);
         lengths: int array [count]."""
@@ -44,18 +63,6 @@ class RNNTQSL:
         rng = np.random.default_rng(seed)
         feats = [rng.standard_normal((int(l), R.trans_input_size), dtype=np.float32) for l in lengths]
         return cls(feats, lengths)
-
-    def __len__(self):
-        return self.count
-
-    def sort(self, samples, reverse=True):
-        """Bucket sort by feature length, longest first (rnnt_qsl.cpp:104-133)."""
-        lmin, lmax = int(self.lengths.min()), int(self.lengths.max())
-        buckets = [[] for _ in range(lmax - lmin + 1)]
-        for s in samples:
-            L = int(self.lengths[s.index])
-            buckets[(lmax - L) if reverse else (L - lmin)].append(s)
-        return [s for b in buckets for s in b]
 
     def assemble(self, indices, n_pad=None):
         """-> (x [T_max, n_pad, 256] f32, lens [n_pad] int32), zero padded (rnnt_qsl.cpp:150-188)."""
@@ -70,101 +77,178 @@ class RNNTQSL:
             x[: f.shape[0], i, : R.trans_input_size] = f
         return x, lens
 
+    def batch_inputs(self, indices, n_pad, device):
+        import torch
+        x, lens = self.assemble(indices, n_pad)
+        return dict(x=torch.from_numpy(x).to(device), lens=torch.from_numpy(lens).to(device),
+                    lens_host=lens[: len(indices)], T=x.shape[0])
 
-def deal_batches(sorted_samples, batch_size, rank=0, world=1):
-    """Split a length-sorted query into batch_size chunks and deal them to ranks in snake
-    order (0,1,..,w-1,w-1,..,0,0,..) so every rank gets a similar share of long and short
-    utterances; returns this rank's chunks."""
-    chunks = [sorted_samples[i:i + batch_size] for i in range(0, len(sorted_samples), batch_size)]
-    mine = []
-    for i, ch in enumerate(chunks):
-        r = i % world if (i // world) % 2 == 0 else world - 1 - (i % world)
-        if r == rank:
-            mine.append(ch)
-    return mine
+
+def batch_bounds(n, batch, sizes=None):
+    """Start/end of each batch over a sorted query: ``sizes`` (the last entry repeats) or uniform
+    ``batch``."""
+    out, i, k = [], 0, 0
+    while i < n:
+        b = sizes[min(k, len(sizes) - 1)] if sizes else batch
+        out.append((i, min(n, i + b)))
+        i += b
+        k += 1
+    return out
+
+
+def make_batches(qsl, ids, idx, batch_size, sizes=None):
+    """An Offline query (sample ids, QSL indices) sorted longest first (rnnt_qsl.cpp:104-133) and
+    split into batches: a list of (ids, idx) array pairs."""
+    order = qsl.sort_indices(idx)
+    ids, idx = np.asarray(ids, np.int64)[order], np.asarray(idx, np.int64)[order]
+    return [(ids[i:e], idx[i:e]) for i, e in batch_bounds(len(ids), batch_size, sizes)]
 
 
 class OfflineSUT:
-    def __init__(self, engine, qsl, batch_size=1024, rank=0, world=1, on_complete=None):
-        """engine: one Engine, or a list of Engines on this GPU (one batch in flight each)."""
-        self.engines = list(engine) if isinstance(engine, (list, tuple)) else [engine]
+    def __init__(self, engines, qsl, batch_size=1024, batch_sizes=None, on_complete=None):
+        """engines: one Engine or a list (several per GPU keep batches in flight; engines on
+        different devices serve one query together).  qsl: one QSL, or {device: QSL} when each
+        GPU holds its own copy of the samples (GpuQSL replicas)."""
+        self.engines = list(engines) if isinstance(engines, (list, tuple)) else [engines]
         self.engine = self.engines[0]
-        self.qsl, self.batch_size = qsl, batch_size
-        self.rank, self.world = rank, world
+        self.qsl, self.batch_size, self.batch_sizes = qsl, batch_size, batch_sizes
         self.on_complete = on_complete
-        self.responses = {}
+        self._done_lock = threading.Lock()
+        self.completed = []  # per batch: (sample ids int64 [n], lengths int32 [n], tokens int32 [sum])
+        self._streams = {}
+        self._enc_locks = {}
+
+    def qsl_for(self, device):
+        return self.qsl[device] if isinstance(self.qsl, dict) else self.qsl
 
     def issue_queries(self, samples):
-        import threading
+        """LoadGen's IssueQuery: sort the query longest first, batch it, run it."""
+        ids = np.fromiter((s.id for s in samples), np.int64, len(samples))
+        idx = np.fromiter((s.index for s in samples), np.int64, len(samples))
+        self.issue_batches(make_batches(self.qsl_for(self.engine.device), ids, idx, self.batch_size, self.batch_sizes))
+
+    def issue_batches(self, batches):
+        """Run pre-formed batches -- (sample ids, QSL indices) int64 array pairs, each
+        length-sorted (make_batches) -- on the engines: one host thread per engine pulls the next
+        batch from the shared list.  self.batch_engine[i] records which engine ran batch i."""
         import torch
-        batches = deal_batches(self.qsl.sort(samples), self.batch_size, self.rank, self.world)
-        k = len(self.engines)
-        streams = [torch.cuda.Stream() for _ in range(k)] if k > 1 else [torch.cuda.current_stream()]
-        done = [None] * len(batches)
-        enc_lock = threading.Lock()
+        nxt = [0]
+        take = threading.Lock()
+        errors = []
+        self.batch_engine = [None] * len(batches)
+        for eng in self.engines:
+            if id(eng) not in self._streams:
+                self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
+            self._enc_locks.setdefault(eng.device, threading.Lock())
 
-        def worker(j):
-            eng, st = self.engines[j], streams[j]
-            for bi in range(j, len(batches), k):
-                batch = batches[bi]
-                x, lens = self.qsl.assemble([s.index for s in batch])
-                n = len(batch)
-                with torch.cuda.stream(st):
-                    xd = torch.from_numpy(x).cuda()
-                    ld = torch.from_numpy(lens).cuda()
-                    res = torch.empty((n, eng.max_res), dtype=torch.int32, device="cuda")
-                    rl = torch.empty(n, dtype=torch.int32, device="cuda")
-                with enc_lock:
-                    eng.encode(xd, ld, lens[:n], n=n, stream=st)
-                    st.synchronize()
-                eng.decode(res, rl, stream=st)
-                done[bi] = (batch, res, rl, xd, ld)
+        def worker(eng):
+            try:
+                while True:
+                    with take:
+                        i = nxt[0]
+                        nxt[0] += 1
+                    if i >= len(batches):
+                        return
+                    self.batch_engine[i] = self.engines.index(eng)
+                    self._run_batch(eng, *batches[i])
+            except Exception as ex:  # surfaced below: never leave the query half-complete silently
+                errors.append(ex)
 
-        if k == 1:
-            worker(0)
+        if len(self.engines) == 1:
+            worker(self.engines[0])
         else:
-            ths = [threading.Thread(target=worker, args=(j,)) for j in range(k)]
+            ths = [threading.Thread(target=worker, args=(e,)) for e in self.engines]
             for t in ths:
                 t.start()
             for t in ths:
                 t.join()
-        for st in streams:
-            st.synchronize()
-        for batch, res, rl, _, _ in done:
-            self.query_samples_complete(batch, res, rl)
+        if errors:
+            raise errors[0]
 
-    def query_samples_complete(self, batch, res, res_len):
+    def _run_batch(self, eng, ids, idx):
+        import torch
+        st = self._streams[id(eng)]
+        n = len(ids)
+        n_pad = pad_batch(n)
+        with torch.cuda.device(eng.device), torch.cuda.stream(st):
+            inp = self.qsl_for(eng.device).batch_inputs(idx, n_pad, torch.device("cuda", eng.device))
+            res = torch.empty((n, eng.max_res), dtype=torch.int32, device=st.device)
+            rl = torch.empty(n, dtype=torch.int32, device=st.device)
+            with self._enc_locks[eng.device]:  # encoders on one GPU take turns
+                if "store" in inp:
+                    eng.encode_gather(inp["store"], inp["offsets"], inp["lens"], inp["lens_host"], inp["T"], n, n_pad,
+                                      stream=st)
+                else:
+                    eng.encode(inp["x"], inp["lens"], inp["lens_host"], n=n, stream=st)
+                st.synchronize()
+            eng.decode(res, rl, stream=st)
+            rlh = rl.cpu().numpy()
+            toks = res[:, : max(1, int(rlh.max()))].cpu().numpy()
+        self.query_samples_complete(ids, idx, toks, rlh)
+
+    def query_samples_complete(self, ids, idx, toks, lens):
         """Response = int32 tokens [res_len] per sample (torch_sut.cpp:221-236)."""
-        rl = res_len.cpu().numpy()
-        width = int(rl.max()) if len(rl) else 0
-        toks = res[:, :max(width, 1)].cpu().numpy()
-        for i, s in enumerate(batch):
-            row = toks[i, : rl[i]].copy()
-            self.responses[s.id] = row
+        flat = toks[np.arange(toks.shape[1])[None, :] < lens[:, None]]
+        with self._done_lock:
+            self.completed.append((ids, lens.astype(np.int32), flat.astype(np.int32)))
             if self.on_complete:
-                self.on_complete(s, row)
+                off = 0
+                for i in range(len(ids)):
+                    self.on_complete(QuerySample(id=int(ids[i]), index=int(idx[i])), flat[off: off + lens[i]])
+                    off += int(lens[i])
+
+    def take_completed(self):
+        """-> (ids int64 [n], lengths int32 [n], tokens int32 [sum]) of every completed sample
+        since the last call (the payloads QuerySamplesComplete hands LoadGen)."""
+        with self._done_lock:
+            done, self.completed = self.completed, []
+        if not done:
+            return np.zeros(0, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32)
+        return tuple(np.concatenate([d[k] for d in done]) for k in range(3))
+
+    @property
+    def responses(self):
+        """{sample id: token row} of the completed samples."""
+        out = {}
+        with self._done_lock:
+            for ids, lens, flat in self.completed:
+                off = 0
+                for i, L in zip(ids, lens):
+                    out[int(i)] = flat[off: off + L].copy()
+                    off += int(L)
+        return out
 
     def flush_queries(self):
         pass
 
 
-class GpuQSL:
-    """QSL with every sample's features resident in HBM, ragged ([sum T_i, 240] fp32), and the
-    AssembleSamples gather done on the device (LoadSamplesToRam + AssembleSamples,
-    rnnt_qsl.cpp:150-188).  Synthetic N(0,1) features, seeded."""
+class GpuQSL(_SortedQSL):
+    """QSL with every sample's features resident in HBM, ragged ([sum T_i, 240] fp32,
+    LoadSamplesToRam); AssembleSamples (rnnt_qsl.cpp:150-188) is the engine's gather-quantize pass
+    over this store (rnnt_engine_encode_gather), or ``assemble`` for an explicit padded copy.
+    Synthetic N(0,1) features, seeded (the same seed gives the same store on every device)."""
 
-    def __init__(self, lengths, seed, device="cuda"):
+    def __init__(self, lengths, seed, device="cuda", store=None):
         import torch
         self.lengths = np.asarray(lengths, np.int32)
         self.count = len(self.lengths)
         self.offsets = np.concatenate([[0], np.cumsum(self.lengths)[:-1]]).astype(np.int64)
-        g = torch.Generator(device=device)
-        g.manual_seed(int(seed))
-        self.feats = torch.randn((int(self.lengths.sum()), R.trans_input_size), device=device, generator=g)
-        self.device = device
+        if store is None:
+            g = torch.Generator(device=device)
+            g.manual_seed(int(seed))
+            store = torch.randn((int(self.lengths.sum()), R.trans_input_size), device=device, generator=g)
+        self.feats = store
+        self.device = torch.device(device)
 
-    def __len__(self):
-        return self.count
+    def batch_inputs(self, indices, n_pad, device=None):
+        import torch
+        idx = np.asarray(indices, np.int64)
+        n = len(idx)
+        bl = self.lengths[idx].astype(np.int32)
+        lp = np.zeros(n_pad, np.int32)
+        lp[:n] = bl
+        return dict(store=self.feats, offsets=torch.from_numpy(self.offsets[idx]).to(self.device),
+                    lens=torch.from_numpy(lp).to(self.device), lens_host=bl, T=max(int(bl.max()), 1))
 
     def assemble(self, indices, n_pad=None):
         """-> (x cuda [T_max, n_pad, 256] fp32, lens cuda int32 [n_pad], lens_host [n])."""
@@ -185,7 +269,7 @@ class GpuQSL:
         return x, torch.from_numpy(lp).to(self.device), bl
 
 
-class GpuWavQSL:
+class GpuWavQSL(_SortedQSL):
     """WAV=true QSL (launch_sut.sh:53-55; AssembleSamples(processor=true) + AudioProcessor,
     rnnt_qsl.cpp:150-188, torch_sut.cpp:192-200): every sample's 16 kHz audio resident in HBM,
     ragged, and ``assemble`` runs the GPU featurizer straight from that storage (per-row
@@ -194,7 +278,6 @@ class GpuWavQSL:
     ``lengths`` are the feature lengths (what the SUT sorts by), ``wav_lengths`` the samples."""
 
     def __init__(self, wavs, device="cuda", featurizer_kwargs=None):
-        import threading
         import torch
         from .featurizer import feature_frames
         self.wav_lengths = np.array([len(w) for w in wavs], np.int32)
@@ -207,9 +290,6 @@ class GpuWavQSL:
         self._kw = dict(sample_rate=16000, window="hann", n_fft=512, nfilt=80, frame_splicing=3, pad_out_feat=True)
         self._kw.update(featurizer_kwargs or {})
         self._tls = threading.local()
-
-    def __len__(self):
-        return self.count
 
     def _featurizer(self):
         fz = getattr(self._tls, "fz", None)
@@ -232,6 +312,10 @@ class GpuWavQSL:
         x, lens = self._featurizer().featurize(self.store, torch.from_numpy(wl).to(self.device), wl, n=n, n_pad=n_pad,
                                                T_out=max(int(bl.max()), 1), offsets=off)
         return x, lens, bl
+
+    def batch_inputs(self, indices, n_pad, device=None):
+        x, lens, bl = self.assemble(indices, n_pad)
+        return dict(x=x, lens=lens, lens_host=bl, T=x.shape[0])
 
 
 class ServerSUT:

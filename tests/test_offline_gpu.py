@@ -1,0 +1,69 @@
+"""BASELINE config 4 on the GPU: an MLPerf Offline query over a 2513-sample
+LibriSpeech-dev-clean-shaped QSL through the OfflineSUT bench.py runs -- batches of 4096, three
+engines in flight on one GPU pulling from one shared batch list, AssembleSamples fused into the
+encoder's gather-quantize pass, responses completed through one point.
+
+Checks: every sample of the query answered once; every QSL sample answered identically wherever
+LoadGen's repetition put it (different batches, engines, row positions); 64+ responses spanning
+the longest and shortest batches equal to the CPU restatement."""
+import numpy as np
+import pytest
+import torch
+
+from rnnt_amd import dist, synthetic, weights
+from rnnt_amd.engine import Engine
+from rnnt_amd.sut import GpuQSL, OfflineSUT, make_batches
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pm():
+    return weights.build_model()[0]
+
+
+def test_config4_offline_query(pm, oracle):
+    count, query, batch = 2513, 3 * 4096, 4096
+    qsl = GpuQSL(synthetic.devclean_lengths(count, seed=4), seed=4, device="cuda")
+    engines = [Engine(pm, device=0, max_batch=batch, max_frames=500) for _ in range(3)]
+    try:
+        sut = OfflineSUT(engines, qsl, batch_size=batch)
+        ids, idx = dist.query_arrays(count, query)
+        batches = make_batches(qsl, ids, idx, batch)
+        assert len(batches) == 3
+        sut.issue_batches(batches)
+        torch.cuda.synchronize()
+        assert sorted(set(sut.batch_engine)) == [0, 1, 2]
+        got_ids, lens, toks = sut.take_completed()
+    finally:
+        for e in engines:
+            e.close()
+    assert sorted(got_ids.tolist()) == list(range(query))
+    resp = {}
+    off = 0
+    for sid, L in zip(got_ids, lens):
+        resp[int(sid)] = toks[off: off + int(L)]
+        off += int(L)
+    # the same QSL sample gives the same tokens in every batch / engine / row it landed in
+    first = {}
+    for sid in range(query):
+        q = sid % count
+        if q in first:
+            np.testing.assert_array_equal(resp[sid], resp[first[q]], err_msg=f"QSL sample {q}")
+        else:
+            first[q] = sid
+    # the restatement on rows of the longest and the shortest batch and a middle one
+    pick = np.concatenate([b[1][np.linspace(0, len(b[1]) - 1, 24).round().astype(int)] for b in batches])
+    pick_ids = np.concatenate([b[0][np.linspace(0, len(b[0]) - 1, 24).round().astype(int)] for b in batches])
+    sl = qsl.lengths[pick].astype(np.int32)
+    order = np.argsort(-sl, kind="stable")
+    pick, pick_ids, sl = pick[order], pick_ids[order], sl[order]
+    x = np.zeros((int(sl.max()), len(sl), 256), np.float32)
+    for i, q in enumerate(pick):
+        o = int(qsl.offsets[q])
+        x[: sl[i], i, :240] = qsl.feats[o: o + int(sl[i])].cpu().numpy()
+    f = oracle.encoder_i8(pm, x, sl)
+    ro, rlo, _ = oracle.greedy_decode(pm, f, (sl + 1) // 2, max_res=250 * 30)
+    assert len(sl) >= 64 and rlo.sum() > 100
+    for i, sid in enumerate(pick_ids):
+        np.testing.assert_array_equal(resp[int(sid)], ro[i, : rlo[i]], err_msg=f"sample {sid}")

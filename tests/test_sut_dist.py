@@ -1,4 +1,6 @@
-"""Host-side logic of the SUT/QSL mirror and the multi-rank sharding (CPU, gloo)."""
+"""Host-side logic of the SUT/QSL mirror and of the multi-GPU path bench.py runs (CPU, gloo):
+rnnt_amd.dist.shard_query deals one sorted query over the ranks, each rank completes its share,
+rnnt_amd.dist.gather_responses brings every response to rank 0's host."""
 import os
 import socket
 
@@ -7,7 +9,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from rnnt_amd.sut import QuerySample, RNNTQSL, deal_batches
+from rnnt_amd import dist as rdist
+from rnnt_amd.sut import QuerySample, RNNTQSL, make_batches
 
 
 def _qsl(lengths):
@@ -34,15 +37,27 @@ def test_assemble_layout():
     assert np.all(x[3:, 1] == 0) and np.all(x[:, :, 240:] == 0) and np.all(x[:, 3:] == 0)
 
 
-def test_deal_batches_covers_query_once():
-    samples = list(range(2513))
-    world = 4
+def test_make_batches_sorts_like_the_bucket_sort():
+    lengths = np.random.default_rng(3).integers(47, 501, 777).astype(np.int32)
+    qsl = RNNTQSL([None] * len(lengths), lengths)
+    ids, idx = rdist.query_arrays(len(lengths), 2000)
+    batches = make_batches(qsl, ids, idx, 256)
+    flat = np.concatenate([b[1] for b in batches])
+    ref = [s.index for s in qsl.sort([QuerySample(id=int(i), index=int(j)) for i, j in zip(ids, idx)])]
+    assert list(flat) == ref
+    assert all(len(b[0]) <= 256 for b in batches) and sorted(np.concatenate([b[0] for b in batches])) == list(ids)
+
+
+def test_shard_query_covers_query_once():
+    lengths = synthetic_lengths = np.random.default_rng(1).integers(47, 501, 2513).astype(np.int32)
+    qsl = RNNTQSL([None] * len(lengths), synthetic_lengths)
+    ids, idx = rdist.query_arrays(len(lengths), 24576)
     got = []
-    for r in range(world):
-        for b in deal_batches(samples, 256, r, world):
-            assert len(b) <= 256
-            got.extend(b)
-    assert sorted(got) == samples
+    for r in range(4):
+        for b in rdist.shard_query(qsl, ids, idx, 2048, r, 4):
+            assert len(b[0]) <= 2048
+            got.extend(b[0])
+    assert sorted(got) == list(ids)
 
 
 def _free_port():
@@ -53,26 +68,39 @@ def _free_port():
     return p
 
 
+def _tokens(sid):
+    """a deterministic stand-in response per sample id (variable length, incl. empty)"""
+    return (np.arange(sid % 7, dtype=np.int32) + sid) % 29
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     import torch.distributed as dist
-    from rnnt_amd import dist as rdist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    r, _, w, group = rdist.setup("gloo")
+    assert (r, w) == (rank, world)
     lengths = np.random.default_rng(0).integers(47, 501, 1000).astype(np.int32)
     qsl = RNNTQSL([None] * len(lengths), lengths)
-    samples = [QuerySample(id=i, index=i) for i in range(len(lengths))]
-    mine = [s.index for b in deal_batches(qsl.sort(samples), 128, rank, world) for s in b]
-    total = rdist.reduce_sum(len(mine))
-    frames = rdist.reduce_sum(int(lengths[mine].sum()))
-    slowest = rdist.reduce_max(float(rank + 1))
-    rdist.barrier()
-    q.put((rank, sorted(mine), total, frames, slowest))
+    ids, idx = rdist.query_arrays(len(lengths), 3000)
+    mine = rdist.shard_query(qsl, ids, idx, 128, rank, world)
+    # this rank "completes" its samples (bench.py: OfflineSUT.take_completed)
+    my_ids = np.concatenate([b[0] for b in mine])
+    rows = [_tokens(int(i)) for i in my_ids]
+    lens = np.array([len(t) for t in rows], np.int32)
+    toks = np.concatenate(rows).astype(np.int32)
+    got = rdist.gather_responses(my_ids, lens, toks, world, group)
+    frames = rdist.reduce_sum(int(lengths[np.concatenate([b[1] for b in mine])].sum()), group)
+    slowest = rdist.reduce_max(float(rank + 1), group)
+    rdist.barrier(group)
+    out = None
+    if got is not None:
+        out = (got[0].tolist(), got[1].tolist(), got[2].tolist())
+    q.put((rank, sorted(my_ids.tolist()), frames, slowest, out))
     dist.destroy_process_group()
 
 
-def test_two_rank_sharding_gloo():
-    """world_size-2 run of the multi-GPU path's control plane: disjoint shards that cover the
-    query, sum/max reductions as bench.py uses them."""
+def test_two_rank_query_shard_and_gather_gloo():
+    """world_size-2 run of bench.py's multi-GPU path (rnnt_amd.dist): disjoint shards covering
+    the query, every response gathered to rank 0 intact, sum/max reductions."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -83,13 +111,19 @@ def test_two_rank_sharding_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    outs.sort()
+    outs.sort(key=lambda o: o[0])
     a, b = outs[0][1], outs[1][1]
-    assert not set(a) & set(b) and sorted(a + b) == list(range(1000))
-    assert outs[0][2] == outs[1][2] == 1000
+    assert not set(a) & set(b) and sorted(a + b) == list(range(3000))
     lengths = np.random.default_rng(0).integers(47, 501, 1000)
-    assert outs[0][3] == int(lengths.sum())
-    assert outs[0][4] == outs[1][4] == 2.0
-    # round-robin dealing of sorted chunks balances the shards' work
-    fa, fb = lengths[a].sum(), lengths[b].sum()
+    assert outs[0][2] == outs[1][2] == float(lengths[np.arange(3000) % 1000].sum())
+    assert outs[0][3] == outs[1][3] == 2.0
+    assert outs[1][4] is None
+    gids, glens, gtoks = outs[0][4]
+    assert sorted(gids) == list(range(3000))
+    off = 0
+    for sid, L in zip(gids, glens):
+        np.testing.assert_array_equal(gtoks[off: off + L], _tokens(sid))
+        off += L
+    # snake dealing of sorted batches balances the shards' work
+    fa, fb = lengths[np.array(a) % 1000].sum(), lengths[np.array(b) % 1000].sum()
     assert abs(fa - fb) / (fa + fb) < 0.1

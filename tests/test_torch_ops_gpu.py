@@ -120,10 +120,10 @@ def test_weights_are_the_ones_passed(pm, W):
     hx = [torch.zeros((N, 320), dtype=torch.bfloat16, device="cuda") for _ in range(2)]
     cx = [torch.zeros((N, 320), dtype=torch.float32, device="cuda") for _ in range(2)]
     a = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0].clone()
-    b_ih = W["pred"][0][2]
-    b_ih.add_(0.5)  # in place: bumps the tensor's version counter
+    b_fused = W["pred"][0][3]  # b_hh + b_ih of layer 0 (changing only b_ih would move b_ih and b_hh oppositely)
+    b_fused.add_(0.5)  # in place: bumps the tensor's version counter
     b = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0].clone()
-    b_ih.sub_(0.5)
+    b_fused.sub_(0.5)
     c = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0]
     assert not torch.equal(a, b)
     assert torch.equal(a, c)
