@@ -25,7 +25,7 @@ extern "C" {
 float oracle_exp(float x);
 float oracle_sigmoid(float x);
 float oracle_tanh(float x);
-float oracle_act_sig_t(float t);  /* table sigma at t = 4x + 64 (int8 cell, see rnnt_oracle.c) */
+float oracle_act_sig_t(float t);  /* table sigma at t = 64x + 1024 (int8 cell, see rnnt_oracle.c) */
 float oracle_enc_bias(float bq, float rb, int gate);
 void oracle_enc_cell(const int32_t acc[4], const float B[4], float rb, float c_prev,
                      float* c_out, float* h_out);

@@ -5,14 +5,9 @@
 
 namespace rnnt {
 
-// Encoder workgroup tile: 256 gate rows x 128*ENC_WN batch rows (ENC_WN batch-column waves of
-// 128 rows, 4 gate-row waves each).  ENC_WN = 2: one 8-wave workgroup per CU; ENC_WN = 1: two
-// 4-wave workgroups per CU, so one's VALU epilogue overlaps the other's MFMA main loop.
-#ifndef ENC_WN
-#define ENC_WN 2
-#endif
-constexpr int ENC_BATCH_TILE = 128 * ENC_WN;  // batch rows per encoder workgroup
-constexpr int ENC_PAD = 256;                  // batch buffers are padded to a multiple of this
+// Encoder workgroup tile: 256 gate rows x 256 batch rows (8 waves, one workgroup per CU).
+constexpr int ENC_BATCH_TILE = 256;  // batch rows per encoder workgroup
+constexpr int ENC_PAD = 256;         // batch buffers are padded to a multiple of this
 
 // Packed row of (unit u, gate g) in the encoder weight image.  Each wave's 64 gate rows hold
 // 16 units: MFMA tile i = u&3, lane group q = (u>>2)&3 and accumulator register g, i.e.

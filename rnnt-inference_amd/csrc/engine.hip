@@ -176,9 +176,9 @@ extern "C" int rnnt_engine_load_encoder_layers(rnnt_engine* e, int first, int co
       for (int u = 0; u < H; ++u) {
         const int pr = enc_packed_row(u, g);
         memcpy(&wp[(size_t)pr * K], w[i] + (size_t)(g * H + u) * K, K);
-        // the cell's folded bias term, as oracle_enc_bias: (bq rb) * (g == 2 ? 8 : 4) + 64
+        // the cell's folded bias term, as oracle_enc_bias: (bq rb) * (g == 2 ? 128 : 64) + 1024
         const float bqr = bq[i][g * H + u] * rb[i];
-        b[pr] = g == 2 ? bqr * 8.0f + 64.0f : bqr * 4.0f + 64.0f;
+        b[pr] = g == 2 ? bqr * 128.0f + 1024.0f : bqr * 64.0f + 1024.0f;
       }
     int r = load_buf(e, &e->enc_w[l], wp);
     if (!r) r = load_buf(e, &e->enc_bq[l], b);

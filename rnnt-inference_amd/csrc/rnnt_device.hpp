@@ -90,39 +90,43 @@ __device__ __forceinline__ float det_tanh(float x) {
 }
 
 // ---- int8 encoder cell (bit-identical to oracle_act_sig_t / oracle_enc_cell, where the
-// contract is documented): sigma from a 128-interval piecewise-cubic table held in LDS
-// (float4 per interval), indexed by t = 4x + 64; tanh(x) = 2 sigma(2x) - 1; the
-// dequantisation folded into the index, t = fma((float)acc, A, B).  STRIDE: entry k sits at
-// tab[k * STRIDE] (the encoder keeps 16 interleaved copies, one per 16-byte LDS bank slot).
-template <int STRIDE = 1>
-__device__ __forceinline__ float act_sig_t(const float4* __restrict__ tab, float t) {
-  t = __builtin_fminf(__builtin_fmaxf(t, 0.0f), 127.99998f);
-  const int k = (int)t;
-  const float fr = __builtin_amdgcn_fractf(t);  // v_fract_f32: t - floor(t), exact for t >= 0
-#ifdef RNNT_DEV_NO_TAB  // development ablation: no LDS lookup
-  const float4 c = float4{t * 0.001f, (float)k, 0.5f, 0.25f};
-#else
-  const float4 c = tab[k * STRIDE];
-#endif
-  return __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c.w, fr, c.z), fr, c.y), fr, c.x);
+// contract is documented): sigma from a 2048-interval piecewise-linear table held in LDS, indexed
+// by t = 64x + 1024 and stored as (d0, c1) pairs so that sigma = fma(c1, t, d0) -- no fractional
+// part; tanh(x) = 2 sigma(2x) - 1; the dequantisation folded into the index,
+// t = fma((float)acc, A, B).
+constexpr int ENC_TAB_N = 2048;
+__device__ __forceinline__ float act_sig_t(const float2* __restrict__ tab, float t) {
+  t = __builtin_amdgcn_fmed3f(t, 0.0f, 2047.9998f);  // = min(max(t, 0), 2047.9998) for finite t
+  const float2 e = tab[(int)t];
+  return __builtin_fmaf(e.y, t, e.x);
 }
 // acc: int32 gate sums (i, f, g, o); B: packed per-gate bias terms (oracle_enc_bias);
-// As = 4 rb, Ag = 8 rb.  Returns c (fp32) and h.
-template <int STRIDE = 1>
-__device__ __forceinline__ void enc_cell(const float4* __restrict__ tab, const v4i acc, const float4 B, float As,
+// As = 64 rb, Ag = 128 rb.  Returns c (fp32) and h.
+__device__ __forceinline__ void enc_cell(const float2* __restrict__ tab, const v4i acc, const float4 B, float As,
                                          float Ag, float c_prev, float& c_out, float& h_out) {
-  const float ig = act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[0], As, B.x));
-  const float fg = act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[1], As, B.y));
-  const float gg = __builtin_fmaf(2.0f, act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[2], Ag, B.z)), -1.0f);
-  const float og = act_sig_t<STRIDE>(tab, __builtin_fmaf((float)acc[3], As, B.w));
+  const float ig = act_sig_t(tab, __builtin_fmaf((float)acc[0], As, B.x));
+  const float fg = act_sig_t(tab, __builtin_fmaf((float)acc[1], As, B.y));
+  const float gg = __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf((float)acc[2], Ag, B.z)), -1.0f);
+  const float og = act_sig_t(tab, __builtin_fmaf((float)acc[3], As, B.w));
   float c = __builtin_fmaf(fg, c_prev, ig * gg);
   // opaque here: otherwise the backend folds fma + the later f32->f16 store conversion into
   // v_fma_mixlo_f16 (one rounding straight to f16), which is not the contract's fp32 c
   // rounded to fp16
   asm volatile("" : "+v"(c));
-  const float tc = __builtin_fmaf(2.0f, act_sig_t<STRIDE>(tab, __builtin_fmaf(c, 8.0f, 64.0f)), -1.0f);
+  const float tc = __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf(c, 128.0f, 1024.0f)), -1.0f);
   c_out = c;
   h_out = og * tc;
+}
+// q8(v) (= clamp(rint(v), -128, 127), RNE) in the int8 byte of the result: v + 1.5 * 2^23
+// rounds to the integer grid exactly as rint does (|v| < 2^22; larger values clamp anyway), the
+// clamp runs on the biased float, and the low byte of its bits is the two's-complement value.
+__device__ __forceinline__ uint32_t q8_biased(float v) {
+  const float m = __builtin_amdgcn_fmed3f(v + 12582912.0f, 12582784.0f, 12583039.0f);
+  return __float_as_uint(m);
+}
+// the low bytes of four q8_biased results packed into one word (byte i from b_i)
+__device__ __forceinline__ uint32_t pack_q8(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3) {
+  return __builtin_amdgcn_perm(b1, b0, 0x0c0c0400u) | __builtin_amdgcn_perm(b3, b2, 0x04000c0cu);
 }
 
 // f32 -> f16 round-half-even and f16 -> f32 on the hardware converters (v_cvt_f16_f32 /
