@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--wav", action="store_true",
                     help="WAV=true path (launch_sut.sh:53-55): the QSL holds 16 kHz audio and every batch runs the "
                          "GPU featurizer (FilterbankFeatures.forward) inside the timed region")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "tools", "roofline_traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (profiles/), if present")
     return ap.parse_args()
 

@@ -3,7 +3,8 @@
     python tools/summarize_profile.py gpurun_out/prof_round profiles/r01
 writes <prefix>_kernel_stats.csv (rocprofv3 --stats, copied), <prefix>_pmc_summary.json
 (per-kernel mean counters per dispatch, derived HBM bytes/launch with the gfx950 FETCH_SIZE x2
-correction) and profiles/traffic_latest.json (read by bench.py's roofline.traffic).
+correction) and tools/roofline_traffic.json (read by bench.py's roofline.traffic; tools/ travels to the GPU
+box, profiles/ does not).
 """
 import collections
 import csv
@@ -41,7 +42,7 @@ def main():
     tick = summary.get("rnnt::lstm_i8_tick_kernel", {})
     if "hbm_bytes_per_launch" in tick:
         json.dump({"lstm_i8_step_bytes_per_launch": tick["hbm_bytes_per_launch"], "source": prefix + "_pmc_summary.json"},
-                  open(os.path.join(os.path.dirname(prefix), "traffic_latest.json"), "w"), indent=1)
+                  open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "roofline_traffic.json"), "w"), indent=1)
     for k, d in summary.items():
         print(k, {c: round(v, 3) for c, v in d.items() if c in ("dispatches", "hbm_bytes_per_launch", "mfma_busy_frac", "SQ_INSTS_VALU", "SQ_INSTS_MFMA")})
 
