@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RNNT_ABI_VERSION 6
+#define RNNT_ABI_VERSION 7
 
 #define RNNT_OK 0
 #define RNNT_EINVAL (-22)
@@ -124,6 +124,25 @@ int rnnt_engine_encode_gather(rnnt_engine* e, const float* store, const int64_t*
 /* Greedy decode of the last encoded batch: res device int32 [n][max_res] (filled with -1 first),
  * res_len device int32 [n]. */
 int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream);
+
+/* ---- Server continuous batching (PipelineState, csrc/metadata.cpp:97-194; TorchModel::encode's
+ * split_len loop, rnnt_model.hpp:62-90): the engine's rows are slots that carry their LSTM and
+ * greedy state from one call to the next, so an utterance can be fed in chunks while finished
+ * slots are refilled with new samples.
+ * rnnt_engine_encode_stream: one chunk, gathered like rnnt_engine_encode_gather (offsets[i] = the
+ * first stored frame of slot i's chunk, lens = the chunk's frames per slot, 0 for an idle slot).
+ * reset device int32 [n_pad]: 1 = a new utterance starts in this slot (its h/c start at zero, the
+ * masked_fill_ of PipelineState::update), 0 = continue from the slot's state after the previous
+ * chunk.  Every chunk of an utterance but its last must have an even length (StackTime pairs
+ * frames within the chunk).  n_pad is fixed for an engine's stream (the slot count).
+ * rnnt_engine_decode_stream: greedy decode of that chunk's frames (f_lens = ceil(lens/2)) carrying
+ * pre_g / pre_hg / pre_cg and the result row: a slot flagged in reset starts from SOS with
+ * res[i] = -1 and res_len[i] = 0; the others append to res[i] (same buffer every call, max_res
+ * the full utterance's bound).  res_len[i] = the slot's total symbols so far. */
+int rnnt_engine_encode_stream(rnnt_engine* e, const float* store, const int64_t* offsets, const int32_t* lens,
+                              const int32_t* lens_host, const int32_t* reset, int T, int n, int n_pad, void* stream);
+int rnnt_engine_decode_stream(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, const int32_t* reset,
+                              void* stream);
 
 /* encode + decode. */
 int rnnt_engine_infer(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host, int T,

@@ -285,6 +285,41 @@ __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
   }
 }
 
+// Server continuous batching (PipelineState, metadata.cpp:97-194): rows are slots that keep their
+// greedy state across calls.  A slot flagged in reset starts an utterance (the State::init /
+// masked_fill_ values above, its result row refilled with -1); the others keep pre_g, the
+// committed prediction state (slot) and res / idx, and only the per-call frame counters restart
+// (TorchModel::decode zeroes symbols_added and time_idx every call, rnnt_model.hpp:95-98).  Every
+// live slot re-runs the prediction of its committed state on pre_g -- the candidate the previous
+// call already held, recomputed bit-identically (a pure function of that state).
+__global__ void __launch_bounds__(256) dec_init_stream_kernel(DecArgs a, const int32_t* __restrict__ reset) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= a.Npad) return;
+  const int fl = row < a.N ? a.f_lens[row] : 0;
+  DecState& s = a.s;
+  if (row >= a.N || reset[row]) {
+    s.idx[row] = -1; s.preg[row] = SOS; s.slot[row] = 0;
+    float* h = hc_part(a.hc, row, 0, 0);
+    for (int k = 0; k < 4 * P; ++k) h[k] = 0.0f;
+  }
+  s.time[row] = 0; s.added[row] = 0;
+  s.fin[row] = fl <= 0;
+  if (fl > 0) {
+    const int pg = s.preg[row];
+    s.list[atomicAdd(&s.count[0], 1)] = emit_entry(row, s.slot[row], pg < 0 ? 28 : pg);
+    s.live[atomicAdd(&s.count[2], 1)] = row;
+    atomicAdd(s.unfinished, 1);
+  }
+}
+
+// result rows of the slots flagged in reset refilled with -1 (one workgroup per row, coalesced)
+__global__ void __launch_bounds__(256) dec_reset_res_kernel(int32_t* __restrict__ res, int max_res,
+                                                            const int32_t* __restrict__ reset) {
+  const int row = blockIdx.x;
+  if (!reset[row]) return;
+  for (int k = threadIdx.x; k < max_res; k += 256) res[(size_t)row * max_res + k] = -1;
+}
+
 // One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates =
 // (b_ih + x.W_ih^T) + (b_hh + h.W_hh^T); c fp32, h bf16.  A workgroup (4 waves) owns 4 gate
 // tiles, one per wave, whose W_hh (and, layer 1, W_ih) rows stay in registers for the launch
@@ -641,12 +676,17 @@ __global__ void dec_finish_kernel(DecArgs a) {
   if (row < a.N) a.res_len[row] = a.s.idx[row] + 1;
 }
 
-int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st) {
+int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st, const int32_t* reset) {
   const int rt = a.Npad / DEC_RT;
   if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (hipMemsetAsync(a.s.unfinished, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
-  if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
-  hipLaunchKernelGGL(dec_init_kernel, dim3((a.Npad + 255) / 256), dim3(256), 0, st, a);
+  if (reset) {
+    hipLaunchKernelGGL(dec_reset_res_kernel, dim3(a.N), dim3(256), 0, st, a.res, a.max_res, reset);
+    hipLaunchKernelGGL(dec_init_stream_kernel, dim3((a.Npad + 255) / 256), dim3(256), 0, st, a, reset);
+  } else {
+    if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
+    hipLaunchKernelGGL(dec_init_kernel, dim3((a.Npad + 255) / 256), dim3(256), 0, st, a);
+  }
   constexpr int CHUNK = 32;
   int step = 0, chunk = 0;
   int live_bound = a.N;  // unfinished rows at the end of the last chunk read back (an upper bound)

@@ -49,6 +49,9 @@ int launch_dec_xtab(const DecWeights& w, float* xtab, hipStream_t st);
 // Host-driven lock-step loop; polls the live-row counter (host_flags: 2 pinned words, evs: 2
 // events) one 32-step chunk behind.
 // Returns the number of steps enqueued (>= 0) or -1.
-int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st);
+// reset != nullptr: Server continuous batching -- slots keep their greedy state across calls and
+// reset[row] != 0 starts a new utterance in that slot (dec_init_stream_kernel).
+int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st,
+                         const int32_t* reset = nullptr);
 
 }  // namespace rnnt

@@ -65,6 +65,9 @@ struct rnnt_engine {
   hipEvent_t poll_ev[2] = {nullptr, nullptr};
   // last encoded batch
   int last_T = 0, last_n = 0, last_npad = 0;
+  // h ping-pong: layer l's state before its step t sits in h[l][(t + hpar[l]) & 1]; a stream
+  // (carried-state) encode advances hpar by the steps it ran
+  int hpar[5] = {};
   // Stream ordering of the engine's own state (h/c, x0q, the encoder output, decode state):
   // every call that touches it waits for the previous such call's completion event, on
   // whatever stream that one ran, and records its own -- so encode -> decode -> next encode
@@ -497,8 +500,8 @@ static EncStepArgs make_job(rnnt_engine* e, int l, int t, int n_pad, const int8_
   a.W = e->enc_w[l];
   a.bq = e->enc_bq[l];
   a.x = x + (size_t)t * n_pad * I;
-  a.h_in = e->h[l][t & 1];
-  a.h_out = e->h[l][(t + 1) & 1];
+  a.h_in = e->h[l][(t + e->hpar[l]) & 1];
+  a.h_out = e->h[l][(t + 1 + e->hpar[l]) & 1];
   a.c = e->c[l];
   a.I = I;
   a.mode = mode;
@@ -570,6 +573,21 @@ static std::vector<int> tile_maxima(const int32_t* lens_host, int n, int n_pad) 
   return tm;
 }
 
+// Encoder state of the slots flagged in reset zeroed (PipelineState::update's masked_fill_ of
+// pre/post hx and cx, metadata.cpp:120-131): workgroup (row, layer), 64 lanes x 16 B of h and c.
+struct EncStateRows {
+  int8_t* h[5];
+  uint16_t* c[5];
+};
+__global__ void __launch_bounds__(64) enc_reset_rows_kernel(EncStateRows st, const int32_t* __restrict__ reset) {
+  const int row = blockIdx.x, l = blockIdx.y;
+  if (!reset[row]) return;
+  const uint4 z = uint4{0u, 0u, 0u, 0u};
+  *(uint4*)(st.h[l] + (size_t)row * H + threadIdx.x * 16) = z;
+  *(uint4*)(st.c[l] + (size_t)row * H + threadIdx.x * 8) = z;
+  *(uint4*)(st.c[l] + (size_t)row * H + 512 + threadIdx.x * 8) = z;
+}
+
 // The input of encode: an assembled [T][n_pad][256] fp32 batch, or the QSL's ragged sample store
 // gathered in the quantize pass (store != nullptr).
 struct EncInput {
@@ -578,8 +596,10 @@ struct EncInput {
   const int64_t* offsets = nullptr;
 };
 
+// reset == nullptr: a batch of whole utterances (every row's state starts at zero); otherwise a
+// stream chunk (rnnt_engine_encode_stream): rows keep their state unless flagged.
 static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, const int32_t* lens_host, int T, int n,
-                       int n_pad, float* f_out, void* stream) {
+                       int n_pad, float* f_out, void* stream, const int32_t* reset = nullptr) {
   if (!e || !lens || !(in.feats || (in.store && in.offsets))) return fail(RNNT_EINVAL, "null argument");
   if (e->enc_loaded != 0x1f) return fail(RNNT_EINVAL, "encoder weights not loaded");
   int r = check_batch(e, T, n, n_pad);
@@ -589,9 +609,20 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
   if ((r = state_acquire(e, st))) return r;
   const int Tp = (T + 1) / 2;
   const std::vector<int> tm = tile_maxima(lens_host, n, n_pad);
-  for (int l = 0; l < 5; ++l) {
-    HIPCHK(hipMemsetAsync(e->h[l][0], 0, (size_t)n_pad * H, st));
-    HIPCHK(hipMemsetAsync(e->c[l], 0, (size_t)n_pad * H * 2, st));
+  if (!reset) {
+    for (int l = 0; l < 5; ++l) {
+      e->hpar[l] = 0;
+      HIPCHK(hipMemsetAsync(e->h[l][0], 0, (size_t)n_pad * H, st));
+      HIPCHK(hipMemsetAsync(e->c[l], 0, (size_t)n_pad * H * 2, st));
+    }
+  } else {
+    EncStateRows sr;
+    for (int l = 0; l < 5; ++l) {
+      sr.h[l] = e->h[l][e->hpar[l] & 1];
+      sr.c[l] = e->c[l];
+    }
+    hipLaunchKernelGGL(enc_reset_rows_kernel, dim3(n_pad, 5), dim3(64), 0, st, sr, reset);
+    HIPCHK(hipGetLastError());
   }
   hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
   if (in.store ? launch_quantize_gather(in.store, in.offsets, lens, T, n, n_pad, e->in_s[0], e->x0q, st)
@@ -623,6 +654,9 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
   }
   hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->flen, n_pad);
   HIPCHK(hipGetLastError());
+  // every layer ran all its steps (layers 0/1: T frames, post_rnn: Tp stacked frames); rows of a
+  // skipped tile are past their length in this call, i.e. finished
+  for (int l = 0; l < 5; ++l) e->hpar[l] = (e->hpar[l] + (l < 2 ? T : Tp)) & 1;
   if (e->prof) e->ev_enc.push_back({ev0, new_event(st)});
   if ((r = state_release(e, st))) return r;
   e->encode_calls++;
@@ -651,7 +685,31 @@ extern "C" int rnnt_engine_encode_gather(rnnt_engine* e, const float* store, con
   return encode_impl(e, in, lens, lens_host, T, n, n_pad, f_out, stream);
 }
 
+extern "C" int rnnt_engine_encode_stream(rnnt_engine* e, const float* store, const int64_t* offsets,
+                                         const int32_t* lens, const int32_t* lens_host, const int32_t* reset, int T,
+                                         int n, int n_pad, void* stream) {
+  if (!lens_host || !reset) return fail(RNNT_EINVAL, "encode_stream needs the host lengths and the reset flags");
+  for (int i = 0; i < n; ++i)
+    if (lens_host[i] < 0 || lens_host[i] > T) return fail(RNNT_EINVAL, "a chunk length exceeds T");
+  EncInput in;
+  in.store = store;
+  in.offsets = offsets;
+  return encode_impl(e, in, lens, lens_host, T, n, n_pad, nullptr, stream, reset);
+}
+
+static int decode_impl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream,
+                       const int32_t* reset);
 extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream) {
+  return decode_impl(e, res, res_len, max_res, stream, nullptr);
+}
+extern "C" int rnnt_engine_decode_stream(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res,
+                                         const int32_t* reset, void* stream) {
+  if (!reset) return fail(RNNT_EINVAL, "decode_stream needs the reset flags");
+  return decode_impl(e, res, res_len, max_res, stream, reset);
+}
+
+static int decode_impl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream,
+                       const int32_t* reset) {
   if (!e || !res || !res_len) return fail(RNNT_EINVAL, "null argument");
   if (e->last_n <= 0) return fail(RNNT_EINVAL, "decode before encode");
   if (!e->xtab_ok || !e->joint1_loaded || !e->joint2_loaded)
@@ -679,7 +737,7 @@ extern "C" int rnnt_engine_decode(rnnt_engine* e, int32_t* res, int32_t* res_len
   a.max_res = max_res;
   a.s = e->ds;
   a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
-  const int steps = launch_greedy_decode(a, e->host_flags, e->poll_ev, st);
+  const int steps = launch_greedy_decode(a, e->host_flags, e->poll_ev, st, reset);
   if (steps < 0) return fail(RNNT_EDEVICE, "greedy launch failed");
   e->decode_steps += steps;
   if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
@@ -755,6 +813,7 @@ extern "C" int rnnt_op_lstm_int8(rnnt_engine* e, int first, int count, const voi
   for (int i = 0; i < count; ++i) {
     const int l = first + i;
     const size_t NH = (size_t)n_pad * H;
+    e->hpar[l] = 0;
     HIPCHK(hipMemcpyAsync(e->h[l][0], hx + i * NH, NH, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(e->c[l], cx + i * NH, NH * 2, hipMemcpyDeviceToDevice, st));
     const bool last = (i == count - 1);

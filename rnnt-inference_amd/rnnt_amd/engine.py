@@ -111,6 +111,25 @@ class Engine:
                                                  n_pad, _ptr(f_out), _stream_handle(stream))
         _lib.check(rc, "rnnt_engine_encode_gather")
 
+    def encode_stream(self, store, offsets, lens, lens_host, reset, T, n, n_pad, stream=None):
+        """One chunk of Server continuous batching (PipelineState, metadata.cpp:97-194): slot i's
+        chunk is lens_host[i] frames from store row offsets[i]; reset cuda int32 [n_pad] flags the
+        slots that start a new utterance (their LSTM state restarts at zero), the others carry
+        their state from the previous chunk."""
+        assert store.is_contiguous() and store.shape[1] == R.trans_input_size and offsets.dtype.itemsize == 8
+        assert reset.dtype.itemsize == 4 and reset.numel() >= n_pad
+        lh = np.ascontiguousarray(lens_host, np.int32)
+        rc = self._lib.rnnt_engine_encode_stream(self._h, _ptr(store), _ptr(offsets), _ptr(lens), lh.ctypes.data,
+                                                 _ptr(reset), T, n, n_pad, _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_encode_stream")
+
+    def decode_stream(self, res, res_len, reset, stream=None):
+        """Greedy decode of the last stream chunk, carrying each slot's prediction state and result
+        row (res cuda int32 [n, max_res], the same buffer every call); reset as for encode_stream."""
+        rc = self._lib.rnnt_engine_decode_stream(self._h, _ptr(res), _ptr(res_len), res.shape[1], _ptr(reset),
+                                                 _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_decode_stream")
+
     def decode(self, res, res_len, stream=None):
         """res: cuda int32 [n, max_res]; res_len: cuda int32 [n]."""
         rc = self._lib.rnnt_engine_decode(self._h, _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))

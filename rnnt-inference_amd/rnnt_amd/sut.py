@@ -319,13 +319,185 @@ class GpuWavQSL(_SortedQSL):
 
 
 class ServerSUT:
-    """Server scenario SUT (reference ServerSUT, csrc/torch_sut.cpp:238-571, with
-    PipelineState continuous batching, metadata.cpp:97-194).  MI355X form: one worker thread
-    per engine (HIP stream each); whenever a worker is free it takes every pending sample (up
-    to max_batch, longest first), assembles the batch on the device, encodes (encoders take
-    turns), decodes and completes each sample with its token row.  A batch's latency on the GPU
-    (tens of ms) is far below the 1 s Server budget, so dynamic batching replaces the
-    reference's slot refilling.  Latency per sample = completion - issue time."""
+    """Server scenario SUT with continuous batching (reference ServerSUT, csrc/torch_sut.cpp:238-571,
+    PipelineState, csrc/metadata.cpp:97-194; TorchModel::encode's split_len loop, rnnt_model.hpp:62-90).
+
+    Each engine is one PipelineState of ``slots`` rows that carry their LSTM and greedy state from
+    one round to the next.  A round (one host thread per engine, its own HIP stream):
+      1. refill (PipelineState::update): free slots take waiting samples, first come first served;
+         their encoder / prediction state and result row restart (the reset flags);
+      2. encode one chunk of ``split_len`` frames of every busy slot from the QSL's HBM-resident
+         feature store (rnnt_engine_encode_stream: per-slot offsets, h/c carried), then decode that
+         chunk's frames (rnnt_engine_decode_stream: pre_g / pre_hg / pre_cg / result row carried);
+      3. respond early (QuerySamplesComplete, torch_sut.cpp:542-571): every slot whose features are
+         used up is answered with its token row and freed, the others continue next round.
+    Encoders of the engines on one GPU take turns, so one engine's decode overlaps the next
+    engine's encode.  Chunked encoding is exact (h/c carry, StackTime pairs within even chunks) and
+    so is the chunked greedy decode (symbols_added / time restart at a chunk boundary exactly as
+    at a frame boundary): every answer equals the Offline answer for that sample.
+    QoS deferral (torch_sut.cpp:396-414): samples longer than ``qos_len`` feature frames wait until
+    ``flush_queries`` (LoadGen's FlushQueries, lStop_) and then run after the regular queue.
+    ``response_size`` of the reference (the minimum number of finished rows per consumer
+    iteration, which amortises its CPU iteration) is subsumed: a round is one chunk and answers
+    every slot that finished in it.  Latency per sample = completion - issue time."""
+
+    def __init__(self, engines, qsl, slots=2048, split_len=32, qos_len=None, on_complete=None):
+        import threading
+        from .engine import pad_batch
+        if split_len <= 0 or split_len % 2:
+            raise ValueError("split_len must be a positive even number of frames (StackTime pairs frames)")
+        self.engines = list(engines) if isinstance(engines, (list, tuple)) else [engines]
+        self.qsl, self.split_len, self.qos_len = qsl, int(split_len), qos_len
+        self.slots = pad_batch(int(slots))
+        for e in self.engines:
+            if e.max_batch < self.slots:
+                raise ValueError(f"engine max_batch {e.max_batch} < {self.slots} slots")
+        self.on_complete = on_complete
+        self.responses, self.latency = {}, {}
+        self._pending, self._qos = [], []  # (issue_time, QuerySample)
+        self._cv = threading.Condition()
+        self._enc_locks = {}
+        self._stop = self._flushed = False
+        self._threads = []
+        self.rounds = 0
+        self.errors = []
+
+    # LoadGen-facing surface -------------------------------------------------------------
+    def start(self):
+        import threading
+        for e in self.engines:
+            self._enc_locks.setdefault(e.device, threading.Lock())
+        for j in range(len(self.engines)):
+            t = threading.Thread(target=self._worker, args=(j,), daemon=True)
+            t.start()
+            self._threads.append(t)
+
+    def issue_query(self, samples, now=None):
+        import time
+        now = time.perf_counter() if now is None else now
+        with self._cv:
+            for s in samples:
+                long_ = self.qos_len is not None and int(self.qsl.lengths[s.index]) > self.qos_len
+                (self._qos if long_ else self._pending).append((now, s))
+            self._cv.notify_all()
+
+    def flush_queries(self):
+        """LoadGen's FlushQueries (torch_sut.hpp:120-122): no more queries; deferred QoS samples run."""
+        with self._cv:
+            self._flushed = True
+            self._cv.notify_all()
+
+    def stop(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        for t in self._threads:
+            t.join()
+
+    # consumer -----------------------------------------------------------------------------
+    def _take(self, k, busy):
+        """Up to k waiting samples for free slots; blocks only while this engine has no busy slot.
+        None: stopped and nothing left for this engine."""
+        with self._cv:
+            while True:
+                if self._pending:
+                    out = self._pending[:k]
+                    del self._pending[:k]
+                    return out
+                if self._flushed and self._qos:  # torch_sut.cpp:408-414: QoS samples once issuing stopped
+                    out = self._qos[:k]
+                    del self._qos[:k]
+                    return out
+                if busy or k == 0:
+                    return []
+                if self._stop:
+                    return None
+                self._cv.wait()
+
+    def _worker(self, j):
+        import time
+        import torch
+        eng = self.engines[j]
+        S, L, qsl = self.slots, self.split_len, self.qsl
+        dev = torch.device("cuda", eng.device)
+        with torch.cuda.device(eng.device):
+            st = torch.cuda.Stream(device=dev)
+            res = torch.empty((S, eng.max_res), dtype=torch.int32, device=dev)
+            rl = torch.zeros(S, dtype=torch.int32, device=dev)
+            # per-round host -> device inputs: reset flags, chunk lengths, row offsets (pinned)
+            h_reset = torch.zeros(S, dtype=torch.int32).pin_memory()
+            h_lens = torch.zeros(S, dtype=torch.int32).pin_memory()
+            h_off = torch.zeros(S, dtype=torch.int64).pin_memory()
+            d_reset = torch.zeros(S, dtype=torch.int32, device=dev)
+            d_lens = torch.zeros(S, dtype=torch.int32, device=dev)
+            d_off = torch.zeros(S, dtype=torch.int64, device=dev)
+        store = qsl.feats
+        sample = [None] * S               # (issue_time, QuerySample) per slot
+        pos = np.zeros(S, np.int64)       # next frame of the slot's sample
+        remain = np.zeros(S, np.int32)    # frames left
+        base = np.zeros(S, np.int64)      # first stored row of the slot's sample
+        try:
+            while True:
+                free = [i for i in range(S) if sample[i] is None]
+                new = self._take(len(free), busy=len(free) < S)
+                if new is None:
+                    return
+                rs = h_reset.numpy()
+                rs[:] = 0
+                for i, item in zip(free, new):
+                    sample[i] = item
+                    idx = item[1].index
+                    pos[i], remain[i], base[i] = 0, int(qsl.lengths[idx]), int(qsl.offsets[idx])
+                    rs[i] = 1
+                busy = np.array([x is not None for x in sample])
+                if not busy.any():
+                    continue
+                cl = np.where(busy, np.minimum(remain, L), 0).astype(np.int32)
+                h_lens.numpy()[:] = cl
+                h_off.numpy()[:] = np.where(busy, base + pos, 0)
+                T = max(int(cl.max()), 1)
+                with torch.cuda.device(eng.device), torch.cuda.stream(st):
+                    d_reset.copy_(h_reset, non_blocking=True)
+                    d_lens.copy_(h_lens, non_blocking=True)
+                    d_off.copy_(h_off, non_blocking=True)
+                    with self._enc_locks[eng.device]:  # encoders on one GPU take turns
+                        eng.encode_stream(store, d_off, d_lens, cl, d_reset, T, S, S, stream=st)
+                        st.synchronize()
+                    eng.decode_stream(res, rl, d_reset, stream=st)
+                    pos += cl
+                    remain -= cl
+                    done = np.nonzero(busy & (remain == 0))[0]
+                    if len(done):
+                        di = torch.from_numpy(done).to(dev)
+                        lens_d = rl.index_select(0, di)
+                        rlh = lens_d.cpu().numpy()
+                        toks = res.index_select(0, di)[:, : max(1, int(rlh.max()))].cpu().numpy()
+                    else:
+                        st.synchronize()
+                self.rounds += 1
+                now = time.perf_counter()
+                for k, i in enumerate(done):
+                    t0, s = sample[i]
+                    row = toks[k, : rlh[k]].copy()
+                    self.responses[s.id] = row
+                    self.latency[s.id] = now - t0
+                    if self.on_complete:
+                        self.on_complete(s, row)
+                    sample[i] = None
+        except Exception as ex:  # surface in the caller, never hang the query
+            self.errors.append(ex)
+            for item in sample:
+                if item is not None:
+                    self.latency[item[1].id] = float("inf")
+
+
+class DynamicBatchServerSUT:
+    """Server scenario SUT by dynamic batching of whole utterances: one worker thread per engine
+    (HIP stream each); whenever a worker is free it takes every pending sample (up to max_batch,
+    longest first), assembles the batch on the device (any QSL, incl. the WAV featurizer path),
+    encodes (encoders take turns), decodes and completes each sample with its token row.
+    ``ServerSUT`` (continuous batching with carried state) is the reference's structure; this one
+    serves QSLs without a resident feature store.  Latency per sample = completion - issue time."""
 
     def __init__(self, engines, qsl, max_batch=2048, on_complete=None):
         import threading

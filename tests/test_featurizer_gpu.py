@@ -137,7 +137,7 @@ def test_server_sut_over_wav_qsl():
     import time
     from rnnt_amd import weights
     from rnnt_amd.engine import Engine
-    from rnnt_amd.sut import GpuWavQSL, QuerySample, ServerSUT
+    from rnnt_amd.sut import DynamicBatchServerSUT, GpuWavQSL, QuerySample
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     pm, _ = weights.build_model()
@@ -147,7 +147,7 @@ def test_server_sut_over_wav_qsl():
     assert qsl.lengths.tolist() == frames.tolist()
     engines = [Engine(pm, device=0, max_batch=64, max_frames=128) for _ in range(2)]
     try:
-        srv = ServerSUT(engines, qsl, max_batch=8)
+        srv = DynamicBatchServerSUT(engines, qsl, max_batch=8)
         srv.start()
         samples = [QuerySample(id=i, index=i) for i in range(len(frames))]
         for k in range(0, len(samples), 5):

@@ -80,16 +80,16 @@ def test_offline_sut_batches_in_flight(dec, model):
 
 
 def test_server_sut_dynamic_batching(dec, model):
-    """ServerSUT (dynamic batching over two engines in flight) answers every sample with the
+    """DynamicBatchServerSUT (dynamic batching over two engines in flight) answers every sample with the
     same tokens as the Offline path, whatever batches the arrivals happened to form."""
     import time
     from rnnt_amd.engine import Engine
-    from rnnt_amd.sut import GpuQSL, OfflineSUT, QuerySample, ServerSUT
+    from rnnt_amd.sut import DynamicBatchServerSUT, GpuQSL, OfflineSUT, QuerySample
     lengths = np.minimum(synthetic.devclean_lengths(40, seed=51), 128)
     qsl = GpuQSL(lengths, seed=52)
     e2 = Engine(model, device=0, max_batch=64, max_frames=128)
     try:
-        srv = ServerSUT([dec.engine, e2], qsl, max_batch=16)
+        srv = DynamicBatchServerSUT([dec.engine, e2], qsl, max_batch=16)
         srv.start()
         samples = [QuerySample(id=i, index=i) for i in range(len(lengths))]
         for k in range(0, len(samples), 7):

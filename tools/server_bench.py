@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """MLPerf Server scenario on one MI355X (BASELINE config 5, per GPU): Poisson arrivals of
 single-sample queries at a target QPS over a dev-clean-shaped QSL, served by
-rnnt_amd.sut.ServerSUT (dynamic batching over engines in flight); reports latency percentiles
+rnnt_amd.sut.ServerSUT (continuous batching: slots carrying LSTM / greedy state across split_len
+chunks, refilled as samples finish -- the reference's PipelineState) or, with --mode dynamic,
+DynamicBatchServerSUT (whole utterances, dynamic batches); reports latency percentiles
 and, with --search, the largest QPS whose p99 latency meets the Server bound
 (rnnt.Server.target_latency = 1000 ms, reference configs/mlperf.conf).
 
-    python tools/server_bench.py --qps 20000 --duration 10
-    python tools/server_bench.py --search
+    python tools/server_bench.py --qps 20000 --duration 10 [--slots 4096 --split-len 32]
+    python tools/server_bench.py --search [--mode dynamic]
 Latency = completion (tokens on the host) - scheduled arrival time.  8 GPUs = 8 independent
 processes (queries are dealt per GPU; no collective), so per-GPU QPS x 8 is the node figure.
 """
@@ -25,14 +27,17 @@ import torch  # noqa: E402
 
 from rnnt_amd import synthetic, weights  # noqa: E402
 from rnnt_amd.engine import Engine  # noqa: E402
-from rnnt_amd.sut import GpuQSL, QuerySample, ServerSUT  # noqa: E402
+from rnnt_amd.sut import DynamicBatchServerSUT, GpuQSL, QuerySample, ServerSUT  # noqa: E402
 
 TARGET_LATENCY_S = 1.0   # mlperf.conf rnnt.Server.target_latency (ms) / 1000
 PERCENTILE = 99.0        # mlperf.conf *.Server.target_latency_percentile
 
 
-def run_point(engines, qsl, qps, duration, max_batch, seed):
-    sut = ServerSUT(engines, qsl, max_batch=max_batch)
+def run_point(engines, qsl, qps, duration, max_batch, seed, args):
+    if args.mode == "dynamic":
+        sut = DynamicBatchServerSUT(engines, qsl, max_batch=max_batch)
+    else:
+        sut = ServerSUT(engines, qsl, slots=max_batch, split_len=args.split_len, qos_len=args.qos_len)
     sut.start()
     rng = np.random.default_rng(seed)
     n = max(1, int(qps * duration))
@@ -49,6 +54,8 @@ def run_point(engines, qsl, qps, duration, max_batch, seed):
             i = j
         else:
             time.sleep(min(0.0005, arrivals[i] - now))
+    if hasattr(sut, "flush_queries"):
+        sut.flush_queries()  # LoadGen's FlushQueries after the last issue: deferred QoS samples run
     deadline = time.perf_counter() + 60.0
     while len(sut.latency) < n and time.perf_counter() < deadline and not sut.errors:
         time.sleep(0.005)
@@ -57,7 +64,8 @@ def run_point(engines, qsl, qps, duration, max_batch, seed):
         raise sut.errors[0]
     lat = np.array([sut.latency.get(k, np.inf) for k in range(n)])
     span = time.perf_counter() - t0
-    return dict(target_qps=qps, samples=n, achieved_qps=round(n / max(span, 1e-9), 1), batches=sut.batches,
+    return dict(target_qps=qps, samples=n, achieved_qps=round(n / max(span, 1e-9), 1),
+                rounds=getattr(sut, "rounds", None), batches=getattr(sut, "batches", None),
                 p50_ms=round(float(np.percentile(lat, 50)) * 1e3, 2), p90_ms=round(float(np.percentile(lat, 90)) * 1e3, 2),
                 p99_ms=round(float(np.percentile(lat, PERCENTILE)) * 1e3, 2),
                 max_ms=round(float(lat.max()) * 1e3, 2), valid=bool(np.percentile(lat, PERCENTILE) <= TARGET_LATENCY_S))
@@ -67,7 +75,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--qps", type=float, default=20000.0)
     ap.add_argument("--duration", type=float, default=10.0)
-    ap.add_argument("--max-batch", type=int, default=4096)
+    ap.add_argument("--mode", choices=["continuous", "dynamic"], default="continuous")
+    ap.add_argument("--max-batch", "--slots", type=int, default=4096, help="slots per engine (continuous) / max batch")
+    ap.add_argument("--split-len", type=int, default=32, help="continuous: frames per chunk (reference LEN)")
+    ap.add_argument("--qos-len", type=int, default=None, help="continuous: defer samples longer than this (frames)")
     ap.add_argument("--inflight", type=int, default=2)
     ap.add_argument("--qsl", type=int, default=2513)
     ap.add_argument("--search", action="store_true", help="largest QPS with p99 <= 1000 ms")
@@ -77,14 +88,14 @@ def main():
     pm, _ = weights.build_model()
     engines = [Engine(pm, device=0, max_batch=args.max_batch, max_frames=500) for _ in range(args.inflight)]
     qsl = GpuQSL(synthetic.devclean_lengths(args.qsl, seed=args.seed), seed=args.seed)
-    run_point(engines, qsl, 2000.0, 1.0, args.max_batch, seed=1)  # warm-up
+    run_point(engines, qsl, 2000.0, 1.0, args.max_batch, 1, args)  # warm-up
     points = []
     if not args.search:
-        points.append(run_point(engines, qsl, args.qps, args.duration, args.max_batch, args.seed))
+        points.append(run_point(engines, qsl, args.qps, args.duration, args.max_batch, args.seed, args))
     else:
         lo, hi, q = 0.0, None, 10000.0
         while hi is None and q < 1e6:
-            p = run_point(engines, qsl, q, args.duration, args.max_batch, args.seed)
+            p = run_point(engines, qsl, q, args.duration, args.max_batch, args.seed, args)
             points.append(p)
             print(json.dumps(p), flush=True)
             if p["valid"]:
@@ -93,13 +104,14 @@ def main():
                 hi = q
         for _ in range(4 if hi else 0):
             q = 0.5 * (lo + hi)
-            p = run_point(engines, qsl, q, args.duration, args.max_batch, args.seed)
+            p = run_point(engines, qsl, q, args.duration, args.max_batch, args.seed, args)
             points.append(p)
             print(json.dumps(p), flush=True)
             lo, hi = (q, hi) if p["valid"] else (lo, q)
     best = max((p for p in points if p["valid"]), key=lambda p: p["target_qps"], default=None)
     print(json.dumps({"scenario": "Server", "target_latency_ms": TARGET_LATENCY_S * 1e3, "percentile": PERCENTILE,
-                      "duration_s": args.duration, "max_batch": args.max_batch, "inflight": args.inflight,
+                      "duration_s": args.duration, "mode": args.mode, "slots_or_max_batch": args.max_batch,
+                      "split_len": args.split_len if args.mode == "continuous" else None, "inflight": args.inflight,
                       "best_valid_qps_per_gpu": best["target_qps"] if best else None, "points": points}))
     for e in engines:
         e.close()
