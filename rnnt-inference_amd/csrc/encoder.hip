@@ -11,6 +11,9 @@
 // Weight rows are gate-interleaved (packed row 4u+g = original row g*1024+u), so a 16x16
 // accumulator tile holds the i,f,g,o pre-activations of one (unit, batch row) in one lane's
 // four registers (C/D map: row = 4*(lane>>4)+reg, col = lane&15).
+#include <stdlib.h>
+#include <string.h>
+
 #include "rnnt_device.hpp"
 #include "encoder.hpp"
 
@@ -71,30 +74,74 @@ __global__ void __launch_bounds__(256) quantize_gather_kernel(const float* __res
 }
 
 // ---------------------------------------------------------------- LSTM step
-// Workgroup tile: 256 packed gate rows (64 units) x 256 batch rows, K swept in 128-byte stages.
-// 8 waves as 4 (gate) x 2 (batch); each wave owns 64 gate rows x 128 batch rows = 4 x 8 MFMA
-// 16x16x64 tiles (128 accumulator VGPRs).  The 256x256 tile is the largest whose int32
-// accumulators fit the register file at 2 waves/SIMD; it balances the per-CU L2->LDS load path
-// against the MFMA.
-constexpr int BM = 256;
-constexpr int BN = ENC_BATCH_TILE;
+// Workgroup tile: BM packed gate rows (BM/4 units) x BN batch rows, K swept in 128-byte stages;
+// 8 waves as 4 (gate) x 2 (batch), each wave WMT x WNT MFMA 16x16x64 tiles (BM = 64 WMT,
+// BN = 32 WNT).  Two shapes:
+//   * 256 x 256 (WMT 4, WNT 8): 128 accumulator VGPRs per lane at 2 waves/SIMD, one workgroup
+//     per CU -- the largest tile whose int32 accumulators fit the register file; it balances the
+//     per-CU L2->LDS load path against the MFMA.  Ticks with many tiles.
+//   * 128 x 128 (WMT 2, WNT 4): 32 accumulator VGPRs, 80 KiB of LDS, two workgroups per CU --
+//     8x the tiles of a layer-step, each with a quarter of the bytes per stage.  Ticks that would
+//     leave CUs idle with the large tile: small batches, the tail ticks of a length-sorted batch.
 constexpr int NWAVE = 8;
-constexpr int STAGE = 65536;                  // one stage: 128 K bytes of 256 A + 256 B rows
-constexpr int TAB_OFF = 2 * STAGE;            // LDS: sigma table after the two stage buffers
-constexpr int SMEM_BYTES = TAB_OFF + ENC_TAB_N * 8;
-static_assert(BN == 256 && SMEM_BYTES <= 160 * 1024, "tile / LDS budget");
-static_assert(BN * 128 <= STAGE && BN * 80 <= STAGE, "the epilogue images fit one stage buffer each");
+template <int WMT, int WNT, int NBUF_ = 2>
+struct TileCfg {
+  static constexpr int BM = 64 * WMT, BN = 32 * WNT;
+  static constexpr int NBUF = NBUF_;             // stage ring depth (NBUF - 1 stages in flight)
+  static constexpr int STAGE = (BM + BN) * 128;  // one stage: 128 K bytes of BM A + BN B rows
+  static constexpr int TAB_OFF = NBUF * STAGE;   // LDS: sigma table after the stage ring
+  static constexpr int SMEM = TAB_OFF + ENC_TAB_N * 8;
+  static constexpr int PA = BM / 64, PB = BN / 64;  // 1 KiB DMA pieces per wave per stage (A, B)
+  static constexpr int CROW = BM / 2;            // fp16 cell-state bytes per batch row of the tile
+  static constexpr int CPR = CROW / 16;          // 16-byte chunks per cell-state row
+  static constexpr int HC = BM / 64;             // 16-byte chunks per int8 h / y row
+  static constexpr int HP = BM / 4 + 16;         // int8 image pitch (16-B aligned rows, offset banks)
+  static constexpr int NGT = G4 / BM;            // gate tiles per layer-step
+  static constexpr int GPX = NGT / 4;            // gate tiles per XCD group
+  static_assert(BM >= 128 && BN >= 128, "staging swizzle: wave row blocks are 16-row aligned");
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(BN * CROW + BN * HP <= STAGE, "c and h images share one stage buffer");
+  static_assert((BN * CPR) % (NWAVE * 64) == 0 && (BN * CPR) / (NWAVE * 64) >= 1, "c DMA pieces per wave");
+};
+using BigTile = TileCfg<4, 8>;
+using SmallTile = TileCfg<2, 4>;
+// the small tile with a 4-deep ring (144 KiB, one workgroup per CU) for ticks of at most one
+// workgroup per CU: a K loop with one stage in flight is latency-bound there (weights stream
+// from MALL / HBM at small batch)
+using TinyTile = TileCfg<2, 4, 4>;
+static_assert(BigTile::BN == ENC_BATCH_TILE && SmallTile::BN == ENC_ROW_TILE, "engine batch tiles");
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(1))) void glb_void;
 
-// byte offset of (row r, byte b < 128) in a swizzled [rows][128 B] image: 16-byte chunk c of
-// row r sits at chunk slot c ^ (r & 7)
-__device__ __forceinline__ int cimg_off(int r, int b) { return r * 128 + ((((b >> 4) ^ r) & 7) << 4) + (b & 15); }
+// byte offset of (row r, byte b < ROWB) in a swizzled [rows][ROWB] image: 16-byte chunk c of
+// row r sits at chunk slot c ^ (r mod chunks-per-row)
+template <int ROWB>
+__device__ __forceinline__ int cimg_off(int r, int b) {
+  return r * ROWB + ((((b >> 4) ^ r) & (ROWB / 16 - 1)) << 4) + (b & 15);
+}
 
+// Top of main-loop iteration s: wait until this wave's pieces of stage s have landed -- at most
+// min(NBUF - 2, stages left after s) later stages (PPS pieces each) may still be in flight --
+// drain its LDS reads, and meet the other waves at the barrier.
+template <int PPS, int NBUF>
+__device__ __forceinline__ void wait_stage(int later) {
+  if (NBUF <= 2 || later <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else if (NBUF == 3 || later == 1) {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(PPS) : "memory");
+  } else {
+    static_assert(NBUF <= 4, "ring depth");
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * PPS) : "memory");
+  }
+}
+
+template <int WMT, int WNT, int NBUF>
 __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem,
                                              unsigned long long st_t0) {
+  using C = TileCfg<WMT, WNT, NBUF>;
+  constexpr int BM = C::BM, BN = C::BN, STAGE = C::STAGE;
   (void)st_t0;
 #ifdef RNNT_DEV_STAMPS
   unsigned est_k;
@@ -112,107 +159,118 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   const int K = a.I + H;
   const int nS = K / 128;  // stages
   const int q = lane >> 4, col = lane & 15;
-  const int u0 = (m0 >> 2) + wm * 16 + q * 4;  // this lane's 4 consecutive units
-  const int nb = n0 + wn * 128 + col;          // batch row of accumulator column j = 0 (row j: nb + 16 j)
+  // this lane's WMT consecutive units: packed rows of the wave start at R = m0 + 16 WMT wm, in
+  // 64-row block R >> 6 at MFMA tile (R & 63) >> 4 (enc_packed_row)
+  const int R = m0 + wm * 16 * WMT;
+  const int u0 = 16 * (R >> 6) + 4 * q + ((R & 63) >> 4);
+  const int nb = n0 + wn * 16 * WNT + col;  // batch row of accumulator column j = 0 (row j: nb + 16 j)
   lds_char* lds = (lds_char*)(lds_void*)smem;
 
-  // ---- staging.  A stage holds K bytes k0..k0+127 (two MFMA k steps) of all 256 A and 256 B
+  // ---- staging.  A stage holds K bytes k0..k0+127 (two MFMA k steps) of all BM A and BN B
   // rows; each 1 KiB LDS-DMA piece moves 8 whole 128-byte rows (8 full cache lines).  Image:
   // 16-byte column c of row r at slot c ^ ((r >> 1) & 7) (two 128-B rows per 256-B bank row), so
   // the ds_read_b128 fragment reads are conflict-free; the swizzle is applied on the DMA source
-  // address.  Wave w moves A rows 32w..32w+31 and B rows 32w..32w+31 (4 pieces each); lane l of
-  // piece j lands at row 32w + 8j + (l >> 3), slot l & 7.  SGPR tile bases + 32-bit lane offsets.
+  // address.  Wave w moves A rows 8 PA w .. and B rows 8 PB w .. (PA / PB pieces each); lane l of
+  // piece j lands at row 8 PA w + 8j + (l >> 3), slot l & 7.  SGPR tile bases + 32-bit lane offsets.
   const int r8 = lane >> 3, sl = lane & 7;
   const int gc0 = (sl ^ ((r8 >> 1) & 7)) * 16;        // even pieces (rows 8j + r8, j even)
   const int gc1 = (sl ^ (((8 + r8) >> 1) & 7)) * 16;  // odd pieces
-  const uint32_t rl = (uint32_t)(32 * wave + r8);
-  const uint32_t oA0 = rl * K + gc0, oA1 = rl * K + gc1;
-  const uint32_t oX0 = rl * a.I + gc0, oX1 = rl * a.I + gc1;
-  const uint32_t oH0 = rl * H + gc0, oH1 = rl * H + gc1;
+  const uint32_t rlA = (uint32_t)(8 * C::PA * wave + r8), rlB = (uint32_t)(8 * C::PB * wave + r8);
+  const uint32_t oA0 = rlA * K + gc0, oA1 = rlA * K + gc1;
+  const uint32_t oX0 = rlB * a.I + gc0, oX1 = rlB * a.I + gc1;
+  const uint32_t oH0 = rlB * H + gc0, oH1 = rlB * H + gc1;
   const int8_t* wbase = a.W + (size_t)m0 * K;
   const int8_t* xbase = a.x + (size_t)n0 * a.I;
   const int8_t* hbase = a.h_in + (size_t)n0 * H - a.I;  // k >= I indexes h at k - I
   auto issueA = [&](int s) __attribute__((always_inline)) {
     const int k = s * 128;
-    lds_char* st = lds + (s & 1) * STAGE + wave * 4096;
+    lds_char* st = lds + (s % NBUF) * STAGE + wave * (C::PA * 1024);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < C::PA; ++j)
       __builtin_amdgcn_global_load_lds((glb_void*)(wbase + (size_t)(8 * j) * K + k + ((j & 1) ? oA1 : oA0)),
                                        (lds_void*)(st + j * 1024), 16, 0, 0);
   };
   auto issueB = [&](int s) __attribute__((always_inline)) {
     const int k = s * 128;
-    lds_char* st = lds + (s & 1) * STAGE + 32768 + wave * 4096;
+    lds_char* st = lds + (s % NBUF) * STAGE + BM * 128 + wave * (C::PB * 1024);
     if (k < a.I) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < C::PB; ++j)
         __builtin_amdgcn_global_load_lds((glb_void*)(xbase + (size_t)(8 * j) * a.I + k + ((j & 1) ? oX1 : oX0)),
                                          (lds_void*)(st + j * 1024), 16, 0, 0);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < C::PB; ++j)
         __builtin_amdgcn_global_load_lds((glb_void*)(hbase + (size_t)(8 * j) * H + k + ((j & 1) ? oH1 : oH0)),
                                          (lds_void*)(st + j * 1024), 16, 0, 0);
     }
   };
-  // the tile's fp16 cell state (BN rows x 64 units x 2 B = 32 KiB), DMA'd into the buffer the last
-  // stage does not occupy once its reads are retired; piece p, lane l: row 8p + (l >> 3), chunk
-  // l & 7 at slot (l & 7) ^ (row & 7) (cimg_off: 2-way instead of 8-way epilogue conflicts)
-  const int cbuf = (nS & 1) * STAGE;
+  // the tile's fp16 cell state (BN rows x CROW bytes), DMA'd into the buffer the last stage does
+  // not occupy once its reads are retired; piece p, lane l: row p (64 / CPR) + l / CPR, chunk
+  // (l % CPR) ^ (row % CPR) at slot l % CPR (cimg_off: 2-way instead of 8-way epilogue conflicts)
+  const int cbuf = (nS % NBUF) * STAGE;
   auto issue_c = [&]() __attribute__((always_inline)) {
-    const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+    constexpr int RPP = 64 / C::CPR, NPC = BN * C::CPR / (NWAVE * 64);
+    const int cr = lane / C::CPR, cc = lane % C::CPR;
+    const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + (cc ^ (cr & (C::CPR - 1))) * 8;
 #pragma unroll
-    for (int pc = 0; pc < 4; ++pc) {
-      const int p = wave * 4 + pc;
-      __builtin_amdgcn_global_load_lds((glb_void*)(cb + (size_t)(8 * p + (lane >> 3)) * H), (lds_void*)(lds + cbuf + p * 1024),
+    for (int pc = 0; pc < NPC; ++pc) {
+      const int p = wave * NPC + pc;
+      __builtin_amdgcn_global_load_lds((glb_void*)(cb + (size_t)(RPP * p + cr) * H), (lds_void*)(lds + cbuf + p * 1024),
                                        16, 0, 0);
     }
   };
 
-  v4i acc[4][8];
+  v4i acc[WMT][WNT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < WMT; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+    for (int j = 0; j < WNT; ++j) acc[i][j] = v4i{0, 0, 0, 0};
 
-  // ---- main loop.  Stage s+1 is DMA'd into the other buffer while stage s is consumed: every
-  // wave issues its A pieces right after the stage barrier and its B pieces after the first k
-  // step's 32 MFMAs (two half bursts per stage on the load path; measured best of the issue
-  // points tried), MFMA clusters at s_setprio 1.  Fragment reads: A rows
-  // wm*64 + 16i + col, B rows wn*128 + 16j + col, 16-byte column 4kk + q.
+  // ---- main loop.  Stages s+1 .. s+NBUF-1 are DMA'd into the other ring buffers while stage s
+  // is consumed: every wave issues its A pieces of stage s+NBUF-1 right after the stage barrier
+  // and its B pieces after the first k step's MFMAs (two half bursts per stage on the load path;
+  // measured best of the issue points tried), MFMA clusters at s_setprio 1.
+  // Fragment reads: A rows 16 WMT wm + 16i + col, B rows 16 WNT wn + 16j + col, 16-byte column
+  // 4kk + q.
   const int sw = col >> 1;  // (row >> 1) & 7 for rows 16i + col
-  const int fa0 = (wm * 64 + col) * 128, fb0 = 32768 + (wn * 128 + col) * 128;
-  issueA(0);
-  issueB(0);
+  const int fa0 = (wm * 16 * WMT + col) * 128, fb0 = BM * 128 + (wn * 16 * WNT + col) * 128;
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s)
+    if (s < nS) {
+      issueA(s);
+      issueB(s);
+    }
 #ifdef RNNT_DEV_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stamps only: stage 0 landed (this wave)
   EST_PUT(3, __builtin_amdgcn_s_memrealtime());
   EST_PUT(6, __builtin_amdgcn_s_memtime());
 #endif
   for (int s = 0; s < nS; ++s) {
-    // this wave's DMA of stage s has landed and its LDS reads are drained; after the barrier
-    // every wave's has, and every wave is done reading the buffer stage s+1 refills
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (s + 1 < nS) issueA(s + 1);
-    else issue_c();
-    const int8_t* st = smem + (s & 1) * STAGE;
+    // this wave's DMA of stage s has landed (only later stages' pieces may be outstanding) and
+    // its LDS reads are drained; after the barrier every wave's has, and every wave is done
+    // reading the buffer stage s+NBUF-1 refills
+    wait_stage<C::PA + C::PB, NBUF>(nS - 1 - s);
+    if (s + NBUF - 1 < nS) issueA(s + NBUF - 1);
+    else if (s == nS - 1) issue_c();
+    const int8_t* st = smem + (s % NBUF) * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int cs = ((kk * 4 + q) ^ sw) << 4;
-      v4i fra[4], frb[8];
+      v4i fra[WMT], frb[WNT];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fra[i] = *(const v4i*)(st + fa0 + cs + i * 2048);
+      for (int i = 0; i < WMT; ++i) fra[i] = *(const v4i*)(st + fa0 + cs + i * 2048);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) frb[j] = *(const v4i*)(st + fb0 + cs + j * 2048);
+      for (int j = 0; j < WNT; ++j) frb[j] = *(const v4i*)(st + fb0 + cs + j * 2048);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < WMT; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < WNT; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (kk == 0 && s + 1 < nS) {
-        issueB(s + 1);
+      if (kk == 0 && s + NBUF - 1 < nS) {
+        issueB(s + NBUF - 1);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -226,28 +284,34 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 
   // ---- fused LSTM cell epilogue (quant_lstm.py:162-183 semantics; oracle_enc_cell)
   const float As = a.rb * 64.0f, Ag = a.rb * 128.0f, ins = a.in_s, outs = a.out_s;
-  const float2* tab = (const float2*)(smem + TAB_OFF);
-  float4 bq[4];
+  const float2* tab = (const float2*)(smem + C::TAB_OFF);
+  float4 bq[WMT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) bq[i] = *(const float4*)(a.bq + m0 + wm * 64 + i * 16 + q * 4);
-  // results go to LDS first and leave as whole 128-/64-byte row segments (16 B per lane, full
-  // cache lines per wave instruction) instead of 4-/8-byte scattered per-lane stores: c_new in
-  // place over the c_in image (each lane rewrites exactly what it read), h and y / the bf16
-  // output in the other stage buffer (free after the main loop)
-  const int ul = u0 - (m0 >> 2);  // this lane's first unit within the tile's 64
-  lds_char* hs = lds + cbuf + 32768;
-  lds_char* ys = lds + ((nS - 1) & 1) * STAGE;
-  constexpr int HP = 80;  // int8 image pitch (64 B + 16: conflict-free 4-byte writes, 16-B aligned rows)
+  for (int i = 0; i < WMT; ++i) bq[i] = *(const float4*)(a.bq + R + i * 16 + q * 4);
+  // results go to LDS first and leave as whole row segments (16 B per lane, full cache lines per
+  // wave instruction) instead of scattered per-lane stores: c_new in place over the c_in image
+  // (each lane rewrites exactly what it read), h and y / the bf16 output in the other stage
+  // buffer (free after the main loop)
+  const int ul = u0 - (m0 >> 2);  // this lane's first unit within the tile's BM / 4
+  lds_char* hs = lds + cbuf + BN * C::CROW;
+  lds_char* ys = lds + ((nS - 1) % NBUF) * STAGE;
+  constexpr int HP = C::HP;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < WNT; ++j) {
     const int n = nb + 16 * j, r = n - n0;
-    const uint2 cv = *(const uint2*)(smem + cbuf + cimg_off(r, ul * 2));
-    const float cin[4] = {h2f((uint16_t)(cv.x & 0xffff)), h2f((uint16_t)(cv.x >> 16)), h2f((uint16_t)(cv.y & 0xffff)),
-                          h2f((uint16_t)(cv.y >> 16))};
-    uint32_t cw[2] = {0u, 0u}, hb[4], yb[4];
-    float hv[4];
+    float cin[WMT];
+    if (WMT == 4) {
+      const uint2 cv = *(const uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
+      cin[0] = h2f((uint16_t)(cv.x & 0xffff)); cin[1] = h2f((uint16_t)(cv.x >> 16));
+      cin[2 % WMT] = h2f((uint16_t)(cv.y & 0xffff)); cin[3 % WMT] = h2f((uint16_t)(cv.y >> 16));
+    } else {
+      const uint32_t cv = *(const uint32_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
+      cin[0] = h2f((uint16_t)(cv & 0xffff)); cin[1 % WMT] = h2f((uint16_t)(cv >> 16));
+    }
+    uint32_t cw[2] = {0u, 0u}, hb[4] = {0u, 0u, 0u, 0u}, yb[4] = {0u, 0u, 0u, 0u};
+    float hv[WMT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < WMT; ++i) {
       float cn, hh;
       enc_cell(tab, acc[i][j], bq[i], As, Ag, cin[i], cn, hh);
       cw[i >> 1] |= (uint32_t)f2h(cn) << (16 * (i & 1));
@@ -256,30 +320,44 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       yb[i] = q8_biased(hh * outs);
     }
     const uint32_t hq = pack_q8(hb[0], hb[1], hb[2], hb[3]), yq = pack_q8(yb[0], yb[1], yb[2], yb[3]);
-    *(uint2*)(smem + cbuf + cimg_off(r, ul * 2)) = uint2{cw[0], cw[1]};
-    *(uint32_t*)(hs + r * HP + ul) = hq;
-    if (a.mode == ENC_OUT_FINAL) {
-      if (a.y32) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1], hv[2], hv[3]};
-      *(uint2*)(ys + cimg_off(r, ul * 2)) = uint2{(uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1]) << 16),
-                                               (uint32_t)f2bf_ftz(hv[2]) | ((uint32_t)f2bf_ftz(hv[3]) << 16)};
+    if (WMT == 4) {
+      *(uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)) = uint2{cw[0], cw[1]};
+      *(uint32_t*)(hs + r * HP + ul) = hq;
     } else {
+      *(uint32_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)) = cw[0];
+      *(uint16_t*)(hs + r * HP + ul) = (uint16_t)hq;
+    }
+    if (a.mode == ENC_OUT_FINAL) {
+      if (a.y32) {
+        if (WMT == 4) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1 % WMT], hv[2 % WMT], hv[3 % WMT]};
+        else *(float2*)(a.y32 + (size_t)n * H + u0) = float2{hv[0], hv[1 % WMT]};
+      }
+      const uint32_t f01 = (uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1 % WMT]) << 16);
+      if (WMT == 4)
+        *(uint2*)(ys + cimg_off<C::CROW>(r, ul * 2)) =
+            uint2{f01, (uint32_t)f2bf_ftz(hv[2 % WMT]) | ((uint32_t)f2bf_ftz(hv[3 % WMT]) << 16)};
+      else
+        *(uint32_t*)(ys + cimg_off<C::CROW>(r, ul * 2)) = f01;
+    } else if (WMT == 4) {
       *(uint32_t*)(ys + r * HP + ul) = yq;
+    } else {
+      *(uint16_t*)(ys + r * HP + ul) = (uint16_t)yq;
     }
   }
   __syncthreads();  // the staged images are complete
-  // copy-out: thread t moves 16-byte chunks; a wave instruction writes 8 (c, bf16 f) or 16 (h, y)
-  // whole row segments
+  // copy-out: thread t moves 16-byte chunks; a wave instruction writes whole row segments
   const int um = m0 >> 2;
 #pragma unroll
-  for (int it = 0; it < BN * 8 / (NWAVE * 64); ++it) {  // c: BN rows x 128 B
-    const int idx = it * NWAVE * 64 + tid, r = idx >> 3, ch = idx & 7;
-    *(uint4*)(a.c + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(smem + cbuf + cimg_off(r, ch * 16));
+  for (int it = 0; it < BN * C::CPR / (NWAVE * 64); ++it) {  // c (and bf16 f): BN rows x CROW bytes
+    const int idx = it * NWAVE * 64 + tid, r = idx / C::CPR, ch = idx % C::CPR;
+    *(uint4*)(a.c + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(smem + cbuf + cimg_off<C::CROW>(r, ch * 16));
     if (a.mode == ENC_OUT_FINAL)
-      *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + cimg_off(r, ch * 16));
+      *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + cimg_off<C::CROW>(r, ch * 16));
   }
 #pragma unroll
-  for (int it = 0; it < BN * 4 / (NWAVE * 64); ++it) {  // h, y: BN rows x 64 B
-    const int idx = it * NWAVE * 64 + tid, r = idx >> 2, ch = idx & 3, n = n0 + r;
+  for (int it = 0; it < (BN * C::HC + NWAVE * 64 - 1) / (NWAVE * 64); ++it) {  // h, y: BN rows x BM / 4 bytes
+    const int idx = it * NWAVE * 64 + tid, r = idx / C::HC, ch = idx % C::HC, n = n0 + r;
+    if ((BN * C::HC) % (NWAVE * 64) != 0 && idx >= BN * C::HC) break;
     *(uint4*)(a.h_out + (size_t)n * H + um + ch * 16) = *(const uint4*)(hs + r * HP + ch * 16);
     if (a.mode == ENC_OUT_I8) {
       *(uint4*)(a.y8 + (size_t)n * H + um + ch * 16) = *(const uint4*)(ys + r * HP + ch * 16);
@@ -303,40 +381,48 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 
 // One launch = one wavefront tick: up to 5 independent layer-steps (jobs, longest K first).
 // XCD-aware tile order: workgroup id -> XCD id % 8 (round-robin dispatch).  XCD x takes gate
-// tiles 4(x&3)..4(x&3)+3 and the (x>>2)-th half of each job's active batch tiles, so the 32
-// workgroups resident on an XCD share 4 weight tiles and ~8 activation tiles through its L2
-// (weights fetched from HBM/MALL 2x, activations 4x per tick, instead of 1x / 8x).
+// tiles GPX (x&3) .. GPX (x&3) + GPX - 1 and the (x>>2)-th half of each job's active batch tiles,
+// so the workgroups resident on an XCD share a quarter of the weight tiles and half the
+// activation tiles through its L2 (weights fetched from HBM/MALL 2x, activations 4x per tick,
+// instead of 1x / 8x).  Batch tiles of a job: its active 128-row tiles in the tile's rows.
+template <class C>
+__device__ __forceinline__ int job_tiles(const EncTickArgs& args, int j) {
+  return C::BN == 256 ? (args.nbt[j] + 1) >> 1 : args.nbt[j];
+}
 // job tile k (0..) of XCD xcd -> (mt, nt); -1 past the XCD's last tile
+template <class C>
 __device__ __forceinline__ int xcd_pick(const EncTickArgs& args, int xcd, int k, int& mt, int& nt) {
   const int gsel = xcd & 3, psel = xcd >> 2;
   for (int j = 0; j < args.njobs; ++j) {
-    const int nbt = args.nbt[j];
+    const int nbt = job_tiles<C>(args, j);
     const int b0 = psel ? (nbt + 1) >> 1 : 0;
     const int b1 = psel ? nbt : (nbt + 1) >> 1;
-    const int cnt = 4 * (b1 - b0);
+    const int cnt = C::GPX * (b1 - b0);
     if (k < cnt) {
-      mt = gsel * 4 + (k & 3);
-      nt = b0 + (k >> 2);
+      mt = gsel * C::GPX + k % C::GPX;
+      nt = b0 + k / C::GPX;
       return j;
     }
     k -= cnt;
   }
   return -1;
 }
-__global__ void __launch_bounds__(NWAVE * 64, 1) lstm_i8_tick_kernel(EncTickArgs args) {
+template <int WMT, int WNT, int NBUF>
+__global__ void __launch_bounds__(NWAVE * 64) lstm_i8_tick_kernel(EncTickArgs args) {
+  using C = TileCfg<WMT, WNT, NBUF>;
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   unsigned long long st_t0 = 0ull;
   EST_MARK(st_t0);
   // sigma table into LDS (read after the main loop's first stage barrier)
 #pragma unroll
   for (int i = 0; i < ENC_TAB_N / (2 * NWAVE * 64); ++i)
-    ((float4*)(smem + TAB_OFF))[i * NWAVE * 64 + threadIdx.x] = ((const float4*)g_act_tab)[i * NWAVE * 64 + threadIdx.x];
+    ((float4*)(smem + C::TAB_OFF))[i * NWAVE * 64 + threadIdx.x] = ((const float4*)g_act_tab)[i * NWAVE * 64 + threadIdx.x];
   int mt = 0, nt = 0;
-  const int jsel = xcd_pick(args, blockIdx.x & 7, blockIdx.x >> 3, mt, nt);
+  const int jsel = xcd_pick<C>(args, blockIdx.x & 7, blockIdx.x >> 3, mt, nt);
   if (jsel < 0) return;
   // wave-uniform runtime index into the kernarg segment: the job's fields stay scalar loads
-  lstm_i8_step(args.job[__builtin_amdgcn_readfirstlane(jsel)], __builtin_amdgcn_readfirstlane(mt),
-               __builtin_amdgcn_readfirstlane(nt), smem, st_t0);
+  lstm_i8_step<WMT, WNT, NBUF>(args.job[__builtin_amdgcn_readfirstlane(jsel)], __builtin_amdgcn_readfirstlane(mt),
+                         __builtin_amdgcn_readfirstlane(nt), smem, st_t0);
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -360,17 +446,55 @@ int launch_quantize_gather(const float* store, const int64_t* offsets, const int
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
+// Per tick: the 256 x 256 tile unless its last round of workgroups would leave many CUs idle
+// and the 128 x 128 tile (two per CU, 8x the tiles) finishes sooner.  Cost model in units of a
+// large-tile round (one 256 x 256 tile per CU), measured at N=8192 / 2048 / 256 (DESIGN.md
+// section 4): a full round of small tiles (two per CU) costs ENC_SMALL_ROUND of it, and a
+// small-tile launch takes at least ENC_SMALL_FLOOR (its K loop's latency); the small tile must
+// win by ENC_SMALL_MARGIN (its co-resident workgroups also leave room for the overlapped
+// decode's, which slows the encoder).  RNNT_ENC_TILE=big|small|tiny forces a shape.
+constexpr int ENC_CUS = 256;
+constexpr float ENC_SMALL_ROUND = 0.59f, ENC_SMALL_FLOOR = 0.5f, ENC_SMALL_MARGIN = 0.9f;
+static int enc_tile_choice() {  // read per launch (a test may switch it between calls)
+  const char* s = getenv("RNNT_ENC_TILE");
+  if (!s) return 0;
+  if (!strcmp(s, "big")) return 1;
+  if (!strcmp(s, "small")) return 2;
+  if (!strcmp(s, "tiny")) return 3;
+  return 0;
+}
+template <class C>
+static int tick_grid(const EncTickArgs& a) {  // workgroups: 8 XCDs x the batch-half-0 XCDs' (larger) share
+  int per_xcd = 0;
+  for (int j = 0; j < a.njobs; ++j) {
+    const int nbt = C::BN == 256 ? (a.nbt[j] + 1) / 2 : a.nbt[j];
+    per_xcd += C::GPX * ((nbt + 1) / 2);
+  }
+  return 8 * per_xcd;
+}
+template <class C>
+static int launch_tick(const EncTickArgs& a, int grid, hipStream_t st) {
   static std::atomic<uint64_t> attr{0};
-  if (set_smem_attr_once((const void*)lstm_i8_tick_kernel, SMEM_BYTES, attr)) return -1;
+  const void* fn = (const void*)lstm_i8_tick_kernel<C::BM / 64, C::BN / 32, C::NBUF>;
+  if (set_smem_attr_once(fn, C::SMEM, attr)) return -1;
+  hipLaunchKernelGGL((lstm_i8_tick_kernel<C::BM / 64, C::BN / 32, C::NBUF>), dim3(grid), dim3(NWAVE * 64), C::SMEM, st, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
   // shapes the kernel's staging assumes (checked on the host: a mismatch would read out of bounds)
   for (int j = 0; j < a.njobs; ++j)
     if (a.job[j].I % 128 != 0 || a.nbt[j] < 0) return -1;
-  int per_xcd = 0;  // the batch-half-0 XCDs carry the larger half
-  for (int j = 0; j < a.njobs; ++j) per_xcd += 4 * ((a.nbt[j] + 1) / 2);
-  if (per_xcd <= 0) return 0;
-  hipLaunchKernelGGL(lstm_i8_tick_kernel, dim3(8 * per_xcd), dim3(NWAVE * 64), SMEM_BYTES, st, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  const int gb = tick_grid<BigTile>(a), gs = tick_grid<SmallTile>(a);
+  if (gb <= 0) return 0;
+  int choice = enc_tile_choice();
+  if (choice == 0) {
+    const float rb = (float)((gb + ENC_CUS - 1) / ENC_CUS);
+    const float rs = fmaxf((float)gs / (2 * ENC_CUS) * ENC_SMALL_ROUND, ENC_SMALL_FLOOR);
+    choice = rs < ENC_SMALL_MARGIN * rb ? 2 : 1;
+  }
+  if (choice == 0 && gs <= ENC_CUS) choice = 3;  // at most one small workgroup per CU: the deep ring
+  if (choice == 1) return launch_tick<BigTile>(a, gb, st);
+  return choice == 3 ? launch_tick<TinyTile>(a, gs, st) : launch_tick<SmallTile>(a, gs, st);
 }
 
 }  // namespace rnnt

@@ -5,8 +5,10 @@
 
 namespace rnnt {
 
-// Encoder workgroup tile: 256 gate rows x 256 batch rows (8 waves, one workgroup per CU).
-constexpr int ENC_BATCH_TILE = 256;  // batch rows per encoder workgroup
+// Encoder workgroup tiles (encoder.hip): 256 gate rows x 256 batch rows (one workgroup per CU)
+// or 128 x 128 (two per CU), chosen per tick; tick jobs count active batch rows in 128-row tiles.
+constexpr int ENC_BATCH_TILE = 256;  // batch rows of the large tile
+constexpr int ENC_ROW_TILE = 128;    // batch rows of the small tile = the granularity of EncTickArgs::nbt
 constexpr int ENC_PAD = 256;         // batch buffers are padded to a multiple of this
 
 // Packed row of (unit u, gate g) in the encoder weight image.  Each wave's 64 gate rows hold
@@ -44,7 +46,7 @@ struct EncStepArgs {
 constexpr int ENC_MAX_JOBS = 5;
 struct EncTickArgs {
   EncStepArgs job[ENC_MAX_JOBS];
-  int nbt[ENC_MAX_JOBS];  // active 256-row batch tiles per job
+  int nbt[ENC_MAX_JOBS];  // active 128-row batch tiles per job (leading tiles holding a row still running)
   int njobs;
 };
 

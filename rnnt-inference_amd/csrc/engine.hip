@@ -484,7 +484,7 @@ static int state_release(rnnt_engine* e, hipStream_t st) {
   return 0;
 }
 
-// number of leading 256-row tiles that hold a row with len > thr
+// number of leading 128-row tiles that hold a row with len > thr
 static int active_tiles(const std::vector<int>& tile_max, int thr) {
   int last = -1;
   for (int i = 0; i < (int)tile_max.size(); ++i)
@@ -551,7 +551,7 @@ static int run_layer(rnnt_engine* e, int l, int T, int n_pad, const int8_t* x, i
                      hipStream_t st) {
   for (int t = 0; t < T; ++t) {
     TickBuilder tb;
-    tb.add(make_job(e, l, t, n_pad, x, mode, y, y32, nullptr, 0), n_pad / ENC_BATCH_TILE);
+    tb.add(make_job(e, l, t, n_pad, x, mode, y, y32, nullptr, 0), n_pad / ENC_ROW_TILE);
     int r = tb.launch(e, st);
     if (r) return r;
   }
@@ -568,8 +568,8 @@ static int check_batch(rnnt_engine* e, int T, int n, int n_pad) {
 static std::vector<int> tile_maxima(const int32_t* lens_host, int n, int n_pad) {
   std::vector<int> tm;
   if (!lens_host) return tm;
-  tm.assign(n_pad / ENC_BATCH_TILE, 0);
-  for (int i = 0; i < n; ++i) tm[i / ENC_BATCH_TILE] = std::max(tm[i / ENC_BATCH_TILE], (int)lens_host[i]);
+  tm.assign(n_pad / ENC_ROW_TILE, 0);
+  for (int i = 0; i < n; ++i) tm[i / ENC_ROW_TILE] = std::max(tm[i / ENC_ROW_TILE], (int)lens_host[i]);
   return tm;
 }
 
@@ -631,7 +631,7 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
   // Wavefront schedule: tick tau runs layer 0 at frame tau, layer 1 at frame tau-1, and the
   // post_rnn layers 2/3/4 at stacked frame t' on ticks 2t'+3 / 2t'+4 / 2t'+5, i.e. as soon as
   // their inputs exist.  Every job of a tick is independent (inputs come from earlier ticks).
-  const int nt_all = n_pad / ENC_BATCH_TILE;
+  const int nt_all = n_pad / ENC_ROW_TILE;
   auto tiles = [&](int thr) { return tm.empty() ? nt_all : active_tiles(tm, thr); };
   const int n_ticks = std::max(T + 1, 2 * Tp + 4);
   for (int tau = 0; tau < n_ticks; ++tau) {

@@ -27,6 +27,14 @@ def engine(model):
     e.close()
 
 
+@pytest.fixture(params=["big", "small", "tiny"])
+def tile(request, monkeypatch):
+    """Every encoder tile variant (256 x 256; 128 x 128 with a 2- and a 4-deep stage ring,
+    encoder.hip) forced in turn; the engine otherwise picks one per tick."""
+    monkeypatch.setenv("RNNT_ENC_TILE", request.param)
+    return request.param
+
+
 def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
@@ -36,7 +44,7 @@ def _valid(f, lens):
     return np.concatenate([f[: fl[n], n].reshape(-1) for n in range(len(lens))])
 
 
-def test_pre_rnn_layers_bitexact(engine, model, oracle):
+def test_pre_rnn_layers_bitexact(engine, model, oracle, tile):
     T, n, n_pad = 7, 5, 256
     rng = np.random.default_rng(5)
     x = synthetic.make_features(T, n_pad, seed=3)
@@ -56,7 +64,7 @@ def test_pre_rnn_layers_bitexact(engine, model, oracle):
     np.testing.assert_array_equal(cd.cpu().numpy(), np.stack([c0, c1]))
 
 
-def test_post_rnn_layers_bitexact(engine, model, oracle):
+def test_post_rnn_layers_bitexact(engine, model, oracle, tile):
     T, n_pad = 5, 256
     rng = np.random.default_rng(6)
     x = rng.integers(-128, 128, (T, n_pad, 2048)).astype(np.int8)
@@ -109,18 +117,18 @@ def _run(engine, model, oracle, T, lens, seed):
     return rlo, steps
 
 
-def test_infer_small_batch(engine, model, oracle):
+def test_infer_small_batch(engine, model, oracle, tile):
     rl, steps = _run(engine, model, oracle, 60, np.array([60, 51, 33, 8, 1, 60, 17, 2], np.int32), seed=1)
     assert rl.sum() > 0
 
 
-def test_infer_edge_cases(engine, model, oracle):
+def test_infer_edge_cases(engine, model, oracle, tile):
     """odd T, a zero-length utterance (batch padding row), length-1 and unsorted lengths."""
     _run(engine, model, oracle, 31, np.array([3, 31, 0, 1, 30, 29], np.int32), seed=2)
     _run(engine, model, oracle, 2, np.array([2], np.int32), seed=4)
 
 
-def test_config3_int8_full_batch128(engine, model, oracle):
+def test_config3_int8_full_batch128(engine, model, oracle, tile):
     """BASELINE config 3: int8 enc + bf16 pred/joint greedy, N=128, lengths U{47..500}, sorted
     descending like the QSL (rnnt_qsl.cpp:104-133)."""
     lens = np.sort(synthetic.uniform_lengths(128, seed=3))[::-1].copy()
@@ -129,17 +137,19 @@ def test_config3_int8_full_batch128(engine, model, oracle):
     assert 0.02 < emit_rate < 5, emit_rate
 
 
-def test_large_batch_rows_match_small_batch(engine, model, oracle):
-    """N=4096 (16 batch tiles: several tiles per workgroup / CU, every tick schedule path) vs the
-    same rows run as small batches: the int8 encoder is exact and row-independent, so encoder
-    frames must be bit-identical and tokens identical whatever the batch composition; the first
-    rows are also checked against the oracle directly."""
+def test_large_batch_rows_match_small_batch(engine, model, oracle, monkeypatch):
+    """N=4096 (16 batch tiles: several tiles per workgroup / CU, every tick schedule path) on the
+    256 x 256 tile vs the same rows run as small batches on the 128 x 128 tile: the int8 encoder
+    is exact and row-independent, so encoder frames must be bit-identical and tokens identical
+    whatever the batch composition and tile shape; the first rows are also checked against the
+    oracle directly."""
     from rnnt_amd.engine import Engine
     n, T = 4096, 20
     lens = np.sort(np.random.default_rng(11).integers(1, T + 1, n).astype(np.int32))[::-1].copy()
     x = synthetic.make_features(T, n, seed=11, lens=lens)
     Tp = (T + 1) // 2
     big = Engine(model, device=0, max_batch=n, max_frames=T)
+    monkeypatch.setenv("RNNT_ENC_TILE", "big")
     try:
         f = torch.zeros((Tp, n, 1024), dtype=torch.float32, device="cuda")
         res = torch.empty((n, big.max_res), dtype=torch.int32, device="cuda")
@@ -150,6 +160,7 @@ def test_large_batch_rows_match_small_batch(engine, model, oracle):
         fg, res_g, rl_g = f.cpu().numpy(), res.cpu().numpy(), rl.cpu().numpy()
     finally:
         big.close()
+    monkeypatch.setenv("RNNT_ENC_TILE", "small")
     for lo in (0, 1800, 4096 - 200):
         rows = np.arange(lo, lo + 200)
         sl = lens[rows]
