@@ -28,6 +28,15 @@ struct EncF32StepArgs {
 };
 
 int launch_lstm_f32_step(const EncF32StepArgs& a, hipStream_t st);
+
+// One launch = one wavefront tick of the fp32 stack (the int8 encoder's schedule, engine.hip):
+// up to 5 independent layer-steps over the same n rows (n_pad a multiple of 64).
+constexpr int ENC_F32_MAX_JOBS = 5;
+struct EncF32TickArgs {
+  EncF32StepArgs job[ENC_F32_MAX_JOBS];  // longest K first
+  int njobs;
+};
+int launch_lstm_f32_tick(const EncF32TickArgs& a, hipStream_t st);
 int launch_permute_feats(const float* x, int64_t rows, float* y, hipStream_t st);
 
 }  // namespace rnnt

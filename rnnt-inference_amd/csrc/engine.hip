@@ -84,7 +84,8 @@ struct rnnt_engine {
   float *f32_wih[5] = {}, *f32_whh[5] = {}, *f32_bih[5] = {}, *f32_bhh[5] = {};
   std::vector<void*> f32_ws;
   size_t f32_ws_T = 0, f32_ws_np = 0;
-  float *f32_x = nullptr, *f32_ya = nullptr, *f32_xs = nullptr, *f32_yb = nullptr, *f32_h[2] = {}, *f32_c = nullptr;
+  float *f32_x = nullptr, *f32_ya = nullptr, *f32_xs = nullptr, *f32_yb = nullptr, *f32_yc = nullptr;
+  float *f32_h[5][2] = {}, *f32_c[5] = {};  // per layer: the wavefront ticks run the layers concurrently
   // fp32 decoder (rnnt_engine_load_f32_decoder) and the last fp32 encode's outputs it decodes
   bool f32_dec_loaded = false;
   DecF32Weights dw32{};
@@ -906,9 +907,12 @@ static int f32_workspace(rnnt_engine* e, int T, int n_pad) {
   if (!r) r = al(&e->f32_ya, (size_t)T * NH);
   if (!r) r = al(&e->f32_xs, Tp * NH * 2);
   if (!r) r = al(&e->f32_yb, Tp * NH);
-  if (!r) r = al(&e->f32_h[0], NH);
-  if (!r) r = al(&e->f32_h[1], NH);
-  if (!r) r = al(&e->f32_c, NH);
+  if (!r) r = al(&e->f32_yc, Tp * NH);
+  for (int l = 0; l < 5; ++l) {
+    if (!r) r = al(&e->f32_h[l][0], NH);
+    if (!r) r = al(&e->f32_h[l][1], NH);
+    if (!r) r = al(&e->f32_c[l], NH);
+  }
   if (r) {
     e->f32_ws_T = e->f32_ws_np = 0;
     return r;
@@ -918,42 +922,37 @@ static int f32_workspace(rnnt_engine* e, int T, int n_pad) {
   return 0;
 }
 
-// one fp32 layer over T steps; x / y advance by their per-frame strides
-static int run_f32_layer(rnnt_engine* e, int l, int T, int n, int n_pad, const float* x, int mode, float* y,
-                         const int32_t* lens, int stacked_T, hipStream_t st) {
+// fp32 layer l's step at frame t (x / y advance by their per-frame strides); h ping-pongs by t
+static EncF32StepArgs f32_job(rnnt_engine* e, int l, int t, int n, int n_pad, const float* x, int mode, float* y,
+                              const int32_t* lens, int stacked_T) {
   const size_t NH = (size_t)n_pad * H;
-  HIPCHK(hipMemsetAsync(e->f32_h[0], 0, NH * sizeof(float), st));
-  HIPCHK(hipMemsetAsync(e->f32_c, 0, NH * sizeof(float), st));
-  for (int t = 0; t < T; ++t) {
-    EncF32StepArgs a{};
-    a.wih = e->f32_wih[l];
-    a.whh = e->f32_whh[l];
-    a.bih = e->f32_bih[l];
-    a.bhh = e->f32_bhh[l];
-    a.I = F32_I[l];
-    a.Ip = F32_IP[l];
-    a.x = x + (size_t)t * n_pad * a.Ip;
-    a.h_in = e->f32_h[t & 1];
-    a.h_out = e->f32_h[(t + 1) & 1];
-    a.c = e->f32_c;
-    a.n = n;
-    a.mode = mode;
-    a.lens = lens;
-    if (mode == ENC_F32_STACKED) {
-      a.y = y + (size_t)(t / 2) * NH * 2;
-      a.t = t;
-      a.half = t & 1;
-      a.zero_next = ((t & 1) == 0 && t + 1 == stacked_T);
-    } else {
-      a.y = y ? y + (size_t)t * NH : nullptr;
-      if (mode == ENC_F32_FINAL) {  // the decoders' copies of f: chain-permuted fp32, and bf16
-        a.y2 = e->f32_fc + (size_t)t * NH;
-        a.ybf = e->fbf && n_pad <= e->np_max && t < e->tp_max ? e->fbf + (size_t)t * NH : nullptr;
-      }
+  EncF32StepArgs a{};
+  a.wih = e->f32_wih[l];
+  a.whh = e->f32_whh[l];
+  a.bih = e->f32_bih[l];
+  a.bhh = e->f32_bhh[l];
+  a.I = F32_I[l];
+  a.Ip = F32_IP[l];
+  a.x = x + (size_t)t * n_pad * a.Ip;
+  a.h_in = e->f32_h[l][t & 1];
+  a.h_out = e->f32_h[l][(t + 1) & 1];
+  a.c = e->f32_c[l];
+  a.n = n;
+  a.mode = mode;
+  a.lens = lens;
+  if (mode == ENC_F32_STACKED) {
+    a.y = y + (size_t)(t / 2) * NH * 2;
+    a.t = t;
+    a.half = t & 1;
+    a.zero_next = ((t & 1) == 0 && t + 1 == stacked_T);
+  } else {
+    a.y = y ? y + (size_t)t * NH : nullptr;
+    if (mode == ENC_F32_FINAL) {  // the decoders' copies of f: chain-permuted fp32, and bf16
+      a.y2 = e->f32_fc + (size_t)t * NH;
+      a.ybf = e->fbf && n_pad <= e->np_max && t < e->tp_max ? e->fbf + (size_t)t * NH : nullptr;
     }
-    if (launch_lstm_f32_step(a, st)) return fail(RNNT_EDEVICE, "fp32 lstm step launch failed");
   }
-  return 0;
+  return a;
 }
 
 extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const int32_t* lens, int T, int n, int n_pad,
@@ -969,12 +968,37 @@ extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const 
   if ((r = f32_workspace(e, T, n_pad))) return r;
   const int Tp = (T + 1) / 2;
   if (launch_permute_feats(feats, (int64_t)T * n_pad, e->f32_x, st)) return fail(RNNT_EDEVICE, "permute launch failed");
-  // Transcription.forward (modeling_rnnt.py:116-144): pre_rnn 2 layers -> StackTime -> post_rnn 3 layers
-  if ((r = run_f32_layer(e, 0, T, n, n_pad, e->f32_x, ENC_F32_NEXT, e->f32_ya, lens, T, st))) return r;
-  if ((r = run_f32_layer(e, 1, T, n, n_pad, e->f32_ya, ENC_F32_STACKED, e->f32_xs, lens, T, st))) return r;
-  if ((r = run_f32_layer(e, 2, Tp, n, n_pad, e->f32_xs, ENC_F32_NEXT, e->f32_yb, lens, Tp, st))) return r;
-  if ((r = run_f32_layer(e, 3, Tp, n, n_pad, e->f32_yb, ENC_F32_NEXT, e->f32_ya, lens, Tp, st))) return r;
-  if ((r = run_f32_layer(e, 4, Tp, n, n_pad, e->f32_ya, ENC_F32_FINAL, f_out, lens, Tp, st))) return r;
+  // Transcription.forward (modeling_rnnt.py:116-144): pre_rnn 2 layers -> StackTime -> post_rnn 3
+  // layers, on the int8 path's wavefront schedule: tick tau runs layer 0 at frame tau, layer 1 at
+  // tau-1 and post_rnn layer l at stacked frame t' on tick 2t' + l + 1 (encode_impl)
+  const size_t NH = (size_t)n_pad * H;
+  for (int l = 0; l < 5; ++l) {
+    HIPCHK(hipMemsetAsync(e->f32_h[l][0], 0, NH * sizeof(float), st));
+    HIPCHK(hipMemsetAsync(e->f32_c[l], 0, NH * sizeof(float), st));
+  }
+  const int n_ticks = std::max(T + 1, 2 * Tp + 4);
+  for (int tau = 0; tau < n_ticks; ++tau) {
+    EncF32TickArgs tk{};
+    auto add = [&](const EncF32StepArgs& a) {  // keep jobs ordered by K descending
+      int p = tk.njobs++;
+      while (p > 0 && tk.job[p - 1].I < a.I) {
+        tk.job[p] = tk.job[p - 1];
+        --p;
+      }
+      tk.job[p] = a;
+    };
+    if (tau < T) add(f32_job(e, 0, tau, n, n_pad, e->f32_x, ENC_F32_NEXT, e->f32_ya, lens, T));
+    if (tau >= 1 && tau - 1 < T) add(f32_job(e, 1, tau - 1, n, n_pad, e->f32_ya, ENC_F32_STACKED, e->f32_xs, lens, T));
+    for (int l = 2; l < 5; ++l) {
+      const int d = tau - (l + 1);  // = 2t'
+      if (d < 0 || (d & 1) || d / 2 >= Tp) continue;
+      const int tp = d / 2;
+      if (l == 2) add(f32_job(e, 2, tp, n, n_pad, e->f32_xs, ENC_F32_NEXT, e->f32_yb, lens, Tp));
+      if (l == 3) add(f32_job(e, 3, tp, n, n_pad, e->f32_yb, ENC_F32_NEXT, e->f32_yc, lens, Tp));
+      if (l == 4) add(f32_job(e, 4, tp, n, n_pad, e->f32_yc, ENC_F32_FINAL, f_out, lens, Tp));
+    }
+    if (launch_lstm_f32_tick(tk, st)) return fail(RNNT_EDEVICE, "fp32 lstm tick launch failed");
+  }
   // f_lens = ceil(lens / 2) for both decoders; the bf16 copy of f (written when the batch fits
   // the int8 workspace) lets rnnt_engine_decode run the f32 + enable_bf16 decoder on it
   hipLaunchKernelGGL(flen_kernel, dim3((n_pad + 255) / 256), dim3(256), 0, st, lens, e->f32_flen, n_pad);

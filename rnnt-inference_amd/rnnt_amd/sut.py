@@ -341,7 +341,7 @@ class ServerSUT:
     iteration, which amortises its CPU iteration) is subsumed: a round is one chunk and answers
     every slot that finished in it.  Latency per sample = completion - issue time."""
 
-    def __init__(self, engines, qsl, slots=2048, split_len=32, qos_len=None, on_complete=None):
+    def __init__(self, engines, qsl, slots=2048, split_len=128, qos_len=None, on_complete=None):
         import threading
         from .engine import pad_batch
         if split_len <= 0 or split_len % 2:

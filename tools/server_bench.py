@@ -7,7 +7,7 @@ DynamicBatchServerSUT (whole utterances, dynamic batches); reports latency perce
 and, with --search, the largest QPS whose p99 latency meets the Server bound
 (rnnt.Server.target_latency = 1000 ms, reference configs/mlperf.conf).
 
-    python tools/server_bench.py --qps 20000 --duration 10 [--slots 4096 --split-len 32]
+    python tools/server_bench.py --qps 20000 --duration 10 [--slots 4096 --split-len 128]
     python tools/server_bench.py --search [--mode dynamic]
 Latency = completion (tokens on the host) - scheduled arrival time.  8 GPUs = 8 independent
 processes (queries are dealt per GPU; no collective), so per-GPU QPS x 8 is the node figure.
@@ -77,7 +77,9 @@ def main():
     ap.add_argument("--duration", type=float, default=10.0)
     ap.add_argument("--mode", choices=["continuous", "dynamic"], default="continuous")
     ap.add_argument("--max-batch", "--slots", type=int, default=4096, help="slots per engine (continuous) / max batch")
-    ap.add_argument("--split-len", type=int, default=32, help="continuous: frames per chunk (reference LEN)")
+    ap.add_argument("--split-len", type=int, default=128,
+                    help="continuous: frames per chunk (the reference's LEN; its CPU Server runs LEN=8, run.sh:74; "
+                         "on the GPU 128-frame chunks measured best: 50k QPS p99 253 ms vs 32-frame chunks invalid)")
     ap.add_argument("--qos-len", type=int, default=None, help="continuous: defer samples longer than this (frames)")
     ap.add_argument("--inflight", type=int, default=2)
     ap.add_argument("--qsl", type=int, default=2513)
