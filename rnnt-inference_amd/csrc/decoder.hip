@@ -407,16 +407,28 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     }
     // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1
     // [h0 of the candidate slot | h1 committed]
-    for (int i = tid; i < DEC_RT * (KX / 8); i += PRED_THREADS) {
-      const int m = i / (KX / 8), k = (i % (KX / 8)) * 8, em = ents[m];
-      uint4 v = uint4{0u, 0u, 0u, 0u};
-      if (em >= 0) {
-        const int r = entry_row(em), smm = entry_slot(em);
+    // every load of the tile first (one memory round trip); entries past the list end read row
+    // 0 (a safe cached address) and stage zeros
+    constexpr int NX = DEC_RT * (KX / 8), NIT = (NX + PRED_THREADS - 1) / PRED_THREADS;
+    uint4 xv[NIT];
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int i = tid + PRED_THREADS * u;
+      if (NX % PRED_THREADS == 0 || i < NX) {
+        const int m = i / (KX / 8), k = (i % (KX / 8)) * 8, em = ents[m];
+        const int r = em >= 0 ? entry_row(em) : 0, smm = em >= 0 ? entry_slot(em) : 0;
         const uint16_t* src = LAYER == 0 ? h_bf(a.hc, r, smm, 0) + k
                                          : (k < P ? h_bf(a.hc, r, smm ^ 1, 0) + k : h_bf(a.hc, r, smm, 1) + k - P);
-        v = *(const uint4*)src;
+        xv[u] = *(const uint4*)src;
       }
-      *(uint4*)&X[m][k] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int i = tid + PRED_THREADS * u;
+      if (NX % PRED_THREADS == 0 || i < NX) {
+        const int m = i / (KX / 8), k = (i % (KX / 8)) * 8;
+        *(uint4*)&X[m][k] = ents[m] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
+      }
     }
     __syncthreads();
     ST_MARK(st2);
@@ -497,13 +509,23 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     }
     __syncthreads();
     ST_MARK(st1);
-    for (int i = tid; i < DEC_RT * (P / 8); i += G_THREADS) {
-      const int m = i / (P / 8), k = (i % (P / 8)) * 8, em = ents[m];
-      uint4 v = uint4{0u, 0u, 0u, 0u};
-      if (em >= 0) {
-        v = *(const uint4*)(h_bf(a.hc, entry_row(em), entry_slot(em) ^ 1, 1) + k);
+    constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
+    uint4 xv[NIT];
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {  // every load first (one round trip); past the list end: row 0, zeros staged
+      const int i = tid + G_THREADS * u;
+      if (NX % G_THREADS == 0 || i < NX) {
+        const int m = i / (P / 8), k = (i % (P / 8)) * 8, em = ents[m];
+        xv[u] = *(const uint4*)(h_bf(a.hc, em >= 0 ? entry_row(em) : 0, em >= 0 ? entry_slot(em) ^ 1 : 0, 1) + k);
       }
-      *(uint4*)&X[m][k] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int i = tid + G_THREADS * u;
+      if (NX % G_THREADS == 0 || i < NX) {
+        const int m = i / (P / 8), k = (i % (P / 8)) * 8;
+        *(uint4*)&X[m][k] = ents[m] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
+      }
     }
     __syncthreads();
     ST_MARK(st2);
@@ -538,11 +560,11 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
 #define RNNT_JOINT_ITERS 2
 #endif
 constexpr int YP = J + 8;
+static_assert(DEC_RT == 16, "the joint's argmax maps 4 waves x 4 rows x 16 lanes onto one 16-row tile");
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][YP];
-  __shared__ float L[DEC_RT][NLAB_PAD + 1];
   __shared__ float Lp[4][DEC_RT][NLAB_PAD + 1];
-  __shared__ int rows[DEC_RT], walking[DEC_RT], tidx[DEC_RT];
+  __shared__ int rows[DEC_RT], walking[DEC_RT], tidx[DEC_RT], emit_e[DEC_RT], fin_f[DEC_RT];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
@@ -586,28 +608,40 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       bool any = false;
       for (int m = 0; m < DEC_RT; ++m) any |= walking[m] != 0;
       if (!any) break;
-      for (int i = tid; i < DEC_RT * (J / 8); i += 256) {
-        const int m = i / (J / 8), k = (i % (J / 8)) * 8;
-        uint4 v = uint4{0u, 0u, 0u, 0u};
-        if (walking[m]) {
-          const int row = rows[m];
-          const float* fr = a.F + ((size_t)tidx[m] * a.Npad + row) * J + k;
-          const float* gr = a.G + (size_t)row * J + k;
-          float y[8];
+      // every load of the tile first (one memory round trip), then y1: rows not walking read a
+      // safe cached address (row 0 of frame 0) and stage zeros
+      constexpr int NIT = DEC_RT * (J / 8) / 256;
+      v4f fl4[NIT][2];
+      float4 gl4[NIT][2];
+      bool wk[NIT];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const v4f f4v = __builtin_nontemporal_load((const v4f*)(fr + 4 * h));  // streamed once
-            const float4 f4 = float4{f4v[0], f4v[1], f4v[2], f4v[3]};
-            const float4 g4 = *(const float4*)(gr + 4 * h);
-            const float s0 = f4.x + g4.x, s1 = f4.y + g4.y, s2 = f4.z + g4.z, s3 = f4.w + g4.w;
-            y[4 * h + 0] = bf_round_ftz(s0 > 0.0f ? s0 : 0.0f);
-            y[4 * h + 1] = bf_round_ftz(s1 > 0.0f ? s1 : 0.0f);
-            y[4 * h + 2] = bf_round_ftz(s2 > 0.0f ? s2 : 0.0f);
-            y[4 * h + 3] = bf_round_ftz(s3 > 0.0f ? s3 : 0.0f);
-          }
-          v = pack8(float4{y[0], y[1], y[2], y[3]}, float4{y[4], y[5], y[6], y[7]});
+      for (int u = 0; u < NIT; ++u) {
+        const int i = tid + 256 * u, m = i / (J / 8), k = (i % (J / 8)) * 8;
+        wk[u] = walking[m] != 0;
+        const int row = wk[u] ? rows[m] : 0, tm = wk[u] ? tidx[m] : 0;
+        const float* fr = a.F + ((size_t)tm * a.Npad + row) * J + k;
+        const float* gr = a.G + (size_t)row * J + k;
+        fl4[u][0] = __builtin_nontemporal_load((const v4f*)fr);  // streamed once
+        fl4[u][1] = __builtin_nontemporal_load((const v4f*)(fr + 4));
+        gl4[u][0] = *(const float4*)gr;
+        gl4[u][1] = *(const float4*)(gr + 4);
+      }
+#pragma unroll
+      for (int u = 0; u < NIT; ++u) {
+        const int i = tid + 256 * u, m = i / (J / 8), k = (i % (J / 8)) * 8;
+        float y[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const v4f f4 = fl4[u][h];
+          const float4 g4 = gl4[u][h];
+          const float s0 = f4[0] + g4.x, s1 = f4[1] + g4.y, s2 = f4[2] + g4.z, s3 = f4[3] + g4.w;
+          y[4 * h + 0] = bf_round_ftz(s0 > 0.0f ? s0 : 0.0f);
+          y[4 * h + 1] = bf_round_ftz(s1 > 0.0f ? s1 : 0.0f);
+          y[4 * h + 2] = bf_round_ftz(s2 > 0.0f ? s2 : 0.0f);
+          y[4 * h + 3] = bf_round_ftz(s3 > 0.0f ? s3 : 0.0f);
         }
-        *(uint4*)&X[m][k] = v;
+        *(uint4*)&X[m][k] = wk[u] ? pack8(float4{y[0], y[1], y[2], y[3]}, float4{y[4], y[5], y[6], y[7]})
+                                  : uint4{0u, 0u, 0u, 0u};
       }
       __syncthreads();
       ST_SET(st2);
@@ -628,44 +662,86 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
         }
       }
       __syncthreads();
-      for (int i = tid; i < DEC_RT * NLAB_PAD; i += 256) {
-        const int m = i / NLAB_PAD, j = i % NLAB_PAD;
-        L[m][j] = ((Lp[0][m][j] + Lp[1][m][j]) + Lp[2][m][j]) + Lp[3][m][j];
-      }
-      __syncthreads();
-      if (tid < DEC_RT && walking[tid]) {
-        const int m = tid, row = rows[m];
-        int best = 0;
-        float bv = L[m][0];
-        for (int j = 1; j < NLAB; ++j)
-          if (L[m][j] > bv) { bv = L[m][j]; best = j; }  // torch.argmax: first maximum
-        if (best != BLANK && s.added[row] != MAXSYM) {
-          const int id = ++s.idx[row];
-          if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
-          s.added[row]++;
-          s.preg[row] = best;
-          const int nsl = s.slot[row] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
-          s.slot[row] = nsl;
-          s.list[(parity ^ 1) * a.Npad + atomicAdd(&s.count[parity ^ 1], 1)] = emit_entry(row, nsl, best);
-          walking[m] = 0;
-        } else {
-          const int fl = a.f_lens[row];
-          int t = tidx[m] + 1;
-          if (t >= fl) {
-            s.fin[row] = 1;
-            atomicSub(s.unfinished, 1);
-            walking[m] = 0;
-            rows[m] = -1;  // finished: not in the next live list
-            t = fl - 1;
+      // logits = ((s0 + s1) + s2) + s3 and the argmax over the 29 real labels: wave w takes rows
+      // 4w .. 4w+3, 16 lanes per row with labels 2l, 2l+1, merged by cross-lane moves (larger
+      // value, ties to the smaller label: torch.argmax's first maximum); the row's first lane
+      // applies greedy_decode_update
+      {
+        const int m = 4 * wave + (lane >> 4), l2 = 2 * (lane & 15);
+        float bv = 0.0f;
+        int bl = -1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int j = l2 + e;
+          const float v = ((Lp[0][m][j] + Lp[1][m][j]) + Lp[2][m][j]) + Lp[3][m][j];
+          if (j < NLAB && (bl < 0 || v > bv)) {
+            bv = v;
+            bl = j;
           }
-          tidx[m] = t;
-          s.time[row] = t;
-          s.added[row] = 0;
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          const float ov = __shfl_xor(bv, off);
+          const int ol = __shfl_xor(bl, off);
+          if (ol >= 0 && (bl < 0 || ov > bv || (ov == bv && ol < bl))) {
+            bv = ov;
+            bl = ol;
+          }
+        }
+        if ((lane & 15) == 0) {
+          emit_e[m] = -1;
+          fin_f[m] = 0;
+          if (walking[m]) {
+            const int row = rows[m], best = bl;
+            if (best != BLANK && s.added[row] != MAXSYM) {
+              const int id = ++s.idx[row];
+              if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
+              s.added[row]++;
+              s.preg[row] = best;
+              const int nsl = s.slot[row] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+              s.slot[row] = nsl;
+              emit_e[m] = emit_entry(row, nsl, best);
+              walking[m] = 0;
+            } else {
+              const int fl = a.f_lens[row];
+              int t = tidx[m] + 1;
+              if (t >= fl) {
+                s.fin[row] = 1;
+                fin_f[m] = 1;
+                walking[m] = 0;
+                rows[m] = -1;  // finished: not in the next live list
+                t = fl - 1;
+              }
+              tidx[m] = t;
+              s.time[row] = t;
+              s.added[row] = 0;
+            }
+          }
         }
       }
       __syncthreads();
+      // one atomic per tile and list: the tile's emitting rows go to the next emit list, its
+      // finished rows leave the live-row counter
+      if (wave == 0) {
+        const int e = lane < DEC_RT ? emit_e[lane] : -1;
+        const unsigned long long me = __ballot(e >= 0);
+        int base = 0;
+        if (lane == 0 && me) base = atomicAdd(&s.count[parity ^ 1], __popcll(me));
+        base = __shfl(base, 0);
+        if (e >= 0) s.list[(parity ^ 1) * a.Npad + base + __popcll(me & ((1ull << lane) - 1))] = e;
+        const unsigned long long mf = __ballot(lane < DEC_RT && fin_f[lane] != 0);
+        if (lane == 0 && mf) atomicSub(s.unfinished, __popcll(mf));
+      }
+      __syncthreads();
     }
-    if (tid < DEC_RT && rows[tid] >= 0) nlist[atomicAdd(&s.count[2 + (parity ^ 1)], 1)] = rows[tid];
+    if (wave == 0) {  // the tile's unfinished rows -> next live list, one atomic
+      const int r = lane < DEC_RT ? rows[lane] : -1;
+      const unsigned long long mr = __ballot(r >= 0);
+      int base = 0;
+      if (lane == 0 && mr) base = atomicAdd(&s.count[2 + (parity ^ 1)], __popcll(mr));
+      base = __shfl(base, 0);
+      if (r >= 0) nlist[base + __popcll(mr & ((1ull << lane) - 1))] = r;
+    }
     __syncthreads();  // rows / walking / tidx / X are reused by the next row tile
     ST_FLUSH(3, st0, st1, st2, 0ull);
   }
