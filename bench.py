@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--inflight", type=int, default=3,
                     help="engines per GPU (one HIP stream + host thread each): one batch's latency-bound greedy "
                          "decode overlaps the next batch's encoder")
+    ap.add_argument("--early-decodes", type=int, default=None,
+                    help="only the first K batches decode beside the next encoder; the others wait for every encode "
+                         "(default: all decode right after their encode)")
     ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wav", action="store_true",
@@ -191,7 +194,7 @@ def main():
     query = args.query * world
     ids, idx = dist.query_arrays(args.qsl, query)
     engines = [Engine(pm, device=local, max_batch=min(args.batch, query), max_frames=500) for _ in range(args.inflight)]
-    sut = OfflineSUT(engines, qsl)
+    sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
 
     def step():
         """One Offline query: sort + batch + deal, this rank's share through the SUT, gather."""

@@ -105,10 +105,14 @@ def make_batches(qsl, ids, idx, batch_size, sizes=None):
 
 
 class OfflineSUT:
-    def __init__(self, engines, qsl, batch_size=1024, batch_sizes=None, on_complete=None):
+    def __init__(self, engines, qsl, batch_size=1024, batch_sizes=None, on_complete=None, early_decodes=None):
         """engines: one Engine or a list (several per GPU keep batches in flight; engines on
         different devices serve one query together).  qsl: one QSL, or {device: QSL} when each
-        GPU holds its own copy of the samples (GpuQSL replicas)."""
+        GPU holds its own copy of the samples (GpuQSL replicas).  early_decodes: None = every
+        batch decodes right after its encode (beside the next batch's encoder); k = when the query
+        has no more batches than engines, only the first k batches do, the others' decodes wait
+        until every encode is done (they then run beside each other, not beside an encoder)."""
+        self.early_decodes = early_decodes
         self.engines = list(engines) if isinstance(engines, (list, tuple)) else [engines]
         self.engine = self.engines[0]
         self.qsl, self.batch_size, self.batch_sizes = qsl, batch_size, batch_sizes
@@ -117,6 +121,7 @@ class OfflineSUT:
         self.completed = []  # per batch: (sample ids int64 [n], lengths int32 [n], tokens int32 [sum])
         self._streams = {}
         self._enc_locks = {}
+        self._hold = None
 
     def qsl_for(self, device):
         return self.qsl[device] if isinstance(self.qsl, dict) else self.qsl
@@ -136,6 +141,11 @@ class OfflineSUT:
         take = threading.Lock()
         errors = []
         self.batch_engine = [None] * len(batches)
+        k = self.early_decodes
+        hold = k is not None and k < len(batches) <= len(self.engines)
+        self._hold = None
+        if hold:  # the held batches wait until every batch of the query is encoded
+            self._hold = (k, threading.Semaphore(0), [0], threading.Lock(), len(batches))
         for eng in self.engines:
             if id(eng) not in self._streams:
                 self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
@@ -150,7 +160,7 @@ class OfflineSUT:
                     if i >= len(batches):
                         return
                     self.batch_engine[i] = self.engines.index(eng)
-                    self._run_batch(eng, *batches[i])
+                    self._run_batch(eng, *batches[i], bi=i)
             except Exception as ex:  # surfaced below: never leave the query half-complete silently
                 errors.append(ex)
 
@@ -165,7 +175,7 @@ class OfflineSUT:
         if errors:
             raise errors[0]
 
-    def _run_batch(self, eng, ids, idx):
+    def _run_batch(self, eng, ids, idx, bi=0):
         import torch
         st = self._streams[id(eng)]
         n = len(ids)
@@ -181,6 +191,15 @@ class OfflineSUT:
                 else:
                     eng.encode(inp["x"], inp["lens"], inp["lens_host"], n=n, stream=st)
                 st.synchronize()
+            if self._hold is not None:
+                k, sem, done, lk, nb = self._hold
+                with lk:
+                    done[0] += 1
+                    if done[0] == nb:  # last encode: release every held decode
+                        for _ in range(nb - k):
+                            sem.release()
+                if bi >= k:
+                    sem.acquire()
             eng.decode(res, rl, stream=st)
             rlh = rl.cpu().numpy()
             toks = res[:, : max(1, int(rlh.max()))].cpu().numpy()
