@@ -328,18 +328,19 @@ __global__ void __launch_bounds__(256) dec_reset_res_kernel(int32_t* __restrict_
 // workgroup is kept small (20-40 KB: in-kernel stamps showed 160-320 KB slices costing 12-20 us
 // per launch).  Grid: x = 20 gate groups, y = row groups striding over the emit list's tiles.
 constexpr int PRED_THREADS = 256;  // 4 waves, one gate tile each: 40 KB of weights per workgroup
-// rows per workgroup iteration of the step kernels (16: one MFMA row tile; 64 measured slower:
-// 148 vs 110 ms per query of greedy decode)
+// rows per workgroup iteration of the prediction / G kernels: 32 (two MFMA row tiles per weight
+// fragment) with 24 / 48 row groups -- isolated greedy 69.5 -> 66.7 ms per query vs 16 rows and
+// 48 / 96 groups (64 rows: 82 ms); the joint keeps 16-row tiles (JRT)
 #ifndef RNNT_DEC_RT
-#define RNNT_DEC_RT 16
+#define RNNT_DEC_RT 32
 #endif
 constexpr int DEC_RT = RNNT_DEC_RT;
 constexpr int DEC_SUB = DEC_RT / 16;
 #ifndef RNNT_PRED_RG
-#define RNNT_PRED_RG 48
+#define RNNT_PRED_RG 24
 #endif
 #ifndef RNNT_G_RG
-#define RNNT_G_RG 96
+#define RNNT_G_RG 48
 #endif
 #ifndef RNNT_JOINT_G
 #define RNNT_JOINT_G 512
@@ -550,7 +551,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
 }
 
 // joint (y1 = bf16(relu(F[t] + G)), logits = b2 + y1.W2^T) + argmax + greedy_decode_update
-// (decoder.py:137-167) for DEC_RT live-list rows per workgroup tile.  A blank (or a forced advance
+// (decoder.py:137-167) for JRT live-list rows per workgroup tile.  A blank (or a forced advance
 // after max_symbols_per_step) moves the row to its next frame with the SAME prediction, so the
 // workgroup evaluates up to RNNT_JOINT_ITERS frames per launch, stopping a row at its first
 // emission (it then needs a new prediction: next step's emit list) or at its last frame; rows
@@ -560,19 +561,19 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
 #define RNNT_JOINT_ITERS 2
 #endif
 constexpr int YP = J + 8;
-static_assert(DEC_RT == 16, "the joint's argmax maps 4 waves x 4 rows x 16 lanes onto one 16-row tile");
+constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 waves x 4 rows x 16 lanes onto it
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
-  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][YP];
-  __shared__ float Lp[4][DEC_RT][NLAB_PAD + 1];
-  __shared__ int rows[DEC_RT], walking[DEC_RT], tidx[DEC_RT], emit_e[DEC_RT], fin_f[DEC_RT];
+  __shared__ __attribute__((aligned(16))) uint16_t X[JRT][YP];
+  __shared__ float Lp[4][JRT][NLAB_PAD + 1];
+  __shared__ int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT], fin_f[JRT];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
   const int* llist = s.live + parity * a.Npad;
   int* nlist = s.live + (parity ^ 1) * a.Npad;
-  const int r_first = tid < DEC_RT ? llist[blockIdx.x * DEC_RT + tid] : 0;
+  const int r_first = tid < JRT ? llist[blockIdx.x * JRT + tid] : 0;
   const int lcnt = s.count[2 + parity];
-  const int ntiles = (lcnt + DEC_RT - 1) / DEC_RT;
+  const int ntiles = (lcnt + JRT - 1) / JRT;
   if ((int)blockIdx.x >= ntiles) return;
   // logits = ((s0 + s1) + s2) + s3, s_b = y1[128b : 128b+128] . W2^T (s0 from b2): wave w runs
   // label half w&1 over k blocks 2(w>>1) and 2(w>>1)+1 as two independent 4-instruction chains
@@ -592,8 +593,8 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     bias = v4f{b0.x, b0.y, b0.z, b0.w};
   }
   for (int rt = blockIdx.x; rt < ntiles; rt += gridDim.x) {
-    if (tid < DEC_RT) {
-      const int i = rt * DEC_RT + tid;
+    if (tid < JRT) {
+      const int i = rt * JRT + tid;
       const int r = i < lcnt ? (rt == (int)blockIdx.x ? r_first : llist[i]) : -1;
       rows[tid] = r;
       walking[tid] = r >= 0;
@@ -606,11 +607,11 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
 #endif
     for (int it = 0; it < RNNT_JOINT_ITERS; ++it) {
       bool any = false;
-      for (int m = 0; m < DEC_RT; ++m) any |= walking[m] != 0;
+      for (int m = 0; m < JRT; ++m) any |= walking[m] != 0;
       if (!any) break;
       // every load of the tile first (one memory round trip), then y1: rows not walking read a
       // safe cached address (row 0 of frame 0) and stage zeros
-      constexpr int NIT = DEC_RT * (J / 8) / 256;
+      constexpr int NIT = JRT * (J / 8) / 256;
       v4f fl4[NIT][2];
       float4 gl4[NIT][2];
       bool wk[NIT];
@@ -646,7 +647,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       __syncthreads();
       ST_SET(st2);
 #pragma unroll
-      for (int st = 0; st < DEC_SUB; ++st) {
+      for (int st = 0; st < 1; ++st) {
         if (!__any(walking[16 * st + c] != 0)) continue;
         const uint16_t* xr = &X[16 * st + c][8 * q];
         v4f s0 = bias, s1 = v4f{0.0f, 0.0f, 0.0f, 0.0f};
@@ -723,19 +724,19 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       // one atomic per tile and list: the tile's emitting rows go to the next emit list, its
       // finished rows leave the live-row counter
       if (wave == 0) {
-        const int e = lane < DEC_RT ? emit_e[lane] : -1;
+        const int e = lane < JRT ? emit_e[lane] : -1;
         const unsigned long long me = __ballot(e >= 0);
         int base = 0;
         if (lane == 0 && me) base = atomicAdd(&s.count[parity ^ 1], __popcll(me));
         base = __shfl(base, 0);
         if (e >= 0) s.list[(parity ^ 1) * a.Npad + base + __popcll(me & ((1ull << lane) - 1))] = e;
-        const unsigned long long mf = __ballot(lane < DEC_RT && fin_f[lane] != 0);
+        const unsigned long long mf = __ballot(lane < JRT && fin_f[lane] != 0);
         if (lane == 0 && mf) atomicSub(s.unfinished, __popcll(mf));
       }
       __syncthreads();
     }
     if (wave == 0) {  // the tile's unfinished rows -> next live list, one atomic
-      const int r = lane < DEC_RT ? rows[lane] : -1;
+      const int r = lane < JRT ? rows[lane] : -1;
       const unsigned long long mr = __ballot(r >= 0);
       int base = 0;
       if (lane == 0 && mr) base = atomicAdd(&s.count[2 + (parity ^ 1)], __popcll(mr));
@@ -773,7 +774,8 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int lt1 = lt > 0 ? lt : 1;
     const int rg_pred = lt1 < PRED_ROW_GROUPS ? lt1 : PRED_ROW_GROUPS;
     const int rg_g = lt1 < G_ROW_GROUPS ? lt1 : G_ROW_GROUPS;
-    const int rg_joint = lt1 < JOINT_GROUPS ? lt1 : JOINT_GROUPS;
+    const int ljt = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
+    const int rg_joint = ljt < JOINT_GROUPS ? ljt : JOINT_GROUPS;
     for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
       if (RNNT_PRED_WIDE_MIN > 0 && live_bound >= RNNT_PRED_WIDE_MIN) {
