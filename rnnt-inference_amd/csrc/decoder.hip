@@ -44,6 +44,12 @@ __device__ __forceinline__ int emit_entry(int row, int slot, int label) { return
 __device__ __forceinline__ int entry_row(int e) { return e & 0xffffff; }
 __device__ __forceinline__ int entry_slot(int e) { return (e >> 24) & 1; }
 __device__ __forceinline__ int entry_label(int e) { return (e >> 25) & 31; }
+// live-list entry: a row still decoding with the greedy state the joint reads and updates, so the
+// joint's update needs no dependent state loads (the DecState arrays are still written: they are
+// the state the op-level entry points, the stream calls and dec_finish read)
+__device__ __forceinline__ int4 live_entry(int row, int slot, int added, int time, int flen, int idx) {
+  return int4{row | (slot << 24) | (added << 25), time | (flen << 16), idx, 0};
+}
 
 // development instrumentation (-DRNNT_DEV_STAMPS, tools/build_variants.sh stamps): thread 0 of
 // each working workgroup of the step kernels records s_memrealtime (100 MHz) at kernel start,
@@ -280,7 +286,7 @@ __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
   for (int k = 0; k < 4 * P; ++k) h[k] = 0.0f;  // committed state starts at zero (metadata.cpp:25-30)
   if (fl > 0) {
     s.list[atomicAdd(&s.count[0], 1)] = emit_entry(row, 0, 28);  // every live row needs its first (SOS) prediction
-    s.live[atomicAdd(&s.count[2], 1)] = row;
+    s.live[atomicAdd(&s.count[2], 1)] = live_entry(row, 0, 0, 0, fl, -1);
     atomicAdd(s.unfinished, 1);
   }
 }
@@ -307,7 +313,7 @@ __global__ void __launch_bounds__(256) dec_init_stream_kernel(DecArgs a, const i
   if (fl > 0) {
     const int pg = s.preg[row];
     s.list[atomicAdd(&s.count[0], 1)] = emit_entry(row, s.slot[row], pg < 0 ? 28 : pg);
-    s.live[atomicAdd(&s.count[2], 1)] = row;
+    s.live[atomicAdd(&s.count[2], 1)] = live_entry(row, s.slot[row], 0, 0, fl, s.idx[row]);
     atomicAdd(s.unfinished, 1);
   }
 }
@@ -560,18 +566,20 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
 #ifndef RNNT_JOINT_ITERS
 #define RNNT_JOINT_ITERS 2
 #endif
+
 constexpr int YP = J + 8;
 constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 waves x 4 rows x 16 lanes onto it
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[JRT][YP];
   __shared__ float Lp[4][JRT][NLAB_PAD + 1];
   __shared__ int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT], fin_f[JRT];
+  __shared__ int slot_[JRT], add_[JRT], flen_[JRT], idx_[JRT];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
-  const int* llist = s.live + parity * a.Npad;
-  int* nlist = s.live + (parity ^ 1) * a.Npad;
-  const int r_first = tid < JRT ? llist[blockIdx.x * JRT + tid] : 0;
+  const int4* llist = s.live + parity * a.Npad;
+  int4* nlist = s.live + (parity ^ 1) * a.Npad;
+  const int4 r_first = tid < JRT ? llist[blockIdx.x * JRT + tid] : int4{0, 0, 0, 0};
   const int lcnt = s.count[2 + parity];
   const int ntiles = (lcnt + JRT - 1) / JRT;
   if ((int)blockIdx.x >= ntiles) return;
@@ -595,25 +603,31 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   for (int rt = blockIdx.x; rt < ntiles; rt += gridDim.x) {
     if (tid < JRT) {
       const int i = rt * JRT + tid;
-      const int r = i < lcnt ? (rt == (int)blockIdx.x ? r_first : llist[i]) : -1;
+      const int4 e = i < lcnt ? (rt == (int)blockIdx.x ? r_first : llist[i]) : int4{-1, 0, 0, 0};
+      const int r = e.x < 0 ? -1 : e.x & 0xffffff;
       rows[tid] = r;
       walking[tid] = r >= 0;
-      tidx[tid] = r >= 0 ? s.time[r] : 0;
+      slot_[tid] = (e.x >> 24) & 1;
+      add_[tid] = (e.x >> 25) & 31;
+      tidx[tid] = e.y & 0xffff;
+      flen_[tid] = (e.y >> 16) & 0xffff;
+      idx_[tid] = e.z;
     }
     __syncthreads();
     ST_MARK(st1);
 #ifdef RNNT_DEV_STAMPS
     unsigned long long st2 = 0ull;
 #endif
+    constexpr int NIT = JRT * (J / 8) / 256;
+    float4 gl4[NIT][2];
     for (int it = 0; it < RNNT_JOINT_ITERS; ++it) {
       bool any = false;
       for (int m = 0; m < JRT; ++m) any |= walking[m] != 0;
       if (!any) break;
       // every load of the tile first (one memory round trip), then y1: rows not walking read a
-      // safe cached address (row 0 of frame 0) and stage zeros
-      constexpr int NIT = JRT * (J / 8) / 256;
+      // safe cached address (row 0 of frame 0) and stage zeros.  G is the same for every frame
+      // of the walk (blank keeps the prediction).
       v4f fl4[NIT][2];
-      float4 gl4[NIT][2];
       bool wk[NIT];
 #pragma unroll
       for (int u = 0; u < NIT; ++u) {
@@ -621,11 +635,13 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
         wk[u] = walking[m] != 0;
         const int row = wk[u] ? rows[m] : 0, tm = wk[u] ? tidx[m] : 0;
         const float* fr = a.F + ((size_t)tm * a.Npad + row) * J + k;
-        const float* gr = a.G + (size_t)row * J + k;
         fl4[u][0] = __builtin_nontemporal_load((const v4f*)fr);  // streamed once
         fl4[u][1] = __builtin_nontemporal_load((const v4f*)(fr + 4));
-        gl4[u][0] = *(const float4*)gr;
-        gl4[u][1] = *(const float4*)(gr + 4);
+        if (it == 0) {
+          const float* gr = a.G + (size_t)row * J + k;
+          gl4[u][0] = *(const float4*)gr;
+          gl4[u][1] = *(const float4*)(gr + 4);
+        }
       }
 #pragma unroll
       for (int u = 0; u < NIT; ++u) {
@@ -694,17 +710,20 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           fin_f[m] = 0;
           if (walking[m]) {
             const int row = rows[m], best = bl;
-            if (best != BLANK && s.added[row] != MAXSYM) {
-              const int id = ++s.idx[row];
+            if (best != BLANK && add_[m] != MAXSYM) {
+              const int id = idx_[m] + 1;
+              idx_[m] = id;
+              s.idx[row] = id;
               if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
-              s.added[row]++;
+              s.added[row] = ++add_[m];
               s.preg[row] = best;
-              const int nsl = s.slot[row] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+              const int nsl = slot_[m] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+              slot_[m] = nsl;
               s.slot[row] = nsl;
               emit_e[m] = emit_entry(row, nsl, best);
               walking[m] = 0;
             } else {
-              const int fl = a.f_lens[row];
+              const int fl = flen_[m];
               int t = tidx[m] + 1;
               if (t >= fl) {
                 s.fin[row] = 1;
@@ -716,6 +735,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
               tidx[m] = t;
               s.time[row] = t;
               s.added[row] = 0;
+              add_[m] = 0;
             }
           }
         }
@@ -741,7 +761,9 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       int base = 0;
       if (lane == 0 && mr) base = atomicAdd(&s.count[2 + (parity ^ 1)], __popcll(mr));
       base = __shfl(base, 0);
-      if (r >= 0) nlist[base + __popcll(mr & ((1ull << lane) - 1))] = r;
+      if (r >= 0)
+        nlist[base + __popcll(mr & ((1ull << lane) - 1))] =
+            live_entry(r, slot_[lane], add_[lane], tidx[lane], flen_[lane], idx_[lane]);
     }
     __syncthreads();  // rows / walking / tidx / X are reused by the next row tile
     ST_FLUSH(3, st0, st1, st2, 0ull);

@@ -23,7 +23,8 @@ struct DecWeights {
 struct DecState {           // per-row greedy state, device arrays [Npad]
   int32_t *time, *added, *idx, *preg, *slot, *fin;
   int32_t* list;             // [2][Npad] emit lists (by step parity): row | slot << 24 | label index << 25
-  int32_t* live;             // [2][Npad] unfinished rows (by step parity)
+  int4* live;                // [2][Npad] unfinished rows (by step parity) with their greedy state:
+                             // {row | slot << 24 | symbols_added << 25, time | f_len << 16, idx, 0}
   int32_t* count;            // [4] list lengths: emit lists 0/1, live lists 2/3
   int32_t* unfinished;       // [4] live-row counter (1 used)
 };

@@ -310,7 +310,7 @@ static int alloc_workspace(rnnt_engine* e) {
   int32_t** ints[] = {&e->ds.time, &e->ds.added, &e->ds.idx, &e->ds.preg, &e->ds.slot, &e->ds.fin};
   for (auto pp : ints) r = r ? r : dev_alloc(e, pp, NP);
   r = r ? r : dev_alloc(e, &e->ds.list, 2 * NP);
-  r = r ? r : dev_alloc(e, &e->ds.live, 2 * NP);
+  r = r ? r : dev_alloc(e, &e->ds.live, 2 * NP);  // int4 entries
   r = r ? r : dev_alloc(e, &e->ds.count, 4);
   r = r ? r : dev_alloc(e, &e->ds.unfinished, 4);
   if (!r && hipHostMalloc((void**)&e->host_flags, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
@@ -355,8 +355,10 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   e->np_max = (e->opts.max_batch + ENC_PAD - 1) / ENC_PAD * ENC_PAD;
   e->tp_max = (e->opts.max_frames + 1) / 2;
   int r = 0;
+  // decode live-list entries hold the row in 24 bits and the frame / f_len in 16 bits each
+  if (e->np_max >= (1 << 24) || e->tp_max > 0xffff) r = fail(RNNT_EINVAL, "max_batch or max_frames too large");
   DeviceScope dscope(device);
-  if (!dscope.ok) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
+  if (!r && !dscope.ok) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
   if (!r && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
   if (!r && model) r = pack_model(e, model);

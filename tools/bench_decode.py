@@ -14,22 +14,26 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from rnnt_amd import weights  # noqa: E402
-from rnnt_amd.engine import Engine  # noqa: E402
+from rnnt_amd import dist, weights  # noqa: E402
+from rnnt_amd.engine import Engine, pad_batch  # noqa: E402
+from rnnt_amd.sut import make_batches  # noqa: E402
 
 
 def main():
     torch.cuda.set_device(0)
     pm, _ = weights.build_model()
-    qsl = bench.build_qsl(2513, seed=4)
-    batches = bench.make_batches(qsl, 24576, 8192)
+    qsl = bench.build_qsl(2513, seed=4, device="cuda:0")
+    ids, idx = dist.query_arrays(2513, 24576)
+    batches = make_batches(qsl, ids, idx, 8192)
     eng = Engine(pm, device=0, max_batch=8192, max_frames=500)
     out = {"lib": os.path.basename(os.environ.get("RNNT_MI355X_LIB", "default"))}
     tot = 0.0
-    for i, b in enumerate(batches):
-        res = torch.empty((b["n"], eng.max_res), dtype=torch.int32, device="cuda")
-        rl = torch.empty(b["n"], dtype=torch.int32, device="cuda")
-        eng.encode(b["x"], b["lens"], b["lens_host"], n=b["n"])
+    for i, (bids, bidx) in enumerate(batches):
+        n = len(bids)
+        b = qsl.batch_inputs(bidx, pad_batch(n), torch.device("cuda", 0))
+        res = torch.empty((n, eng.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(n, dtype=torch.int32, device="cuda")
+        eng.encode_gather(b["store"], b["offsets"], b["lens"], b["lens_host"], b["T"], n, pad_batch(n))
         eng.decode(res, rl)
         torch.cuda.synchronize()
         eng.stats(reset=True)

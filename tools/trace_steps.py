@@ -20,7 +20,7 @@ def main():
     rows.sort()
     steps, cur = [], None
     for s, e, n in rows:
-        if n.startswith("dec_pred_kernel<0>"):
+        if n.startswith("dec_pred_kernel<0"):
             cur = {"start": s, "k": {}}
             steps.append(cur)
         if cur is not None and n.startswith(("dec_pred", "dec_g", "dec_joint")):
