@@ -368,18 +368,21 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
   constexpr int XP = KX + 8;             // bf16 pitch: +16 B per row (conflict-free b128 reads)
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][XP];
-  __shared__ int ents[DEC_RT];
+  constexpr int NK = PRED_THREADS / DEC_RT;  // row tiles whose list entries load up front
+  __shared__ int ents_all[NK][DEC_RT];
   const DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
   const GridXY gxy = xcd_grid(PG4 / (16 * (PRED_THREADS / 64)));
   const int* list = s.list + parity * a.Npad;
-  // the first tile's entries load beside the list length (row groups never exceed Npad/DEC_RT
-  // tiles... except the XCD rounding: guarded)
-  const int e_first = (tid < DEC_RT && gxy.y * DEC_RT < a.Npad) ? list[gxy.y * DEC_RT + tid] : 0;
+  // the entries of this workgroup's first NK row tiles load beside the list length (one round
+  // trip for all of them; indices past Npad -- XCD rounding, long strides -- are guarded)
+  const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
+  const int e0 = i0 < a.Npad ? list[i0] : -1;
   const int cnt = s.count[parity];
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
+  ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
   const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
   uint4 wh[NT][P / 32], wx[NT][LAYER ? P / 32 : 1];
   float4 bh[NT], bx[NT];
@@ -395,22 +398,25 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     }
     bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
   }
-  for (int rt = gxy.y; rt < ntiles; rt += gxy.ny) {
-    if (tid < DEC_RT) {
-      const int e = rt == gxy.y ? e_first : list[rt * DEC_RT + tid];
-      ents[tid] = rt * DEC_RT + tid < cnt ? e : -1;
-    }
+  for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
+    int* ents = ents_all[it % NK];
+    if (it >= NK && tid < DEC_RT)  // past the prefetched tiles (the slot's tile is done)
+      ents[tid] = rt * DEC_RT + tid < cnt ? list[rt * DEC_RT + tid] : -1;
     __syncthreads();
     ST_MARK(st1);
-    // this lane's committed cell states (sub-tile st: row ents[16 st + c]), fetched beside the
-    // input staging
+    // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and, layer 0, its
+    // label-table input halves, fetched beside the input staging
     float cp[DEC_SUB][NT];
+    float4 xt[DEC_SUB][NT];
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ents[16 * st + c];
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt)
+      for (int tt = 0; tt < NT; ++tt) {
         cp[st][tt] = ec >= 0 ? hc_part(a.hc, entry_row(ec), entry_slot(ec), 2 + LAYER)[(t0 + tt) * 4 + q] : 0.0f;
+        if (!LAYER)
+          xt[st][tt] = *(const float4*)(a.w.xtab + (size_t)(ec >= 0 ? entry_label(ec) : 28) * PG4 + (t0 + tt) * 16 + 4 * q);
+      }
     }
     // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1
     // [h0 of the candidate slot | h1 committed]
@@ -444,7 +450,6 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       const int ec = ents[16 * st + c];
       if (!__any(ec >= 0)) continue;  // wave-uniform: the whole sub-tile is past the list end
       const int row = ec >= 0 ? entry_row(ec) : -1, sl = ec >= 0 ? entry_slot(ec) : 0;
-      const int lab = ec >= 0 ? entry_label(ec) : 28;
       const uint16_t* xr = &X[16 * st + c][8 * q];
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
@@ -457,8 +462,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
 #pragma unroll
           for (int b = 0; b < P / 32; ++b) ax = mfma_bf16(wx[tt][b], *(const uint4*)(xr + 32 * b), ax);
         } else {
-          const float4 xt = *(const float4*)(a.w.xtab + (size_t)lab * PG4 + (t0 + tt) * 16 + 4 * q);
-          ax = v4f{xt.x, xt.y, xt.z, xt.w};
+          ax = v4f{xt[st][tt].x, xt[st][tt].y, xt[st][tt].z, xt[st][tt].w};
         }
         if (row >= 0) {
           const v4f gs = ax + ah;
@@ -471,7 +475,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
         }
       }
     }
-    __syncthreads();  // X / ents are restaged by the next tile
+    __syncthreads();  // X (and this entry slot, NK tiles on) are restaged by the next tile
     ST_FLUSH(LAYER, st0, st1, st2, 0ull);
   }
 }
@@ -484,7 +488,8 @@ constexpr int GXP = P + 8;
 constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each; grid x = 8 column groups
 __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
-  __shared__ int ents[DEC_RT];
+  constexpr int NK = G_THREADS / DEC_RT;  // row tiles whose list entries load up front
+  __shared__ int ents_all[NK][DEC_RT];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
@@ -494,10 +499,12 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     s.count[2 + (parity ^ 1)] = 0;
   }
   const int* list = s.list + parity * a.Npad;
-  const int e_first = (tid < DEC_RT && gxy.y * DEC_RT < a.Npad) ? list[gxy.y * DEC_RT + tid] : 0;
+  const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
+  const int e0 = i0 < a.Npad ? list[i0] : -1;
   const int cnt = s.count[parity];
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
+  ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
   constexpr int NJ = 1;  // column tiles per wave
   uint4 wv[NJ][P / 32];
   float4 b0[NJ];
@@ -509,11 +516,9 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
     b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
   }
-  for (int rt = gxy.y; rt < ntiles; rt += gxy.ny) {
-    if (tid < DEC_RT) {
-      const int e = rt == gxy.y ? e_first : list[rt * DEC_RT + tid];
-      ents[tid] = rt * DEC_RT + tid < cnt ? e : -1;
-    }
+  for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
+    int* ents = ents_all[it % NK];
+    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt ? list[rt * DEC_RT + tid] : -1;
     __syncthreads();
     ST_MARK(st1);
     constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;

@@ -27,7 +27,7 @@ def main():
     batches, cur = [], {}
     buckets = (256, 512, 1024, 1 << 30)
     for s, e, n, q, g in rows:
-        if n.startswith("quantize_kernel"):
+        if n.startswith("quantize"):
             b = {"q": q, "enc": [s, e], "dec": None, "ticks": 0, "hist": [[0, 0.0] for _ in buckets]}
             batches.append(b)
             cur[q] = b
