@@ -44,6 +44,10 @@ __device__ __forceinline__ int emit_entry(int row, int slot, int label) { return
 __device__ __forceinline__ int entry_row(int e) { return e & 0xffffff; }
 __device__ __forceinline__ int entry_slot(int e) { return (e >> 24) & 1; }
 __device__ __forceinline__ int entry_label(int e) { return (e >> 25) & 31; }
+// list counters: DecState::count = {emit p0, live p0, emit p1, live p1} -- one parity's two
+// counters adjacent, so the joint appends to both with one 64-bit atomic
+__host__ __device__ constexpr int EMIT_N(int p) { return 2 * p; }
+__host__ __device__ constexpr int LIVE_N(int p) { return 2 * p + 1; }
 // live-list entry: a row still decoding with the greedy state the joint reads and updates, so the
 // joint's update needs no dependent state loads (the DecState arrays are still written: they are
 // the state the op-level entry points, the stream calls and dec_finish read)
@@ -285,9 +289,8 @@ __global__ void __launch_bounds__(256) dec_init_kernel(DecArgs a) {
   float* h = hc_part(a.hc, row, 0, 0);
   for (int k = 0; k < 4 * P; ++k) h[k] = 0.0f;  // committed state starts at zero (metadata.cpp:25-30)
   if (fl > 0) {
-    s.list[atomicAdd(&s.count[0], 1)] = emit_entry(row, 0, 28);  // every live row needs its first (SOS) prediction
-    s.live[atomicAdd(&s.count[2], 1)] = live_entry(row, 0, 0, 0, fl, -1);
-    atomicAdd(s.unfinished, 1);
+    s.list[atomicAdd(&s.count[EMIT_N(0)], 1)] = emit_entry(row, 0, 28);  // every live row needs its first (SOS) prediction
+    s.live[atomicAdd(&s.count[LIVE_N(0)], 1)] = live_entry(row, 0, 0, 0, fl, -1);
   }
 }
 
@@ -312,9 +315,8 @@ __global__ void __launch_bounds__(256) dec_init_stream_kernel(DecArgs a, const i
   s.fin[row] = fl <= 0;
   if (fl > 0) {
     const int pg = s.preg[row];
-    s.list[atomicAdd(&s.count[0], 1)] = emit_entry(row, s.slot[row], pg < 0 ? 28 : pg);
-    s.live[atomicAdd(&s.count[2], 1)] = live_entry(row, s.slot[row], 0, 0, fl, s.idx[row]);
-    atomicAdd(s.unfinished, 1);
+    s.list[atomicAdd(&s.count[EMIT_N(0)], 1)] = emit_entry(row, s.slot[row], pg < 0 ? 28 : pg);
+    s.live[atomicAdd(&s.count[LIVE_N(0)], 1)] = live_entry(row, s.slot[row], 0, 0, fl, s.idx[row]);
   }
 }
 
@@ -379,7 +381,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   // trip for all of them; indices past Npad -- XCD rounding, long strides -- are guarded)
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
   const int e0 = i0 < a.Npad ? list[i0] : -1;
-  const int cnt = s.count[parity];
+  const int cnt = s.count[EMIT_N(parity)];
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
@@ -495,13 +497,13 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   ST_MARK(st0);
   const GridXY gxy = xcd_grid(J / (16 * (G_THREADS / 64)));
   if (blockIdx.x == 0 && tid == 0) {
-    s.count[parity ^ 1] = 0;
-    s.count[2 + (parity ^ 1)] = 0;
+    s.count[EMIT_N(parity ^ 1)] = 0;
+    s.count[LIVE_N(parity ^ 1)] = 0;
   }
   const int* list = s.list + parity * a.Npad;
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
   const int e0 = i0 < a.Npad ? list[i0] : -1;
-  const int cnt = s.count[parity];
+  const int cnt = s.count[EMIT_N(parity)];
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
@@ -577,7 +579,7 @@ constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 wav
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[JRT][YP];
   __shared__ float Lp[4][JRT][NLAB_PAD + 1];
-  __shared__ int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT], fin_f[JRT];
+  __shared__ int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT];
   __shared__ int slot_[JRT], add_[JRT], flen_[JRT], idx_[JRT];
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
@@ -585,7 +587,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   const int4* llist = s.live + parity * a.Npad;
   int4* nlist = s.live + (parity ^ 1) * a.Npad;
   const int4 r_first = tid < JRT ? llist[blockIdx.x * JRT + tid] : int4{0, 0, 0, 0};
-  const int lcnt = s.count[2 + parity];
+  const int lcnt = s.count[LIVE_N(parity)];
   const int ntiles = (lcnt + JRT - 1) / JRT;
   if ((int)blockIdx.x >= ntiles) return;
   // logits = ((s0 + s1) + s2) + s3, s_b = y1[128b : 128b+128] . W2^T (s0 from b2): wave w runs
@@ -612,6 +614,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       const int r = e.x < 0 ? -1 : e.x & 0xffffff;
       rows[tid] = r;
       walking[tid] = r >= 0;
+      emit_e[tid] = -1;
       slot_[tid] = (e.x >> 24) & 1;
       add_[tid] = (e.x >> 25) & 31;
       tidx[tid] = e.y & 0xffff;
@@ -711,8 +714,6 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           }
         }
         if ((lane & 15) == 0) {
-          emit_e[m] = -1;
-          fin_f[m] = 0;
           if (walking[m]) {
             const int row = rows[m], best = bl;
             if (best != BLANK && add_[m] != MAXSYM) {
@@ -732,7 +733,6 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
               int t = tidx[m] + 1;
               if (t >= fl) {
                 s.fin[row] = 1;
-                fin_f[m] = 1;
                 walking[m] = 0;
                 rows[m] = -1;  // finished: not in the next live list
                 t = fl - 1;
@@ -746,28 +746,22 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
         }
       }
       __syncthreads();
-      // one atomic per tile and list: the tile's emitting rows go to the next emit list, its
-      // finished rows leave the live-row counter
-      if (wave == 0) {
-        const int e = lane < JRT ? emit_e[lane] : -1;
-        const unsigned long long me = __ballot(e >= 0);
-        int base = 0;
-        if (lane == 0 && me) base = atomicAdd(&s.count[parity ^ 1], __popcll(me));
-        base = __shfl(base, 0);
-        if (e >= 0) s.list[(parity ^ 1) * a.Npad + base + __popcll(me & ((1ull << lane) - 1))] = e;
-        const unsigned long long mf = __ballot(lane < JRT && fin_f[lane] != 0);
-        if (lane == 0 && mf) atomicSub(s.unfinished, __popcll(mf));
-      }
-      __syncthreads();
     }
-    if (wave == 0) {  // the tile's unfinished rows -> next live list, one atomic
+    // the tile's emitting rows -> next emit list, its unfinished rows -> next live list: ONE
+    // 64-bit atomic on the adjacent (emit, live) counters of the next parity returns both bases
+    if (wave == 0) {
+      const int e = lane < JRT ? emit_e[lane] : -1;
       const int r = lane < JRT ? rows[lane] : -1;
-      const unsigned long long mr = __ballot(r >= 0);
-      int base = 0;
-      if (lane == 0 && mr) base = atomicAdd(&s.count[2 + (parity ^ 1)], __popcll(mr));
+      const unsigned long long me = __ballot(e >= 0), mr = __ballot(r >= 0);
+      unsigned long long base = 0;
+      if (lane == 0 && (me | mr))
+        base = atomicAdd((unsigned long long*)&s.count[EMIT_N(parity ^ 1)],
+                         (unsigned long long)__popcll(me) | ((unsigned long long)__popcll(mr) << 32));
       base = __shfl(base, 0);
+      const unsigned long long below = (1ull << lane) - 1;
+      if (e >= 0) s.list[(parity ^ 1) * a.Npad + (int)(base & 0xffffffffu) + __popcll(me & below)] = e;
       if (r >= 0)
-        nlist[base + __popcll(mr & ((1ull << lane) - 1))] =
+        nlist[(int)(base >> 32) + __popcll(mr & below)] =
             live_entry(r, slot_[lane], add_[lane], tidx[lane], flen_[lane], idx_[lane]);
     }
     __syncthreads();  // rows / walking / tidx / X are reused by the next row tile
@@ -783,7 +777,6 @@ __global__ void dec_finish_kernel(DecArgs a) {
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st, const int32_t* reset) {
   const int rt = a.Npad / DEC_RT;
   if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
-  if (hipMemsetAsync(a.s.unfinished, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (reset) {
     hipLaunchKernelGGL(dec_reset_res_kernel, dim3(a.N), dim3(256), 0, st, a.res, a.max_res, reset);
     hipLaunchKernelGGL(dec_init_stream_kernel, dim3((a.Npad + 255) / 256), dim3(256), 0, st, a, reset);
@@ -818,9 +811,11 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
                          p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
     }
-    // poll the live-row counter one chunk behind, so the host never drains the queue
-    if (hipMemcpyAsync(host_flags + (chunk & 1), a.s.unfinished, sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
-        hipSuccess)
+    // poll the live-row count one chunk behind, so the host never drains the queue: the length of
+    // the live list the chunk's last joint wrote (parity step & 1; the next step's G kernel resets
+    // the other parity's counters)
+    if (hipMemcpyAsync(host_flags + (chunk & 1), a.s.count + LIVE_N(step & 1), sizeof(int32_t), hipMemcpyDeviceToHost,
+                       st) != hipSuccess)
       return -1;
     if (hipEventRecord(evs[chunk & 1], st) != hipSuccess) return -1;
     if (chunk > 0) {

@@ -25,8 +25,8 @@ struct DecState {           // per-row greedy state, device arrays [Npad]
   int32_t* list;             // [2][Npad] emit lists (by step parity): row | slot << 24 | label index << 25
   int4* live;                // [2][Npad] unfinished rows (by step parity) with their greedy state:
                              // {row | slot << 24 | symbols_added << 25, time | f_len << 16, idx, 0}
-  int32_t* count;            // [4] list lengths: emit lists 0/1, live lists 2/3
-  int32_t* unfinished;       // [4] live-row counter (1 used)
+  int32_t* count;            // [4] list lengths {emit p0, live p0, emit p1, live p1} (8-byte aligned)
+  int32_t* unfinished;       // [4] live-row counter (the fp32 decode loop)
 };
 
 struct DecArgs {
