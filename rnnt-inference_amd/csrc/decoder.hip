@@ -426,11 +426,17 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     // 0 (a safe cached address) and stage zeros
     constexpr int NX = DEC_RT * (KX / 8), NIT = (NX + PRED_THREADS - 1) / PRED_THREADS;
     uint4 xv[NIT];
+    int emv[NIT];
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {  // this thread's entries first: one LDS round trip, not one per load
+      const int i = tid + PRED_THREADS * u;
+      emv[u] = (NX % PRED_THREADS == 0 || i < NX) ? ents[i / (KX / 8)] : -1;
+    }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int i = tid + PRED_THREADS * u;
       if (NX % PRED_THREADS == 0 || i < NX) {
-        const int m = i / (KX / 8), k = (i % (KX / 8)) * 8, em = ents[m];
+        const int k = (i % (KX / 8)) * 8, em = emv[u];
         const int r = em >= 0 ? entry_row(em) : 0, smm = em >= 0 ? entry_slot(em) : 0;
         const uint16_t* src = LAYER == 0 ? h_bf(a.hc, r, smm, 0) + k
                                          : (k < P ? h_bf(a.hc, r, smm ^ 1, 0) + k : h_bf(a.hc, r, smm, 1) + k - P);
@@ -442,30 +448,40 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       const int i = tid + PRED_THREADS * u;
       if (NX % PRED_THREADS == 0 || i < NX) {
         const int m = i / (KX / 8), k = (i % (KX / 8)) * 8;
-        *(uint4*)&X[m][k] = ents[m] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
+        *(uint4*)&X[m][k] = emv[u] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
       }
     }
     __syncthreads();
     ST_MARK(st2);
+    // the chains of every sub-tile (h, and x on layer 1) advance together, one k block at a
+    // time, so each block's fragment reads overlap the previous block's MFMAs (sub-tiles past the
+    // list end run on the staged zeros; their results are not stored).  Each chain is still the
+    // contract's natural-k sequence from its bias.
+    static_assert(NT == 1, "one gate tile per wave");
+    int ecs[DEC_SUB];
+    v4f ahs[DEC_SUB], axs[DEC_SUB];
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
-      const int ec = ents[16 * st + c];
-      if (!__any(ec >= 0)) continue;  // wave-uniform: the whole sub-tile is past the list end
+      ecs[st] = ents[16 * st + c];
+      ahs[st] = v4f{bh[0].x, bh[0].y, bh[0].z, bh[0].w};
+      axs[st] = LAYER ? v4f{bx[0].x, bx[0].y, bx[0].z, bx[0].w} : v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
+    }
+#pragma unroll
+    for (int b = 0; b < P / 32; ++b) {
+#pragma unroll
+      for (int st = 0; st < DEC_SUB; ++st) {
+        const uint16_t* xr = &X[16 * st + c][8 * q];
+        ahs[st] = mfma_bf16(wh[0][b], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ahs[st]);
+        if (LAYER) axs[st] = mfma_bf16(wx[0][LAYER ? b : 0], *(const uint4*)(xr + 32 * b), axs[st]);
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < DEC_SUB; ++st) {
+      const int ec = ecs[st];
       const int row = ec >= 0 ? entry_row(ec) : -1, sl = ec >= 0 ? entry_slot(ec) : 0;
-      const uint16_t* xr = &X[16 * st + c][8 * q];
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
-        v4f ah = v4f{bh[tt].x, bh[tt].y, bh[tt].z, bh[tt].w};
-#pragma unroll
-        for (int b = 0; b < P / 32; ++b) ah = mfma_bf16(wh[tt][b], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ah);
-        v4f ax;
-        if (LAYER) {
-          ax = v4f{bx[tt].x, bx[tt].y, bx[tt].z, bx[tt].w};
-#pragma unroll
-          for (int b = 0; b < P / 32; ++b) ax = mfma_bf16(wx[tt][b], *(const uint4*)(xr + 32 * b), ax);
-        } else {
-          ax = v4f{xt[st][tt].x, xt[st][tt].y, xt[st][tt].z, xt[st][tt].w};
-        }
+        const v4f ah = ahs[st], ax = axs[st];
         if (row >= 0) {
           const v4f gs = ax + ah;
           const int u = (t0 + tt) * 4 + q;
@@ -525,11 +541,17 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     ST_MARK(st1);
     constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
     uint4 xv[NIT];
+    int emv[NIT];
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {  // this thread's entries first (one LDS round trip)
+      const int i = tid + G_THREADS * u;
+      emv[u] = (NX % G_THREADS == 0 || i < NX) ? ents[i / (P / 8)] : -1;
+    }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {  // every load first (one round trip); past the list end: row 0, zeros staged
       const int i = tid + G_THREADS * u;
       if (NX % G_THREADS == 0 || i < NX) {
-        const int m = i / (P / 8), k = (i % (P / 8)) * 8, em = ents[m];
+        const int k = (i % (P / 8)) * 8, em = emv[u];
         xv[u] = *(const uint4*)(h_bf(a.hc, em >= 0 ? entry_row(em) : 0, em >= 0 ? entry_slot(em) ^ 1 : 0, 1) + k);
       }
     }
@@ -538,25 +560,28 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       const int i = tid + G_THREADS * u;
       if (NX % G_THREADS == 0 || i < NX) {
         const int m = i / (P / 8), k = (i % (P / 8)) * 8;
-        *(uint4*)&X[m][k] = ents[m] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
+        *(uint4*)&X[m][k] = emv[u] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
       }
     }
     __syncthreads();
     ST_MARK(st2);
+    // every sub-tile's chain advances one k block at a time (fragment reads overlap MFMAs)
+    static_assert(NJ == 1, "one column tile per wave");
+    v4f accs[DEC_SUB];
+#pragma unroll
+    for (int st = 0; st < DEC_SUB; ++st) accs[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
+#pragma unroll
+    for (int b = 0; b < P / 32; ++b)
+#pragma unroll
+      for (int st = 0; st < DEC_SUB; ++st)
+        accs[st] = mfma_bf16(wv[0][b], *(const uint4*)(&X[16 * st + c][8 * q] + 32 * b), accs[st]);
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ents[16 * st + c];
-      if (!__any(ec >= 0)) continue;
-      const uint16_t* xr = &X[16 * st + c][8 * q];
-#pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) {
-        v4f acc = v4f{b0[jj].x, b0[jj].y, b0[jj].z, b0[jj].w};
-#pragma unroll
-        for (int b = 0; b < P / 32; ++b) acc = mfma_bf16(wv[jj][b], *(const uint4*)(xr + 32 * b), acc);
-        const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
-        if (ec >= 0)
-          *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
-      }
+      const v4f acc = accs[st];
+      const int jt = gxy.x * (G_THREADS / 64) + wave;
+      if (ec >= 0)
+        *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
     }
     __syncthreads();
     ST_FLUSH(2, st0, st1, st2, 0ull);
