@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=3,
                     help="engines per GPU (one HIP stream + host thread each): one batch's latency-bound greedy "
                          "decode overlaps the next batch's encoder")
+    ap.add_argument("--batch-sizes", default=None,
+                    help="comma-separated batch sizes over the sorted query (the last repeats); default: --batch")
     ap.add_argument("--early-decodes", type=int, default=None,
                     help="only the first K batches decode beside the next encoder; the others wait for every encode "
                          "(default: all decode right after their encode)")
@@ -193,12 +195,14 @@ def main():
     qsl = build_qsl(args.qsl, seed=4, device=device, wav=args.wav)
     query = args.query * world
     ids, idx = dist.query_arrays(args.qsl, query)
-    engines = [Engine(pm, device=local, max_batch=min(args.batch, query), max_frames=500) for _ in range(args.inflight)]
+    max_b = max([args.batch] + ([int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else []))
+    engines = [Engine(pm, device=local, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
     sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
+    sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None
 
     def step():
         """One Offline query: sort + batch + deal, this rank's share through the SUT, gather."""
-        mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world)
+        mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world, sizes)
         sut.issue_batches(mine)
         local = sut.take_completed()
         got = dist.gather_responses(*local, world, ggroup)
@@ -282,7 +286,7 @@ def main():
                  else "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)"),
         "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
                    "qsl": args.qsl, "query_samples": query, "query_samples_per_gpu": args.query,
-                   "batch_size": args.batch, "batches_in_flight_per_gpu": args.inflight,
+                   "batch_size": args.batch, "batch_sizes": sizes, "batches_in_flight_per_gpu": args.inflight,
                    "input": ("16 kHz audio: GPU featurizer (FilterbankFeatures.forward) in the timed region" if args.wav
                              else "log-mel features resident in HBM, gathered by the encoder's quantize pass"),
                    "encoder": "int8 (lstm_amx_int8)",

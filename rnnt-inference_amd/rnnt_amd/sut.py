@@ -17,6 +17,7 @@ Multi-process (one process per GPU, bench.py / rnnt_amd.dist): every rank sorts 
 ``dist.shard_query`` deals the batches to ranks (snake order), each rank runs its share through
 its OfflineSUT, and the responses are gathered to rank 0's host (``dist.gather_responses``).
 """
+import collections
 import threading
 from dataclasses import dataclass
 
@@ -120,7 +121,7 @@ class OfflineSUT:
         self._done_lock = threading.Lock()
         self.completed = []  # per batch: (sample ids int64 [n], lengths int32 [n], tokens int32 [sum])
         self._streams = {}
-        self._enc_locks = {}
+        self._enc_turns = {}  # device -> (Condition, deque of batch indices in encode order)
         self._hold = None
 
     def qsl_for(self, device):
@@ -149,7 +150,7 @@ class OfflineSUT:
         for eng in self.engines:
             if id(eng) not in self._streams:
                 self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
-            self._enc_locks.setdefault(eng.device, threading.Lock())
+            self._enc_turns.setdefault(eng.device, (threading.Condition(), collections.deque()))
 
         def worker(eng):
             try:
@@ -157,6 +158,8 @@ class OfflineSUT:
                     with take:
                         i = nxt[0]
                         nxt[0] += 1
+                        if i < len(batches):  # encoders on one GPU run in batch order (longest first)
+                            self._enc_turns[eng.device][1].append(i)
                     if i >= len(batches):
                         return
                     self.batch_engine[i] = self.engines.index(eng)
@@ -181,16 +184,25 @@ class OfflineSUT:
         n = len(ids)
         n_pad = pad_batch(n)
         with torch.cuda.device(eng.device), torch.cuda.stream(st):
-            inp = self.qsl_for(eng.device).batch_inputs(idx, n_pad, torch.device("cuda", eng.device))
             res = torch.empty((n, eng.max_res), dtype=torch.int32, device=st.device)
             rl = torch.empty(n, dtype=torch.int32, device=st.device)
-            with self._enc_locks[eng.device]:  # encoders on one GPU take turns
+            # encoders on one GPU take turns in batch order (longest first): the longest batch's
+            # decode overlaps the most encoding, and the last encode is the shortest batch's
+            cv, turn = self._enc_turns[eng.device]
+            with cv:
+                cv.wait_for(lambda: turn[0] == bi)
+            try:
+                inp = self.qsl_for(eng.device).batch_inputs(idx, n_pad, torch.device("cuda", eng.device))
                 if "store" in inp:
                     eng.encode_gather(inp["store"], inp["offsets"], inp["lens"], inp["lens_host"], inp["T"], n, n_pad,
                                       stream=st)
                 else:
                     eng.encode(inp["x"], inp["lens"], inp["lens_host"], n=n, stream=st)
                 st.synchronize()
+            finally:
+                with cv:
+                    turn.popleft()
+                    cv.notify_all()
             if self._hold is not None:
                 k, sem, done, lk, nb = self._hold
                 with lk:
