@@ -23,9 +23,10 @@ def main():
     torch.cuda.set_device(0)
     pm, _ = weights.build_model()
     qsl = bench.build_qsl(2513, seed=4, device="cuda:0")
+    bsz = int(os.environ.get("RNNT_BENCH_BATCH", "4096"))  # the bench's default batch
     ids, idx = dist.query_arrays(2513, 24576)
-    batches = make_batches(qsl, ids, idx, 8192)
-    eng = Engine(pm, device=0, max_batch=8192, max_frames=500)
+    batches = make_batches(qsl, ids, idx, bsz)
+    eng = Engine(pm, device=0, max_batch=bsz, max_frames=500)
     out = {"lib": os.path.basename(os.environ.get("RNNT_MI355X_LIB", "default"))}
     tot = 0.0
     for i, (bids, bidx) in enumerate(batches):
