@@ -122,6 +122,7 @@ class OfflineSUT:
         self.completed = []  # per batch: (sample ids int64 [n], lengths int32 [n], tokens int32 [sum])
         self._streams = {}
         self._enc_turns = {}  # device -> (Condition, deque of batch indices in encode order)
+        self.encode_order = []  # batch indices in the order their encodes ran (all devices)
         self._hold = None
 
     def qsl_for(self, device):
@@ -142,6 +143,7 @@ class OfflineSUT:
         take = threading.Lock()
         errors = []
         self.batch_engine = [None] * len(batches)
+        self.encode_order = []
         k = self.early_decodes
         hold = k is not None and k < len(batches) <= len(self.engines)
         self._hold = None
@@ -191,6 +193,7 @@ class OfflineSUT:
             cv, turn = self._enc_turns[eng.device]
             with cv:
                 cv.wait_for(lambda: turn[0] == bi)
+                self.encode_order.append(bi)
             try:
                 inp = self.qsl_for(eng.device).batch_inputs(idx, n_pad, torch.device("cuda", eng.device))
                 if "store" in inp:

@@ -34,6 +34,7 @@ def test_config4_offline_query(pm, oracle):
         sut.issue_batches(batches)
         torch.cuda.synchronize()
         assert sorted(set(sut.batch_engine)) == [0, 1, 2]
+        assert sut.encode_order == [0, 1, 2]  # one GPU: encodes in batch order, longest batch first
         got_ids, lens, toks = sut.take_completed()
     finally:
         for e in engines:
