@@ -186,15 +186,16 @@ class OfflineSUT:
         n = len(ids)
         n_pad = pad_batch(n)
         with torch.cuda.device(eng.device), torch.cuda.stream(st):
-            res = torch.empty((n, eng.max_res), dtype=torch.int32, device=st.device)
-            rl = torch.empty(n, dtype=torch.int32, device=st.device)
             # encoders on one GPU take turns in batch order (longest first): the longest batch's
-            # decode overlaps the most encoding, and the last encode is the shortest batch's
+            # decode overlaps the most encoding, and the last encode is the shortest batch's.  Every
+            # step after the wait is under the finally, so a failing batch still hands the turn on.
             cv, turn = self._enc_turns[eng.device]
             with cv:
                 cv.wait_for(lambda: turn[0] == bi)
                 self.encode_order.append(bi)
             try:
+                res = torch.empty((n, eng.max_res), dtype=torch.int32, device=st.device)
+                rl = torch.empty(n, dtype=torch.int32, device=st.device)
                 inp = self.qsl_for(eng.device).batch_inputs(idx, n_pad, torch.device("cuda", eng.device))
                 if "store" in inp:
                     eng.encode_gather(inp["store"], inp["offsets"], inp["lens"], inp["lens_host"], inp["T"], n, n_pad,
