@@ -98,6 +98,7 @@ struct TileCfg {
   static constexpr int HP = BM / 4 + 16;         // int8 image pitch (16-B aligned rows, offset banks)
   static constexpr int NGT = G4 / BM;            // gate tiles per layer-step
   static constexpr int GPX = NGT / 4;            // gate tiles per XCD group
+  static_assert(NGT % 8 == 0, "one-batch-tile jobs deal their gate tiles to 8 XCDs");
   static_assert(BM >= 128 && BN >= 128, "staging swizzle: wave row blocks are 16-row aligned");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(BN * CROW + BN * HP <= STAGE, "c and h images share one stage buffer");
@@ -389,12 +390,24 @@ template <class C>
 __device__ __forceinline__ int job_tiles(const EncTickArgs& args, int j) {
   return C::BN == 256 ? (args.nbt[j] + 1) >> 1 : args.nbt[j];
 }
-// job tile k (0..) of XCD xcd -> (mt, nt); -1 past the XCD's last tile
+// job tile k (0..) of XCD xcd -> (mt, nt); -1 past the XCD's last tile.  A job with ONE batch tile
+// (small batches: config 3, short Server rounds, the tail of a sorted batch) spreads its gate tiles
+// over all 8 XCDs instead (the 4 x 2 split would leave XCDs 4-7 without work for it).
 template <class C>
 __device__ __forceinline__ int xcd_pick(const EncTickArgs& args, int xcd, int k, int& mt, int& nt) {
   const int gsel = xcd & 3, psel = xcd >> 2;
   for (int j = 0; j < args.njobs; ++j) {
     const int nbt = job_tiles<C>(args, j);
+    if (nbt == 1) {
+      constexpr int G8 = C::NGT / 8;
+      if (k < G8) {
+        mt = xcd * G8 + k;
+        nt = 0;
+        return j;
+      }
+      k -= G8;
+      continue;
+    }
     const int b0 = psel ? (nbt + 1) >> 1 : 0;
     const int b1 = psel ? nbt : (nbt + 1) >> 1;
     const int cnt = C::GPX * (b1 - b0);
@@ -468,7 +481,7 @@ static int tick_grid(const EncTickArgs& a) {  // workgroups: 8 XCDs x the batch-
   int per_xcd = 0;
   for (int j = 0; j < a.njobs; ++j) {
     const int nbt = C::BN == 256 ? (a.nbt[j] + 1) / 2 : a.nbt[j];
-    per_xcd += C::GPX * ((nbt + 1) / 2);
+    per_xcd += nbt == 1 ? C::NGT / 8 : C::GPX * ((nbt + 1) / 2);  // as xcd_pick
   }
   return 8 * per_xcd;
 }
