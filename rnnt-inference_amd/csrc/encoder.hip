@@ -99,13 +99,18 @@ struct TileCfg {
   static constexpr int NGT = G4 / BM;            // gate tiles per layer-step
   static constexpr int GPX = NGT / 4;            // gate tiles per XCD group
   static_assert(NGT % 8 == 0, "one-batch-tile jobs deal their gate tiles to 8 XCDs");
-  static_assert(BM >= 128 && BN >= 128, "staging swizzle: wave row blocks are 16-row aligned");
+  static_assert(BM >= 64 && BN >= 128, "one A piece (8 rows) per wave at least");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(BN * CROW + BN * HP <= STAGE, "c and h images share one stage buffer");
-  static_assert((BN * CPR) % (NWAVE * 64) == 0 && (BN * CPR) / (NWAVE * 64) >= 1, "c DMA pieces per wave");
+  static constexpr int CPIECES = BN * CPR / 64;   // 1 KiB DMA pieces of the tile's fp16 cell state
+  static_assert(CPIECES % NWAVE == 0 || CPIECES < NWAVE, "c DMA pieces per wave");
 };
 using BigTile = TileCfg<4, 8>;
 using SmallTile = TileCfg<2, 4>;
+// 64 gate rows x 128 batch rows, 4-deep ring (112 KiB): ticks whose jobs all have one batch tile
+// (batches of <= 128 rows, config 3) -- twice the workgroups of the small tile, each moving
+// (64 + 128) K instead of (128 + 128) K bytes, so the K loop of the widest job is a quarter shorter
+using MiniTile = TileCfg<1, 4, 4>;
 // the small tile with a 4-deep ring (144 KiB, one workgroup per CU) for ticks of at most one
 // workgroup per CU: a K loop with one stage in flight is latency-bound there (weights stream
 // from MALL / HBM at small batch)
@@ -174,12 +179,14 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // address.  Wave w moves A rows 8 PA w .. and B rows 8 PB w .. (PA / PB pieces each); lane l of
   // piece j lands at row 8 PA w + 8j + (l >> 3), slot l & 7.  SGPR tile bases + 32-bit lane offsets.
   const int r8 = lane >> 3, sl = lane & 7;
-  const int gc0 = (sl ^ ((r8 >> 1) & 7)) * 16;        // even pieces (rows 8j + r8, j even)
-  const int gc1 = (sl ^ (((8 + r8) >> 1) & 7)) * 16;  // odd pieces
+  // slot of row r = 8 P w + 8 j + r8 is (r >> 1) & 7 = (4 P w + 4 j + (r8 >> 1)) & 7: even / odd pieces
+  const int swA = (4 * C::PA * wave) & 7, swB = (4 * C::PB * wave) & 7;  // 0 unless P is odd
+  const int gA0 = (sl ^ ((swA + (r8 >> 1)) & 7)) * 16, gA1 = (sl ^ ((swA + 4 + (r8 >> 1)) & 7)) * 16;
+  const int gB0 = (sl ^ ((swB + (r8 >> 1)) & 7)) * 16, gB1 = (sl ^ ((swB + 4 + (r8 >> 1)) & 7)) * 16;
   const uint32_t rlA = (uint32_t)(8 * C::PA * wave + r8), rlB = (uint32_t)(8 * C::PB * wave + r8);
-  const uint32_t oA0 = rlA * K + gc0, oA1 = rlA * K + gc1;
-  const uint32_t oX0 = rlB * a.I + gc0, oX1 = rlB * a.I + gc1;
-  const uint32_t oH0 = rlB * H + gc0, oH1 = rlB * H + gc1;
+  const uint32_t oA0 = rlA * K + gA0, oA1 = rlA * K + gA1;
+  const uint32_t oX0 = rlB * a.I + gB0, oX1 = rlB * a.I + gB1;
+  const uint32_t oH0 = rlB * H + gB0, oH1 = rlB * H + gB1;
   const int8_t* wbase = a.W + (size_t)m0 * K;
   const int8_t* xbase = a.x + (size_t)n0 * a.I;
   const int8_t* hbase = a.h_in + (size_t)n0 * H - a.I;  // k >= I indexes h at k - I
@@ -211,12 +218,13 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // (l % CPR) ^ (row % CPR) at slot l % CPR (cimg_off: 2-way instead of 8-way epilogue conflicts)
   const int cbuf = (nS % NBUF) * STAGE;
   auto issue_c = [&]() __attribute__((always_inline)) {
-    constexpr int RPP = 64 / C::CPR, NPC = BN * C::CPR / (NWAVE * 64);
+    constexpr int RPP = 64 / C::CPR, NPC = C::CPIECES >= NWAVE ? C::CPIECES / NWAVE : 1;
     const int cr = lane / C::CPR, cc = lane % C::CPR;
     const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + (cc ^ (cr & (C::CPR - 1))) * 8;
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc) {
       const int p = wave * NPC + pc;
+      if (C::CPIECES < NWAVE && p >= C::CPIECES) break;  // wave-uniform
       __builtin_amdgcn_global_load_lds((glb_void*)(cb + (size_t)(RPP * p + cr) * H), (lds_void*)(lds + cbuf + p * 1024),
                                        16, 0, 0);
     }
@@ -303,8 +311,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     float cin[WMT];
     if (WMT == 4) {
       const uint2 cv = *(const uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
-      cin[0] = h2f((uint16_t)(cv.x & 0xffff)); cin[1] = h2f((uint16_t)(cv.x >> 16));
+      cin[0] = h2f((uint16_t)(cv.x & 0xffff)); cin[1 % WMT] = h2f((uint16_t)(cv.x >> 16));
       cin[2 % WMT] = h2f((uint16_t)(cv.y & 0xffff)); cin[3 % WMT] = h2f((uint16_t)(cv.y >> 16));
+    } else if (WMT == 1) {
+      cin[0] = h2f(*(const uint16_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)));
     } else {
       const uint32_t cv = *(const uint32_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
       cin[0] = h2f((uint16_t)(cv & 0xffff)); cin[1 % WMT] = h2f((uint16_t)(cv >> 16));
@@ -324,6 +334,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     if (WMT == 4) {
       *(uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)) = uint2{cw[0], cw[1]};
       *(uint32_t*)(hs + r * HP + ul) = hq;
+    } else if (WMT == 1) {
+      *(uint16_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)) = (uint16_t)cw[0];
+      *(uint8_t*)(hs + r * HP + ul) = (uint8_t)hq;
     } else {
       *(uint32_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)) = cw[0];
       *(uint16_t*)(hs + r * HP + ul) = (uint16_t)hq;
@@ -331,16 +344,21 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     if (a.mode == ENC_OUT_FINAL) {
       if (a.y32) {
         if (WMT == 4) *(float4*)(a.y32 + (size_t)n * H + u0) = float4{hv[0], hv[1 % WMT], hv[2 % WMT], hv[3 % WMT]};
+        else if (WMT == 1) a.y32[(size_t)n * H + u0] = hv[0];
         else *(float2*)(a.y32 + (size_t)n * H + u0) = float2{hv[0], hv[1 % WMT]};
       }
       const uint32_t f01 = (uint32_t)f2bf_ftz(hv[0]) | ((uint32_t)f2bf_ftz(hv[1 % WMT]) << 16);
       if (WMT == 4)
         *(uint2*)(ys + cimg_off<C::CROW>(r, ul * 2)) =
             uint2{f01, (uint32_t)f2bf_ftz(hv[2 % WMT]) | ((uint32_t)f2bf_ftz(hv[3 % WMT]) << 16)};
+      else if (WMT == 1)
+        *(uint16_t*)(ys + cimg_off<C::CROW>(r, ul * 2)) = (uint16_t)f01;
       else
         *(uint32_t*)(ys + cimg_off<C::CROW>(r, ul * 2)) = f01;
     } else if (WMT == 4) {
       *(uint32_t*)(ys + r * HP + ul) = yq;
+    } else if (WMT == 1) {
+      *(uint8_t*)(ys + r * HP + ul) = (uint8_t)yq;
     } else {
       *(uint16_t*)(ys + r * HP + ul) = (uint16_t)yq;
     }
@@ -349,8 +367,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   // copy-out: thread t moves 16-byte chunks; a wave instruction writes whole row segments
   const int um = m0 >> 2;
 #pragma unroll
-  for (int it = 0; it < BN * C::CPR / (NWAVE * 64); ++it) {  // c (and bf16 f): BN rows x CROW bytes
+  for (int it = 0; it < (BN * C::CPR + NWAVE * 64 - 1) / (NWAVE * 64); ++it) {  // c (and bf16 f): BN rows x CROW bytes
     const int idx = it * NWAVE * 64 + tid, r = idx / C::CPR, ch = idx % C::CPR;
+    if ((BN * C::CPR) % (NWAVE * 64) != 0 && idx >= BN * C::CPR) break;
     *(uint4*)(a.c + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(smem + cbuf + cimg_off<C::CROW>(r, ch * 16));
     if (a.mode == ENC_OUT_FINAL)
       *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + cimg_off<C::CROW>(r, ch * 16));
@@ -465,7 +484,7 @@ int launch_quantize_gather(const float* store, const int64_t* offsets, const int
 // section 4): a full round of small tiles (two per CU) costs ENC_SMALL_ROUND of it, and a
 // small-tile launch takes at least ENC_SMALL_FLOOR (its K loop's latency); the small tile must
 // win by ENC_SMALL_MARGIN (its co-resident workgroups also leave room for the overlapped
-// decode's, which slows the encoder).  RNNT_ENC_TILE=big|small|tiny forces a shape.
+// decode's, which slows the encoder).  RNNT_ENC_TILE=big|small|tiny|mini forces a shape.
 constexpr int ENC_CUS = 256;
 constexpr float ENC_SMALL_ROUND = 0.59f, ENC_SMALL_FLOOR = 0.5f, ENC_SMALL_MARGIN = 0.9f;
 static int enc_tile_choice() {  // read per launch (a test may switch it between calls)
@@ -474,6 +493,7 @@ static int enc_tile_choice() {  // read per launch (a test may switch it between
   if (!strcmp(s, "big")) return 1;
   if (!strcmp(s, "small")) return 2;
   if (!strcmp(s, "tiny")) return 3;
+  if (!strcmp(s, "mini")) return 5;
   return 0;
 }
 template <class C>
@@ -497,16 +517,21 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
   // shapes the kernel's staging assumes (checked on the host: a mismatch would read out of bounds)
   for (int j = 0; j < a.njobs; ++j)
     if (a.job[j].I % 128 != 0 || a.nbt[j] < 0) return -1;
-  const int gb = tick_grid<BigTile>(a), gs = tick_grid<SmallTile>(a);
+  const int gb = tick_grid<BigTile>(a), gs = tick_grid<SmallTile>(a), gm = tick_grid<MiniTile>(a);
   if (gb <= 0) return 0;
   int choice = enc_tile_choice();
   if (choice == 0) {
     const float rb = (float)((gb + ENC_CUS - 1) / ENC_CUS);
     const float rs = fmaxf((float)gs / (2 * ENC_CUS) * ENC_SMALL_ROUND, ENC_SMALL_FLOOR);
     choice = rs < ENC_SMALL_MARGIN * rb ? 2 : 1;
+    if (choice == 2 && gs <= ENC_CUS) {  // at most one small workgroup per CU: a deep ring
+      bool one_tile = true;
+      for (int j = 0; j < a.njobs; ++j) one_tile = one_tile && a.nbt[j] <= 1;
+      choice = one_tile && gm <= ENC_CUS ? 5 : 3;  // still one per CU with half the gate rows: mini
+    }
   }
-  if (choice == 0 && gs <= ENC_CUS) choice = 3;  // at most one small workgroup per CU: the deep ring
   if (choice == 1) return launch_tick<BigTile>(a, gb, st);
+  if (choice == 5) return launch_tick<MiniTile>(a, gm, st);
   return choice == 3 ? launch_tick<TinyTile>(a, gs, st) : launch_tick<SmallTile>(a, gs, st);
 }
 

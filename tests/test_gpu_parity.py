@@ -27,10 +27,11 @@ def engine(model):
     e.close()
 
 
-@pytest.fixture(params=["big", "small", "tiny"])
+@pytest.fixture(params=["big", "small", "tiny", "mini"])
 def tile(request, monkeypatch):
-    """Every encoder tile variant (256 x 256; 128 x 128 with a 2- and a 4-deep stage ring,
-    encoder.hip) forced in turn; the engine otherwise picks one per tick."""
+    """Every encoder tile variant (256 x 256; 128 x 128 with a 2- and a 4-deep stage ring;
+    64 x 128 with a 4-deep ring, encoder.hip) forced in turn; the engine otherwise picks one per
+    tick."""
     monkeypatch.setenv("RNNT_ENC_TILE", request.param)
     return request.param
 
