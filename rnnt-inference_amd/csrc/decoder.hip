@@ -85,11 +85,15 @@ __device__ unsigned int g_st_n;
 struct GridXY {
   int x, y, ny;
 };
+// One row group (a short list: the decode's tail) launches just X workgroups, dealt round-robin
+// to the XCDs: the column groups' weight slices (up to 1.6 MB) then stream through all eight L2s
+// instead of one, and the single row tile's inputs are small.
 __device__ __forceinline__ GridXY xcd_grid(int X) {
+  if ((int)gridDim.x == X) return GridXY{(int)blockIdx.x, 0, 1};
   const int id = blockIdx.x, t = id >> 3;
   return GridXY{t % X, (id & 7) + 8 * (t / X), 8 * (int)(gridDim.x / (8 * X))};
 }
-static inline int xcd_grid_size(int X, int rows) { return 8 * X * ((rows + 7) / 8); }
+static inline int xcd_grid_size(int X, int rows) { return rows <= 1 ? X : 8 * X * ((rows + 7) / 8); }
 
 // ---------------------------------------------------------------- layer-0 input table
 // xtab[g][r] = b_ih0[r] + emb[g].W_ih0[r]^T (g < 28), xtab[28] = b_ih0 (SOS: zero embedding).
