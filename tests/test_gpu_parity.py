@@ -182,3 +182,13 @@ def test_large_batch_rows_match_small_batch(engine, model, oracle, monkeypatch):
         if lo == 0:
             fo = oracle.encoder_i8(model, xs[:, :8], lp[:8])
             np.testing.assert_array_equal(_valid(fg[:, :8], lens[:8]).view(np.uint32), _valid(fo, lens[:8]).view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_engine_rejects_sizes_past_the_decode_entry_fields(model):
+    """The decode's live-list entries hold the row in 24 bits and the frame / f_len in 16 bits
+    each (decoder.hip live_entry): an engine whose frames could exceed them is refused at create."""
+    from rnnt_amd._lib import EngineError
+    from rnnt_amd.engine import Engine
+    with pytest.raises(EngineError, match="max_batch or max_frames too large"):
+        Engine(model, device=0, max_batch=256, max_frames=2 * 65536 + 2)
