@@ -143,6 +143,19 @@ int rnnt_engine_encode_stream(rnnt_engine* e, const float* store, const int64_t*
                               const int32_t* lens_host, const int32_t* reset, int T, int n, int n_pad, void* stream);
 int rnnt_engine_decode_stream(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, const int32_t* reset,
                               void* stream);
+/* Pipelined form of the two calls above: chunk k+1's rnnt_engine_encode_stream_pl may run (on its
+ * own stream, from its own host thread) while chunk k's rnnt_engine_decode_stream_pl runs on
+ * another.  Chunk k's encode copies its output to the decode side once chunk k-1's decode has read
+ * it (encode_stream_pl blocks on the host until that decode has started); decode_stream_pl k must
+ * be called after encode_stream_pl k returned, decodes in chunk order from one thread, encodes in
+ * chunk order from one thread.  Chunk k's reset flags (read by its encode and its decode) must
+ * stay unchanged until its decode has completed on the device.  Do not mix with the other encode /
+ * decode calls on the same engine. */
+int rnnt_engine_encode_stream_pl(rnnt_engine* e, const float* store, const int64_t* offsets, const int32_t* lens,
+                                 const int32_t* lens_host, const int32_t* reset, int T, int n, int n_pad,
+                                 void* stream);
+int rnnt_engine_decode_stream_pl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, const int32_t* reset,
+                                 void* stream);
 
 /* encode + decode. */
 int rnnt_engine_infer(rnnt_engine* e, const float* feats, const int32_t* lens, const int32_t* lens_host, int T,

@@ -9,7 +9,9 @@
 
 #include <algorithm>
 #include <array>
+#include <condition_variable>
 #include <cstdio>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -74,6 +76,19 @@ struct rnnt_engine {
   // are ordered even when the caller puts them on different streams.
   hipEvent_t state_ev = nullptr;
   bool state_rec = false;
+  // Pipelined stream calls (rnnt_engine_encode_stream_pl / decode_stream_pl): chunk k+1's encode
+  // runs while chunk k decodes.  The encoder keeps its own state in stream order; at the end of
+  // chunk k's encode its final-layer output and lengths are copied to the decode side (fbf_dec,
+  // flen_dec) once chunk k-1's decode has handed them off (after its joint_trans and its private
+  // copy of the lengths).  Encode k waits for hand-off k-1 on the host (the condition below) and
+  // on the GPU (pl_handoff_ev); decode k waits for copy k (pl_copy_ev[k & 1]).
+  uint16_t* fbf_dec = nullptr;
+  int32_t *flen_dec = nullptr, *flen_dpriv = nullptr;
+  hipEvent_t pl_copy_ev[2] = {nullptr, nullptr}, pl_handoff_ev = nullptr;
+  int pl_meta[2][3] = {};  // (T, n, n_pad) of chunk k at k & 1
+  int64_t pl_enc_k = 0, pl_dec_k = 0, pl_handoff_k = -1;
+  std::mutex pl_mu;
+  std::condition_variable pl_cv;
   // profiling
   bool prof = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_enc;
@@ -331,6 +346,8 @@ extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
   if (e->op_count_host) (void)hipHostFree(e->op_count_host);
   if (e->host_flags) (void)hipHostFree(e->host_flags);
   for (auto ev : e->poll_ev)
+    if (ev) (void)hipEventDestroy(ev);
+  for (auto ev : {e->pl_copy_ev[0], e->pl_copy_ev[1], e->pl_handoff_ev})
     if (ev) (void)hipEventDestroy(ev);
   if (e->state_ev) {
     (void)hipEventSynchronize(e->state_ev);
@@ -602,14 +619,14 @@ struct EncInput {
 // reset == nullptr: a batch of whole utterances (every row's state starts at zero); otherwise a
 // stream chunk (rnnt_engine_encode_stream): rows keep their state unless flagged.
 static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, const int32_t* lens_host, int T, int n,
-                       int n_pad, float* f_out, void* stream, const int32_t* reset = nullptr) {
+                       int n_pad, float* f_out, void* stream, const int32_t* reset = nullptr, bool pl = false) {
   if (!e || !lens || !(in.feats || (in.store && in.offsets))) return fail(RNNT_EINVAL, "null argument");
   if (e->enc_loaded != 0x1f) return fail(RNNT_EINVAL, "encoder weights not loaded");
   int r = check_batch(e, T, n, n_pad);
   if (r) return r;
   DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
-  if ((r = state_acquire(e, st))) return r;
+  if (!pl && (r = state_acquire(e, st))) return r;
   const int Tp = (T + 1) / 2;
   const std::vector<int> tm = tile_maxima(lens_host, n, n_pad);
   if (!reset) {
@@ -661,7 +678,7 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
   // skipped tile are past their length in this call, i.e. finished
   for (int l = 0; l < 5; ++l) e->hpar[l] = (e->hpar[l] + (l < 2 ? T : Tp)) & 1;
   if (e->prof) e->ev_enc.push_back({ev0, new_event(st)});
-  if ((r = state_release(e, st))) return r;
+  if (!pl && (r = state_release(e, st))) return r;
   e->encode_calls++;
   e->last_T = T;
   e->last_n = n;
@@ -711,6 +728,41 @@ extern "C" int rnnt_engine_decode_stream(rnnt_engine* e, int32_t* res, int32_t* 
   return decode_impl(e, res, res_len, max_res, stream, reset);
 }
 
+// The decode of one encoded batch / chunk: joint_trans of its final-layer output fbf (T frames
+// before stacking, n rows of n_pad) with lengths flen, then the greedy loop; after_jt runs on the
+// host right after joint_trans is enqueued (the pipelined hand-off point).
+template <class AfterJT>
+static int decode_core(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, hipStream_t st,
+                       const int32_t* reset, const uint16_t* fbf, const int32_t* flen, int T, int n, int n_pad,
+                       AfterJT after_jt) {
+  const int Tp = (T + 1) / 2;
+  hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
+  if (launch_joint_trans(e->dw, fbf, flen, e->F, Tp, n_pad, st))
+    return fail(RNNT_EDEVICE, "joint_trans launch failed");
+  hipEvent_t ev1 = e->prof ? new_event(st) : nullptr;
+  int r = after_jt();
+  if (r) return r;
+  DecArgs a{};
+  a.w = e->dw;
+  a.F = e->F;
+  a.f_lens = flen;
+  a.hc = e->hc;
+  a.G = e->G;
+  a.res = res;
+  a.res_len = res_len;
+  a.N = n;
+  a.Npad = n_pad;
+  a.max_res = max_res;
+  a.s = e->ds;
+  a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
+  const int steps = launch_greedy_decode(a, e->host_flags, e->poll_ev, st, reset);
+  if (steps < 0) return fail(RNNT_EDEVICE, "greedy launch failed");
+  e->decode_steps += steps;
+  if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
+  e->decode_calls++;
+  return 0;
+}
+
 static int decode_impl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream,
                        const int32_t* reset) {
   if (!e || !res || !res_len) return fail(RNNT_EINVAL, "null argument");
@@ -722,31 +774,100 @@ static int decode_impl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
   hipStream_t st = pick(e, stream);
   int r = state_acquire(e, st);
   if (r) return r;
-  const int Tp = (e->last_T + 1) / 2;
-  hipEvent_t ev0 = e->prof ? new_event(st) : nullptr;
-  if (launch_joint_trans(e->dw, e->fbf, e->flen, e->F, Tp, e->last_npad, st))
-    return fail(RNNT_EDEVICE, "joint_trans launch failed");
-  hipEvent_t ev1 = e->prof ? new_event(st) : nullptr;
-  DecArgs a{};
-  a.w = e->dw;
-  a.F = e->F;
-  a.f_lens = e->flen;
-  a.hc = e->hc;
-  a.G = e->G;
-  a.res = res;
-  a.res_len = res_len;
-  a.N = e->last_n;
-  a.Npad = e->last_npad;
-  a.max_res = max_res;
-  a.s = e->ds;
-  a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
-  const int steps = launch_greedy_decode(a, e->host_flags, e->poll_ev, st, reset);
-  if (steps < 0) return fail(RNNT_EDEVICE, "greedy launch failed");
-  e->decode_steps += steps;
-  if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
-  if ((r = state_release(e, st))) return r;
-  e->decode_calls++;
+  r = decode_core(e, res, res_len, max_res, st, reset, e->fbf, e->flen, e->last_T, e->last_n, e->last_npad,
+                  [] { return 0; });
+  return r ? r : state_release(e, st);
+}
+
+// ---- pipelined stream calls (see rnnt_engine::fbf_dec)
+static int pl_init(rnnt_engine* e) {
+  if (e->fbf_dec) return 0;
+  const size_t NP = e->np_max, TPM = e->tp_max;
+  int r = dev_alloc(e, &e->fbf_dec, TPM * NP * H);
+  r = r ? r : dev_alloc(e, &e->flen_dec, NP);
+  r = r ? r : dev_alloc(e, &e->flen_dpriv, NP);
+  for (int i = 0; i < 2 && !r; ++i)
+    if (hipEventCreateWithFlags(&e->pl_copy_ev[i], hipEventDisableTiming) != hipSuccess)
+      r = fail(RNNT_EDEVICE, "hipEventCreate failed");
+  if (!r && hipEventCreateWithFlags(&e->pl_handoff_ev, hipEventDisableTiming) != hipSuccess)
+    r = fail(RNNT_EDEVICE, "hipEventCreate failed");
+  return r;
+}
+
+extern "C" int rnnt_engine_encode_stream_pl(rnnt_engine* e, const float* store, const int64_t* offsets,
+                                            const int32_t* lens, const int32_t* lens_host, const int32_t* reset,
+                                            int T, int n, int n_pad, void* stream) {
+  if (!e || !lens_host || !reset) return fail(RNNT_EINVAL, "encode_stream_pl needs the host lengths and the reset flags");
+  for (int i = 0; i < n; ++i)
+    if (lens_host[i] < 0 || lens_host[i] > T) return fail(RNNT_EINVAL, "a chunk length exceeds T");
+  int r = 0;
+  {
+    DEVICE_SCOPE(e->device);
+    if ((r = pl_init(e))) return r;
+  }
+  EncInput in;
+  in.store = store;
+  in.offsets = offsets;
+  if ((r = encode_impl(e, in, lens, lens_host, T, n, n_pad, nullptr, stream, reset, true))) return r;
+  DEVICE_SCOPE(e->device);
+  hipStream_t st = pick(e, stream);
+  const int64_t k = e->pl_enc_k;
+  {  // the decode side's buffers are free once chunk k-1's decode has handed them off
+    std::unique_lock<std::mutex> lk(e->pl_mu);
+    e->pl_cv.wait(lk, [&] { return e->pl_handoff_k >= k - 1; });
+  }
+  if (k >= 1) HIPCHK(hipStreamWaitEvent(st, e->pl_handoff_ev, 0));
+  const int Tp = (T + 1) / 2;
+  HIPCHK(hipMemcpyAsync(e->fbf_dec, e->fbf, (size_t)Tp * n_pad * H * sizeof(uint16_t), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(e->flen_dec, e->flen, (size_t)n_pad * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipEventRecord(e->pl_copy_ev[k & 1], st));
+  {
+    std::lock_guard<std::mutex> lk(e->pl_mu);
+    e->pl_meta[k & 1][0] = T;
+    e->pl_meta[k & 1][1] = n;
+    e->pl_meta[k & 1][2] = n_pad;
+    e->pl_enc_k = k + 1;
+  }
   return 0;
+}
+
+extern "C" int rnnt_engine_decode_stream_pl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res,
+                                            const int32_t* reset, void* stream) {
+  if (!e || !res || !res_len || !reset) return fail(RNNT_EINVAL, "null argument");
+  if (!e->xtab_ok || !e->joint1_loaded || !e->joint2_loaded)
+    return fail(RNNT_EINVAL, "prediction (with embedding) / joint weights not loaded");
+  if (max_res <= 0) return fail(RNNT_EINVAL, "max_res must be positive");
+  const int64_t k = e->pl_dec_k;
+  int T, n, n_pad;
+  {
+    std::lock_guard<std::mutex> lk(e->pl_mu);
+    if (k >= e->pl_enc_k) return fail(RNNT_EINVAL, "decode_stream_pl before its chunk's encode_stream_pl returned");
+    T = e->pl_meta[k & 1][0];
+    n = e->pl_meta[k & 1][1];
+    n_pad = e->pl_meta[k & 1][2];
+  }
+  DEVICE_SCOPE(e->device);
+  hipStream_t st = pick(e, stream);
+  bool handed = false;
+  auto hand_off = [&] {  // chunk k's inputs are consumed: encode k+1 may overwrite them
+    handed = true;
+    const bool ok = hipEventRecord(e->pl_handoff_ev, st) == hipSuccess;
+    {
+      std::lock_guard<std::mutex> lk(e->pl_mu);
+      e->pl_handoff_k = k;
+    }
+    e->pl_cv.notify_all();
+    return ok ? 0 : fail(RNNT_EDEVICE, "hipEventRecord failed");
+  };
+  int r = 0;
+  if (hipStreamWaitEvent(st, e->pl_copy_ev[k & 1], 0) != hipSuccess ||
+      hipMemcpyAsync(e->flen_dpriv, e->flen_dec, (size_t)n_pad * sizeof(int32_t), hipMemcpyDeviceToDevice, st) !=
+          hipSuccess)
+    r = fail(RNNT_EDEVICE, "stream wait / copy failed");
+  if (!r) r = decode_core(e, res, res_len, max_res, st, reset, e->fbf_dec, e->flen_dpriv, T, n, n_pad, hand_off);
+  if (!handed) hand_off();  // never leave the encode side waiting on a failed decode
+  e->pl_dec_k = k + 1;
+  return r;
 }
 
 extern "C" int rnnt_engine_set_profiling(rnnt_engine* e, int on) {

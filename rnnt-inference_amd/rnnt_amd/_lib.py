@@ -75,6 +75,10 @@ _SIGS = {
     "rnnt_engine_encode_stream": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "rnnt_engine_decode_stream": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "rnnt_engine_encode_stream_pl": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]),
+    "rnnt_engine_decode_stream_pl": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                               C.c_void_p]),
     "rnnt_op_lstm_bf16": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_void_p]),
     "rnnt_op_joint_hidden": (C.c_int, [C.c_void_p] * 4 + [C.c_int, C.c_void_p]),
     "rnnt_op_joint_logits": (C.c_int, [C.c_void_p] * 3 + [C.c_int, C.c_void_p]),

@@ -130,6 +130,24 @@ class Engine:
                                                  _stream_handle(stream))
         _lib.check(rc, "rnnt_engine_decode_stream")
 
+    def encode_stream_pl(self, store, offsets, lens, lens_host, reset, T, n, n_pad, stream=None):
+        """Pipelined encode_stream (rnnt_engine_encode_stream_pl): chunk k+1's encode runs while
+        chunk k decodes (decode_stream_pl from another thread).  Returns after chunk k-1's decode
+        has taken its inputs; reset must stay unchanged until this chunk's decode completed."""
+        assert store.is_contiguous() and store.shape[1] == R.trans_input_size and offsets.dtype.itemsize == 8
+        assert reset.dtype.itemsize == 4 and reset.numel() >= n_pad
+        lh = np.ascontiguousarray(lens_host, np.int32)
+        rc = self._lib.rnnt_engine_encode_stream_pl(self._h, _ptr(store), _ptr(offsets), _ptr(lens),
+                                                    lh.ctypes.data, _ptr(reset), T, n, n_pad,
+                                                    _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_encode_stream_pl")
+
+    def decode_stream_pl(self, res, res_len, reset, stream=None):
+        """Pipelined decode_stream: decodes the oldest chunk whose encode_stream_pl returned."""
+        rc = self._lib.rnnt_engine_decode_stream_pl(self._h, _ptr(res), _ptr(res_len), res.shape[1], _ptr(reset),
+                                                    _stream_handle(stream))
+        _lib.check(rc, "rnnt_engine_decode_stream_pl")
+
     def decode(self, res, res_len, stream=None):
         """res: cuda int32 [n, max_res]; res_len: cuda int32 [n]."""
         rc = self._lib.rnnt_engine_decode(self._h, _ptr(res), _ptr(res_len), res.shape[1], _stream_handle(stream))

@@ -376,7 +376,7 @@ class ServerSUT:
     iteration, which amortises its CPU iteration) is subsumed: a round is one chunk and answers
     every slot that finished in it.  Latency per sample = completion - issue time."""
 
-    def __init__(self, engines, qsl, slots=2048, split_len=128, qos_len=None, on_complete=None):
+    def __init__(self, engines, qsl, slots=2048, split_len=128, qos_len=None, on_complete=None, pipelined=False):
         import threading
         from .engine import pad_batch
         if split_len <= 0 or split_len % 2:
@@ -388,6 +388,7 @@ class ServerSUT:
             if e.max_batch < self.slots:
                 raise ValueError(f"engine max_batch {e.max_batch} < {self.slots} slots")
         self.on_complete = on_complete
+        self.pipelined = bool(pipelined)
         self.responses, self.latency = {}, {}
         self._pending, self._qos = [], []  # (issue_time, QuerySample)
         self._cv = threading.Condition()
@@ -403,7 +404,7 @@ class ServerSUT:
         for e in self.engines:
             self._enc_locks.setdefault(e.device, threading.Lock())
         for j in range(len(self.engines)):
-            t = threading.Thread(target=self._worker, args=(j,), daemon=True)
+            t = threading.Thread(target=self._worker_pl if self.pipelined else self._worker, args=(j,), daemon=True)
             t.start()
             self._threads.append(t)
 
@@ -524,6 +525,127 @@ class ServerSUT:
             for item in sample:
                 if item is not None:
                     self.latency[item[1].id] = float("inf")
+
+
+    def _worker_pl(self, j):
+        """Pipelined rounds (``pipelined=True``): this thread plans and encodes round k+1 while a
+        decode thread of the same engine decodes round k (rnnt_engine_encode_stream_pl /
+        decode_stream_pl).  Planning needs only the host frame counters, so a slot whose features
+        run out in round k is refilled in round k+1 before round k's decode has answered it; the
+        decode thread reads finished rows back before it starts round k+1's decode, which resets
+        them.  Answers are those of ``_worker``."""
+        import queue
+        import threading
+        import time
+        import torch
+        eng = self.engines[j]
+        S, L, qsl = self.slots, self.split_len, self.qsl
+        dev = torch.device("cuda", eng.device)
+        NR = 4  # reset-flag ring: round k's flags live until its decode completed (k+3 reuses them)
+        with torch.cuda.device(eng.device):
+            est, dst = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+            res = torch.empty((S, eng.max_res), dtype=torch.int32, device=dev)
+            rl = torch.zeros(S, dtype=torch.int32, device=dev)
+            h_reset = torch.zeros(S, dtype=torch.int32).pin_memory()
+            h_lens = torch.zeros(S, dtype=torch.int32).pin_memory()
+            h_off = torch.zeros(S, dtype=torch.int64).pin_memory()
+            d_reset = [torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(NR)]
+            d_lens = torch.zeros(S, dtype=torch.int32, device=dev)
+            d_off = torch.zeros(S, dtype=torch.int64, device=dev)
+        store = qsl.feats
+        sample = [None] * S
+        pos = np.zeros(S, np.int64)
+        remain = np.zeros(S, np.int32)
+        base = np.zeros(S, np.int64)
+        rounds = queue.Queue(maxsize=2)  # (reset ring index, [(slot, (issue_time, QuerySample))])
+        started = [0]  # rounds whose decode has been called
+        scv = threading.Condition()
+
+        def decoder():
+            failed = False
+            while True:
+                item = rounds.get()
+                with scv:
+                    started[0] += 1
+                    scv.notify()
+                if item is None:
+                    return
+                r, done = item
+                try:  # keep decoding after a failure: the encode side waits for each hand-off
+                    with torch.cuda.device(eng.device), torch.cuda.stream(dst):
+                        eng.decode_stream_pl(res, rl, d_reset[r], stream=dst)
+                        if done and not failed:
+                            di = torch.tensor([i for i, _ in done], device=dev)
+                            rlh = rl.index_select(0, di).cpu().numpy()
+                            toks = res.index_select(0, di)[:, : max(1, int(rlh.max()))].cpu().numpy()
+                        else:
+                            dst.synchronize()
+                    if failed:
+                        raise RuntimeError("an earlier pipelined decode failed")
+                    now = time.perf_counter()
+                    for k, (_, (t0, smp)) in enumerate(done):
+                        row = toks[k, : rlh[k]].copy()
+                        self.responses[smp.id] = row
+                        self.latency[smp.id] = now - t0
+                        if self.on_complete:
+                            self.on_complete(smp, row)
+                    self.rounds += 1
+                except Exception as ex:
+                    if not failed:
+                        self.errors.append(ex)
+                    failed = True
+                    for _, (_, smp) in done:
+                        self.latency[smp.id] = float("inf")
+
+        dthread = threading.Thread(target=decoder, daemon=True)
+        dthread.start()
+        k = 0
+        try:
+            while True:
+                free = [i for i in range(S) if sample[i] is None]
+                new = self._take(len(free), busy=len(free) < S)
+                if new is None:
+                    return
+                rs = h_reset.numpy()
+                rs[:] = 0
+                for i, item in zip(free, new):
+                    sample[i] = item
+                    idx = item[1].index
+                    pos[i], remain[i], base[i] = 0, int(qsl.lengths[idx]), int(qsl.offsets[idx])
+                    rs[i] = 1
+                busy = np.array([x is not None for x in sample])
+                if not busy.any():
+                    continue
+                cl = np.where(busy, np.minimum(remain, L), 0).astype(np.int32)
+                h_lens.numpy()[:] = cl
+                h_off.numpy()[:] = np.where(busy, base + pos, 0)
+                T = max(int(cl.max()), 1)
+                r = k % NR
+                with scv:  # round k's encode hands over once round k-1's decode began: wait for
+                    while started[0] < k:  # that outside the encoders' turn
+                        scv.wait()
+                with torch.cuda.device(eng.device), torch.cuda.stream(est):
+                    d_reset[r].copy_(h_reset, non_blocking=True)
+                    d_lens.copy_(h_lens, non_blocking=True)
+                    d_off.copy_(h_off, non_blocking=True)
+                    with self._enc_locks[eng.device]:  # encoders on one GPU take turns
+                        eng.encode_stream_pl(store, d_off, d_lens, cl, d_reset[r], T, S, S, stream=est)
+                        est.synchronize()
+                pos += cl
+                remain -= cl
+                done = [(int(i), sample[i]) for i in np.nonzero(busy & (remain == 0))[0]]
+                for i, _ in done:
+                    sample[i] = None
+                rounds.put((r, done))
+                k += 1
+        except Exception as ex:  # surface in the caller, never hang the query
+            self.errors.append(ex)
+            for item in sample:
+                if item is not None:
+                    self.latency[item[1].id] = float("inf")
+        finally:
+            rounds.put(None)
+            dthread.join()
 
 
 class DynamicBatchServerSUT:

@@ -4,6 +4,7 @@ csrc/torch_sut.cpp:238-571; PipelineState, csrc/metadata.cpp:97-194).
 * engine level: utterances fed in split_len chunks through rnnt_engine_encode_stream /
   rnnt_engine_decode_stream while finished slots are refilled -- every answer equals the CPU
   restatement's whole-utterance answer (chunking is exact);
+* the same through the pipelined entry points (round k+1 encodes while round k decodes);
 * BASELINE config 5 shape: Poisson arrivals over a 2513-sample dev-clean-shaped QSL into the
   ServerSUT (two engines in flight, slot refill, early response, QoS deferral of the longest
   samples until FlushQueries) -- every response equals the Offline answer for that sample, and a
@@ -37,9 +38,11 @@ def _oracle_answers(oracle, pm, qsl, idx):
     return [ro[i, : rlo[i]] for i in range(len(idx))]
 
 
-def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle):
+@pytest.mark.parametrize("pl", [False, True], ids=["plain", "pipelined_calls"])
+def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl):
     """Slots keep their LSTM / prediction state across chunks; a slot that finishes is refilled
-    (reset) with the next utterance while the others continue."""
+    (reset) with the next utterance while the others continue.  pl: the same rounds through the
+    pipelined entry points (rnnt_engine_encode_stream_pl / decode_stream_pl) from one thread."""
     lens = np.array([137, 64, 92, 161, 45, 130, 77, 104, 59], np.int32)  # odd lengths end in odd chunks
     x = synthetic.make_features(int(lens.max()), len(lens), seed=61, lens=lens)  # emits 251 symbols in all
     store = torch.from_numpy(np.concatenate([x[: lens[i], i, :240] for i in range(len(lens))])).cuda()
@@ -64,9 +67,9 @@ def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle):
             off = np.array([qsl.offsets[s] if s is not None else 0 for s in slot], np.int64) + pos
             T = max(int(cl.max()), 1)
             rd = torch.from_numpy(reset).cuda()
-            eng.encode_stream(qsl.feats, torch.from_numpy(np.where(busy, off, 0)).cuda(), torch.from_numpy(cl).cuda(),
-                              cl, rd, T, S, S)
-            eng.decode_stream(res, rl, rd)
+            enc, dec = (eng.encode_stream_pl, eng.decode_stream_pl) if pl else (eng.encode_stream, eng.decode_stream)
+            enc(qsl.feats, torch.from_numpy(np.where(busy, off, 0)).cuda(), torch.from_numpy(cl).cuda(), cl, rd, T, S, S)
+            dec(res, rl, rd)
             torch.cuda.synchronize()
             pos += cl
             remain -= cl
@@ -84,7 +87,8 @@ def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle):
         np.testing.assert_array_equal(got[q], want[q], err_msg=f"utterance {q} (len {lens[q]})")
 
 
-def test_config5_server_continuous_batching(pm, oracle):
+@pytest.mark.parametrize("pipelined", [False, True], ids=["rounds", "pipelined"])
+def test_config5_server_continuous_batching(pm, oracle, pipelined):
     count, n, qps = 2513, 1200, 3000.0
     lengths = synthetic.devclean_lengths(count, seed=4)
     qsl = GpuQSL(lengths, seed=4, device="cuda")
@@ -94,7 +98,7 @@ def test_config5_server_continuous_batching(pm, oracle):
     arrivals = np.cumsum(rng.exponential(1.0 / qps, size=n))
     qos = 460  # frames (the reference's QOS=233500 wav samples = 14.6 s)
     try:
-        srv = ServerSUT(engines, qsl, slots=512, split_len=32, qos_len=qos)
+        srv = ServerSUT(engines, qsl, slots=512, split_len=32, qos_len=qos, pipelined=pipelined)
         srv.start()
         t0 = time.perf_counter()
         i = 0

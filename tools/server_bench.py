@@ -37,7 +37,8 @@ def run_point(engines, qsl, qps, duration, max_batch, seed, args):
     if args.mode == "dynamic":
         sut = DynamicBatchServerSUT(engines, qsl, max_batch=max_batch)
     else:
-        sut = ServerSUT(engines, qsl, slots=max_batch, split_len=args.split_len, qos_len=args.qos_len)
+        sut = ServerSUT(engines, qsl, slots=max_batch, split_len=args.split_len, qos_len=args.qos_len,
+                        pipelined=args.pipelined)
     sut.start()
     rng = np.random.default_rng(seed)
     n = max(1, int(qps * duration))
@@ -84,6 +85,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=4,
                     help="engines (continuous: 4096 slots each); 4 measured best valid 80k QPS target vs 70k with 2 "
                          "(profiles/r02z_server_search_continuous*.json)")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="continuous: each engine encodes round k+1 while it decodes round k")
     ap.add_argument("--qsl", type=int, default=2513)
     ap.add_argument("--search", action="store_true", help="largest QPS with p99 <= 1000 ms")
     ap.add_argument("--seed", type=int, default=5)
@@ -116,6 +119,7 @@ def main():
     print(json.dumps({"scenario": "Server", "target_latency_ms": TARGET_LATENCY_S * 1e3, "percentile": PERCENTILE,
                       "duration_s": args.duration, "mode": args.mode, "slots_or_max_batch": args.max_batch,
                       "split_len": args.split_len if args.mode == "continuous" else None, "inflight": args.inflight,
+                      "pipelined": args.pipelined,
                       "best_valid_qps_per_gpu": best["target_qps"] if best else None, "points": points}))
     for e in engines:
         e.close()
