@@ -149,8 +149,9 @@ int rnnt_engine_decode_stream(rnnt_engine* e, int32_t* res, int32_t* res_len, in
  * it (encode_stream_pl blocks on the host until that decode has started); decode_stream_pl k must
  * be called after encode_stream_pl k returned, decodes in chunk order from one thread, encodes in
  * chunk order from one thread.  Chunk k's reset flags (read by its encode and its decode) must
- * stay unchanged until its decode has completed on the device.  Do not mix with the other encode /
- * decode calls on the same engine. */
+ * stay unchanged until its decode has completed on the device.  The first encode_stream_pl puts
+ * the engine in pipelined mode for good: its work is ordered after the engine's earlier calls, and
+ * from then on the other encode / decode / op calls on that engine return RNNT_EINVAL. */
 int rnnt_engine_encode_stream_pl(rnnt_engine* e, const float* store, const int64_t* offsets, const int32_t* lens,
                                  const int32_t* lens_host, const int32_t* reset, int T, int n, int n_pad,
                                  void* stream);

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <mutex>
@@ -87,6 +88,7 @@ struct rnnt_engine {
   hipEvent_t pl_copy_ev[2] = {nullptr, nullptr}, pl_handoff_ev = nullptr;
   int pl_meta[2][3] = {};  // (T, n, n_pad) of chunk k at k & 1
   int64_t pl_enc_k = 0, pl_dec_k = 0, pl_handoff_k = -1;
+  std::atomic<bool> pl_mode{false};  // set by the first pipelined call: the other calls then fail
   std::mutex pl_mu;
   std::condition_variable pl_cv;
   // profiling
@@ -494,6 +496,8 @@ static hipStream_t pick(rnnt_engine*, void* s) { return (hipStream_t)s; }
 
 // state_ev protocol (see rnnt_engine::state_ev)
 static int state_acquire(rnnt_engine* e, hipStream_t st) {
+  if (e->pl_mode.load(std::memory_order_acquire))
+    return fail(RNNT_EINVAL, "engine is in pipelined stream mode (rnnt_engine_encode_stream_pl)");
   if (e->state_rec && hipStreamWaitEvent(st, e->state_ev, 0) != hipSuccess)
     return fail(RNNT_EDEVICE, "hipStreamWaitEvent failed");
   return 0;
@@ -801,9 +805,10 @@ extern "C" int rnnt_engine_encode_stream_pl(rnnt_engine* e, const float* store, 
   for (int i = 0; i < n; ++i)
     if (lens_host[i] < 0 || lens_host[i] > T) return fail(RNNT_EINVAL, "a chunk length exceeds T");
   int r = 0;
-  {
+  if (!e->pl_mode.load(std::memory_order_acquire)) {  // first pipelined call: after the earlier calls' work
     DEVICE_SCOPE(e->device);
-    if ((r = pl_init(e))) return r;
+    if ((r = pl_init(e)) || (r = state_acquire(e, pick(e, stream)))) return r;
+    e->pl_mode.store(true, std::memory_order_release);
   }
   EncInput in;
   in.store = store;
@@ -837,6 +842,7 @@ extern "C" int rnnt_engine_decode_stream_pl(rnnt_engine* e, int32_t* res, int32_
   if (!e->xtab_ok || !e->joint1_loaded || !e->joint2_loaded)
     return fail(RNNT_EINVAL, "prediction (with embedding) / joint weights not loaded");
   if (max_res <= 0) return fail(RNNT_EINVAL, "max_res must be positive");
+  if (!e->pl_mode.load(std::memory_order_acquire)) return fail(RNNT_EINVAL, "decode_stream_pl before encode_stream_pl");
   const int64_t k = e->pl_dec_k;
   int T, n, n_pad;
   {

@@ -16,6 +16,7 @@ import pytest
 import torch
 
 from rnnt_amd import synthetic, weights
+from rnnt_amd._lib import EngineError
 from rnnt_amd.engine import Engine
 from rnnt_amd.sut import GpuQSL, OfflineSUT, QuerySample, ServerSUT, make_batches
 
@@ -79,6 +80,9 @@ def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl):
                 slot[i] = None
             rounds += 1
         assert rounds > len(lens) // nslot + 2  # utterances really spanned several chunks
+        if pl:  # the engine stays in pipelined mode: the round-form calls are refused
+            with pytest.raises(EngineError, match="pipelined"):
+                eng.decode_stream(res, rl, rd)
     finally:
         eng.close()
     want = _oracle_answers(oracle, pm, qsl, np.arange(len(lens)))
@@ -126,7 +130,9 @@ def test_config5_server_continuous_batching(pm, oracle, pipelined):
         assert len(srv.responses) == n and deferred == len(long_ids) > 0
         assert srv.rounds > 2 * 500 // 32  # chunked: the longest samples took >= 16 rounds
         # the Offline answers of the same samples (sorted batches of whole utterances)
-        off = OfflineSUT(engines[0], qsl, batch_size=512)
+        if pipelined:  # an engine that ran pipelined stream calls refuses the other calls
+            engines.append(Engine(pm, device=0, max_batch=512, max_frames=500))
+        off = OfflineSUT(engines[-1], qsl, batch_size=512)
         off.issue_batches(make_batches(qsl, np.arange(n), index, 512))
         offline = off.responses
     finally:
