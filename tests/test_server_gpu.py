@@ -53,6 +53,9 @@ def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl):
     try:
         res = torch.empty((S, eng.max_res), dtype=torch.int32, device="cuda")
         rl = torch.zeros(S, dtype=torch.int32, device="cuda")
+        if pl:  # a pipelined decode needs its chunk's pipelined encode first
+            with pytest.raises(EngineError, match="before encode_stream_pl"):
+                eng.decode_stream_pl(res, rl, torch.zeros(S, dtype=torch.int32, device="cuda"))
         queue = list(range(len(lens)))
         slot = [None] * S
         pos, remain = np.zeros(S, np.int64), np.zeros(S, np.int32)
@@ -80,7 +83,9 @@ def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl):
                 slot[i] = None
             rounds += 1
         assert rounds > len(lens) // nslot + 2  # utterances really spanned several chunks
-        if pl:  # the engine stays in pipelined mode: the round-form calls are refused
+        if pl:  # every chunk was decoded: one more decode has no chunk; round-form calls are refused
+            with pytest.raises(EngineError, match="before its chunk"):
+                eng.decode_stream_pl(res, rl, rd)
             with pytest.raises(EngineError, match="pipelined"):
                 eng.decode_stream(res, rl, rd)
     finally:
