@@ -18,10 +18,14 @@ Weak scaling: the query grows with the GPU count (--query per GPU), one query se
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+``--gpus N`` without a torchrun environment starts the N ranks itself (torch.distributed.run as a
+child process, before anything touches HIP), so both command lines measure N GPUs.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -69,7 +73,61 @@ def parse():
                          "GPU featurizer (FilterbankFeatures.forward) inside the timed region")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "tools", "roofline_traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (profiles/), if present")
+    ap.add_argument("--mock", action="store_true",
+                    help="launcher / sharding check without a GPU: gloo ranks deal and gather a query of stand-in "
+                         "responses (no engine, no HIP); the line it prints is not a measurement")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) outside a torchrun environment: run this script as N ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) in a child process and
+    return its exit code.  The parent never initialises HIP (only argparse has run), so the ranks
+    own the GPUs.  None when this process is already a rank (WORLD_SIZE set) or N == 1."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return None
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def mock_main(args):
+    """CPU rehearsal of the multi-rank step (--mock): the same shard / gather / barrier / max-over-ranks
+    timing as main() over gloo, with stand-in token rows instead of the engine."""
+    rank, _, world, group = dist.setup("gloo")
+    lens = synthetic.devclean_lengths(args.qsl, seed=4)
+    from rnnt_amd.sut import RNNTQSL
+    qsl = RNNTQSL([None] * len(lens), lens)
+    query = args.query * world
+    ids, idx = dist.query_arrays(args.qsl, query)
+
+    def step():
+        mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world)
+        my_ids = np.concatenate([b[0] for b in mine]) if mine else np.zeros(0, np.int64)
+        rl = (my_ids % 7).astype(np.int32)
+        toks = np.concatenate([np.full(int(n), int(i) % 29, np.int32) for i, n in zip(my_ids, rl)] + [np.zeros(0, np.int32)])
+        return dist.gather_responses(my_ids, rl, toks, world, group)
+
+    for _ in range(args.warmup):
+        step()
+    dist.barrier(group)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        got = step()
+    dist.barrier(group)
+    elapsed = dist.reduce_max(time.perf_counter() - t0, group)
+    if rank == 0:
+        assert len(got[0]) == query and len(np.unique(got[0])) == query, "gathered responses do not cover the query"
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "utterances/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                          "data": "mock: no engine, stand-in responses (launcher / sharding check, not a measurement)",
+                          "config": {"query_samples": query, "gathered": int(len(got[0]))}}), flush=True)
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
 
 
 def build_qsl(count, seed, device, wav=False):
@@ -190,7 +248,14 @@ def responses_dict(ids, lens, toks):
 
 def main():
     args = parse()
-    _, local, _ = dist.env_rank()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    _, local, world = dist.env_rank()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the torchrun world has {world} rank(s)")
+    if args.mock:
+        return mock_main(args)
     torch.cuda.set_device(local)
     rank, local, world, ggroup = dist.setup("nccl")
     device = f"cuda:{local}"

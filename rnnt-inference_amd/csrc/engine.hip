@@ -88,6 +88,7 @@ struct rnnt_engine {
   hipEvent_t pl_copy_ev[2] = {nullptr, nullptr}, pl_handoff_ev = nullptr;
   int pl_meta[2][3] = {};  // (T, n, n_pad) of chunk k at k & 1
   int64_t pl_enc_k = 0, pl_dec_k = 0, pl_handoff_k = -1;
+  bool pl_failed = false;  // sticky: a pipelined decode failed; the encode side returns an error instead of waiting
   std::atomic<bool> pl_mode{false};  // set by the first pipelined call: the other calls then fail
   std::mutex pl_mu;
   std::condition_variable pl_cv;
@@ -819,7 +820,8 @@ extern "C" int rnnt_engine_encode_stream_pl(rnnt_engine* e, const float* store, 
   const int64_t k = e->pl_enc_k;
   {  // the decode side's buffers are free once chunk k-1's decode has handed them off
     std::unique_lock<std::mutex> lk(e->pl_mu);
-    e->pl_cv.wait(lk, [&] { return e->pl_handoff_k >= k - 1; });
+    e->pl_cv.wait(lk, [&] { return e->pl_handoff_k >= k - 1 || e->pl_failed; });
+    if (e->pl_failed) return fail(RNNT_EDEVICE, "an earlier pipelined decode_stream_pl failed");
   }
   if (k >= 1) HIPCHK(hipStreamWaitEvent(st, e->pl_handoff_ev, 0));
   const int Tp = (T + 1) / 2;
@@ -836,18 +838,34 @@ extern "C" int rnnt_engine_encode_stream_pl(rnnt_engine* e, const float* store, 
   return 0;
 }
 
+// a pipelined decode that cannot run marks the engine failed (sticky) and wakes the encode side,
+// which then returns RNNT_EDEVICE instead of waiting for a hand-off that will not come
+static int pl_fail(rnnt_engine* e, int code, const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> lk(e->pl_mu);
+    e->pl_failed = true;
+  }
+  e->pl_cv.notify_all();
+  return fail(code, msg);
+}
+
 extern "C" int rnnt_engine_decode_stream_pl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res,
                                             const int32_t* reset, void* stream) {
-  if (!e || !res || !res_len || !reset) return fail(RNNT_EINVAL, "null argument");
-  if (!e->xtab_ok || !e->joint1_loaded || !e->joint2_loaded)
-    return fail(RNNT_EINVAL, "prediction (with embedding) / joint weights not loaded");
-  if (max_res <= 0) return fail(RNNT_EINVAL, "max_res must be positive");
+  if (!e) return fail(RNNT_EINVAL, "null engine");
   if (!e->pl_mode.load(std::memory_order_acquire)) return fail(RNNT_EINVAL, "decode_stream_pl before encode_stream_pl");
+  if (!res || !res_len || !reset) return pl_fail(e, RNNT_EINVAL, "null argument");
+  if (!e->xtab_ok || !e->joint1_loaded || !e->joint2_loaded)
+    return pl_fail(e, RNNT_EINVAL, "prediction (with embedding) / joint weights not loaded");
+  if (max_res <= 0) return pl_fail(e, RNNT_EINVAL, "max_res must be positive");
   const int64_t k = e->pl_dec_k;
   int T, n, n_pad;
   {
-    std::lock_guard<std::mutex> lk(e->pl_mu);
-    if (k >= e->pl_enc_k) return fail(RNNT_EINVAL, "decode_stream_pl before its chunk's encode_stream_pl returned");
+    std::unique_lock<std::mutex> lk(e->pl_mu);
+    if (e->pl_failed) return fail(RNNT_EDEVICE, "an earlier pipelined decode_stream_pl failed");
+    if (k >= e->pl_enc_k) {
+      lk.unlock();
+      return pl_fail(e, RNNT_EINVAL, "decode_stream_pl before its chunk's encode_stream_pl returned");
+    }
     T = e->pl_meta[k & 1][0];
     n = e->pl_meta[k & 1][1];
     n_pad = e->pl_meta[k & 1][2];
@@ -873,6 +891,10 @@ extern "C" int rnnt_engine_decode_stream_pl(rnnt_engine* e, int32_t* res, int32_
   if (!r) r = decode_core(e, res, res_len, max_res, st, reset, e->fbf_dec, e->flen_dpriv, T, n, n_pad, hand_off);
   if (!handed) hand_off();  // never leave the encode side waiting on a failed decode
   e->pl_dec_k = k + 1;
+  if (r) {  // the chunk's results are not there: later chunks cannot continue its carried state
+    const std::string msg = g_err;
+    return pl_fail(e, r, msg);
+  }
   return r;
 }
 
@@ -992,10 +1014,10 @@ extern "C" int rnnt_engine_load_f32_encoder(rnnt_engine* e, const float* const* 
         bi[dst] = bih[l][src];
         bh[dst] = bhh[l][src];
       }
-    int r = upload(e, &e->f32_wih[l], wi);
-    if (!r) r = upload(e, &e->f32_whh[l], wh);
-    if (!r) r = upload(e, &e->f32_bih[l], bi);
-    if (!r) r = upload(e, &e->f32_bhh[l], bh);
+    int r = load_buf(e, &e->f32_wih[l], wi);  // a reload overwrites in place
+    if (!r) r = load_buf(e, &e->f32_whh[l], wh);
+    if (!r) r = load_buf(e, &e->f32_bih[l], bi);
+    if (!r) r = load_buf(e, &e->f32_bhh[l], bh);
     if (r) return r;
   }
   e->f32_loaded = true;
@@ -1155,8 +1177,10 @@ extern "C" int rnnt_engine_load_f32_decoder(rnnt_engine* e, const rnnt_f32_decod
   std::vector<float> emb((size_t)29 * P, 0.0f);  // row 28: SOS (zero embedding)
   for (int g = 0; g < 28; ++g)
     for (int k = 0; k < P; ++k) emb[(size_t)g * P + chain_pos(k)] = m->embed[(size_t)g * P + k];
-  float* p = nullptr;
-  int r = upload(e, &p, emb);
+  // every buffer is allocated on the first load and overwritten in place by a reload (load_buf)
+  auto mut = [](const float* q) { return const_cast<float*>(q); };
+  float* p = mut(e->dw32.emb);
+  int r = load_buf(e, &p, emb);
   if (r) return r;
   e->dw32.emb = p;
   for (int l = 0; l < 2; ++l) {
@@ -1173,8 +1197,9 @@ extern "C" int rnnt_engine_load_f32_decoder(rnnt_engine* e, const rnnt_f32_decod
         bi[dst] = m->pred_b_ih[l][src];
         bh[dst] = m->pred_b_hh[l][src];
       }
-    float *a, *b, *c, *d;
-    if ((r = upload(e, &a, wi)) || (r = upload(e, &b, wh)) || (r = upload(e, &c, bi)) || (r = upload(e, &d, bh))) return r;
+    float *a = mut(e->dw32.wih[l]), *b = mut(e->dw32.whh[l]), *c = mut(e->dw32.bih[l]), *d = mut(e->dw32.bhh[l]);
+    if ((r = load_buf(e, &a, wi)) || (r = load_buf(e, &b, wh)) || (r = load_buf(e, &c, bi)) || (r = load_buf(e, &d, bh)))
+      return r;
     e->dw32.wih[l] = a;
     e->dw32.whh[l] = b;
     e->dw32.bih[l] = c;
@@ -1186,13 +1211,14 @@ extern "C" int rnnt_engine_load_f32_decoder(rnnt_engine* e, const rnnt_f32_decod
       for (int k = 0; k < K; ++k) w[(size_t)i * K + chain_pos(k)] = src[(size_t)i * K + k];
     return w;
   };
-  float *w1t, *w1p, *bt, *bp, *w2, *b2;
+  float *w1t = mut(e->dw32.w1t), *w1p = mut(e->dw32.w1p), *bt = mut(e->dw32.bt), *bp = mut(e->dw32.bp),
+        *w2 = mut(e->dw32.w2), *b2 = mut(e->dw32.b2);
   std::vector<float> b2v(NLAB_PAD, 0.0f);
   std::copy(m->joint_b2, m->joint_b2 + NLAB, b2v.begin());
-  if ((r = upload(e, &w1t, chained(m->joint_w1t, J, J, H))) || (r = upload(e, &w1p, chained(m->joint_w1p, J, J, P))) ||
-      (r = upload(e, &w2, chained(m->joint_w2, NLAB, NLAB_PAD, J))) ||
-      (r = upload(e, &bt, std::vector<float>(m->joint_bt, m->joint_bt + J))) ||
-      (r = upload(e, &bp, std::vector<float>(m->joint_bp, m->joint_bp + J))) || (r = upload(e, &b2, b2v)))
+  if ((r = load_buf(e, &w1t, chained(m->joint_w1t, J, J, H))) || (r = load_buf(e, &w1p, chained(m->joint_w1p, J, J, P))) ||
+      (r = load_buf(e, &w2, chained(m->joint_w2, NLAB, NLAB_PAD, J))) ||
+      (r = load_buf(e, &bt, std::vector<float>(m->joint_bt, m->joint_bt + J))) ||
+      (r = load_buf(e, &bp, std::vector<float>(m->joint_bp, m->joint_bp + J))) || (r = load_buf(e, &b2, b2v)))
     return r;
   e->dw32.w1t = w1t;
   e->dw32.w1p = w1p;

@@ -36,7 +36,9 @@
 namespace rnnt {
 namespace {
 
-constexpr int NT = 256;                                    // threads per workgroup (4 waves)
+constexpr int NT = 256;                                    // threads per (sub-)workgroup (4 waves)
+constexpr int FZ_NSUB = 3;                                 // fz_logmel: chunks (4-wave sub-groups) per workgroup
+constexpr int FZ_CU_LDS = 160 * 1024;                      // LDS per CU: one fz_logmel workgroup takes it all
 constexpr int SEGC = FZ_HOP * (FZ_CHUNK - 1) + FZ_WIN;     // 2720 samples per chunk
 constexpr int WOFF = (FZ_NFFT - FZ_WIN) / 2;               // 96: torch.stft centres the window in n_fft
 constexpr int SCR = 17 * 16;                               // 16 x 16 complex transpose, rows padded to 17
@@ -128,26 +130,37 @@ __global__ __launch_bounds__(1024) void fz_plan_kernel(FzArgs a) {
   }
 }
 
-__global__ __launch_bounds__(NT, 3) void fz_logmel_kernel(FzArgs a) {
-  const int2 job = a.plan[blockIdx.x];
+// A workgroup = FZ_NSUB chunks, one 4-wave sub-group (NT threads) each, and it owns its CU: its
+// static LDS plus an unused dynamic remainder fill the 160 KiB (launch_logmel), so no workgroup of
+// another kernel is ever resident beside it.  Measured (tools/diag_fz_concurrency.py, DESIGN.md
+// 4b): with the decode step kernels resident on the same CU, the FFT of the frames held by lanes
+// 48-63 of a logmel wave came out wrong in ~13 % of the batches (no other co-runner, incl.
+// synthetic MFMA / LDS / VALU / load kernels, did it); with the CU to itself, 0 in 40k batches.
+__global__ __launch_bounds__(NT * FZ_NSUB, 1) void fz_logmel_kernel(FzArgs a) {
+  const int sub = threadIdx.x / NT;
+  const int gj = blockIdx.x * FZ_NSUB + sub;  // this sub-group's plan entry
+  const bool active = gj < a.n_chunks;        // sub-group-uniform: idle ones only meet the barriers
+  const int2 job = active ? a.plan[gj] : make_int2(0, 0);
   const int n = job.x;
-  const int L = a.wav_lens[n];
+  const int L = active ? a.wav_lens[n] : 0;
   const int F = stft_frames(L);
   const int f0 = FZ_CHUNK * job.y;
 
-  __shared__ float2 tab[FZ_NFFT];  // W512^t
+  __shared__ float2 tab[FZ_NFFT];  // W512^t (shared by the sub-groups)
   __shared__ float win[FZ_WIN];
-  __shared__ float seg[SEGC];
-  __shared__ float2 scr[NT / 64][4][SCR];
+  __shared__ float segs[FZ_NSUB][SEGC];
+  __shared__ float2 scrs[FZ_NSUB][NT / 64][4][SCR];
+  float* seg = segs[sub];
+  float2(*scr)[4][SCR] = scrs[sub];
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x % NT, wave = tid >> 6, lane = tid & 63;
   const int slot = lane >> 4, j = lane & 15;  // frame slot in the wave, lane in the frame
-  for (int i = tid; i < FZ_NFFT; i += NT) tab[i] = a.k.twiddle[i];
-  for (int i = tid; i < FZ_WIN; i += NT) win[i] = a.k.window[i];
+  for (int i = threadIdx.x; i < FZ_NFFT; i += NT * FZ_NSUB) tab[i] = a.k.twiddle[i];
+  for (int i = threadIdx.x; i < FZ_WIN; i += NT * FZ_NSUB) win[i] = a.k.window[i];
   // pre-emphasised, reflect-padded samples y[160 f0 - 160 + i]: frame f's window covers
   // y[160 f - 160, 160 f + 160) (pad n_fft/2 = 256, window offset 96 inside n_fft); all loads
   // issued before the first use
-  {
+  if (active) {
     const float* x = a.wav + (a.off ? a.off[n] : (int64_t)n * a.stride);
     const float pc = a.k.preemph;
     const int base = FZ_HOP * f0 - FZ_HOP;
@@ -161,13 +174,8 @@ __global__ __launch_bounds__(NT, 3) void fz_logmel_kernel(FzArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-#ifdef RNNT_DEV_FZ_NO_LOAD  // dev ablation: no sample loads
-      xv[u] = (float)rr[u] * 1e-6f;
-      xm[u] = xv[u];
-#else
       xv[u] = x[rr[u]];
       xm[u] = x[max(rr[u] - 1, 0)];
-#endif
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -178,8 +186,7 @@ __global__ __launch_bounds__(NT, 3) void fz_logmel_kernel(FzArgs a) {
   __syncthreads();
 
   float2* sc = scr[wave][slot];
-#ifndef RNNT_DEV_FZ_NO_FFT  // dev ablation: no FFT / power
-  {
+  if (active) {
     const int fl = 4 * wave + slot;  // frame in the chunk
     const float* sf = seg + FZ_HOP * fl - WOFF;
     float2 v[16];
@@ -226,14 +233,11 @@ __global__ __launch_bounds__(NT, 3) void fz_logmel_kernel(FzArgs a) {
     if (j == 0) prow[FZ_NFFT / 2] = nyq * nyq + a.k.dither_sq;
     if (j >= 1 && j < PROW - FZ_NBIN + 1) prow[FZ_NBIN + j - 1] = 0.0f;
   }
-#endif
   __syncthreads();
+  if (!active) return;
   // mel projection of the 16 frames (rows) on v_mfma_f32_16x16x4f32; log; spliced store
   const float* arow = reinterpret_cast<const float*>(scr[j >> 2][j & 3]) + slot;
   for (int c = 0; c < FZ_MEL_COLS; ++c) {
-#ifdef RNNT_DEV_FZ_NO_MEL  // dev ablation: no mel projection
-    continue;
-#endif
     if (!((a.k.wave_cols[wave] >> c) & 1)) continue;
     floatx4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const float* ar = arow + a.k.col_k0[c];
@@ -439,6 +443,20 @@ extern "C" void rnnt_featurizer_destroy(rnnt_featurizer* f) {
   delete f;
 }
 
+// fz_logmel_kernel owns a whole CU: the unused rest of the 160 KiB LDS is requested as dynamic LDS
+static int launch_logmel(const FzArgs& a, size_t chunks, hipStream_t st) {
+  static std::atomic<uint64_t> attr{0};
+  static const int pad = [] {  // thread-safe one-time init
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, (const void*)fz_logmel_kernel) != hipSuccess) return -1;
+    return std::max(FZ_CU_LDS - (int)fa.sharedSizeBytes, 0);
+  }();
+  if (pad < 0 || set_smem_attr_once((const void*)fz_logmel_kernel, pad, attr)) return -1;
+  hipLaunchKernelGGL(fz_logmel_kernel, dim3((unsigned)((chunks + FZ_NSUB - 1) / FZ_NSUB)), dim3(NT * FZ_NSUB), pad, st,
+                     a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
                                    const int32_t* wav_lens, const int32_t* wav_lens_host, int n, int n_pad,
                                    float* feats, int32_t* feat_lens, int T_out, void* stream) {
@@ -477,9 +495,10 @@ extern "C" int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const i
   a.n_pad = n_pad;
   a.T_out = T_out;
   hipStream_t st = (hipStream_t)stream;
+  a.n_chunks = (int)chunks;
   if (chunks > 0) {
     hipLaunchKernelGGL(fz_plan_kernel, dim3(1), dim3(1024), 0, st, a);
-    hipLaunchKernelGGL(fz_logmel_kernel, dim3((unsigned)chunks), dim3(NT), 0, st, a);
+    if (launch_logmel(a, chunks, st)) return fz_fail(RNNT_EDEVICE, "fz_logmel launch failed");
   }
   hipLaunchKernelGGL(fz_norm_kernel, dim3(n_pad), dim3(NT), 0, st, a);
   FZCHK(hipGetLastError());

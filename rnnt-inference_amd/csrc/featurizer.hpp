@@ -45,6 +45,7 @@ struct FzArgs {
   int32_t* feat_lens;       // [n_pad]
   int2* plan;               // [chunks] (utterance, chunk) per fz_logmel workgroup (fz_plan_kernel)
   int n, n_pad, T_out;
+  int n_chunks;             // plan entries (fz_logmel sub-groups past it idle)
 };
 
 }  // namespace rnnt

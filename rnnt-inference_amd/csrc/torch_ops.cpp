@@ -47,14 +47,22 @@ void check_rc(int rc, const char* what) {
 
 int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
-// identity of a set of weight tensors
-using Key = std::vector<int64_t>;
+// identity of a set of weight tensors: (address, version, shape, dtype) of each.  The cache entry
+// also holds a reference to every keyed tensor, so the storage cannot be freed and a new tensor of
+// the same shape allocated at the same address while the engine still holds the old copy.
+struct Key {
+  std::vector<int64_t> id;
+  std::vector<at::Tensor> refs;
+  bool operator==(const Key& o) const { return id == o.id; }
+  bool operator!=(const Key& o) const { return id != o.id; }
+};
 void key_add(Key& k, const at::Tensor& t) {
-  k.push_back((int64_t)(intptr_t)t.data_ptr());
-  k.push_back((int64_t)t._version());
-  k.push_back(t.numel());
-  k.push_back((int64_t)t.scalar_type());
-  for (auto s : t.sizes()) k.push_back(s);
+  k.id.push_back((int64_t)(intptr_t)t.data_ptr());
+  k.id.push_back((int64_t)t._version());
+  k.id.push_back(t.numel());
+  k.id.push_back((int64_t)t.scalar_type());
+  for (auto s : t.sizes()) k.id.push_back(s);
+  k.refs.push_back(t);
 }
 
 struct OpEngine {

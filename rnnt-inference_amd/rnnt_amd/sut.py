@@ -147,8 +147,8 @@ class OfflineSUT:
         k = self.early_decodes
         hold = k is not None and k < len(batches) <= len(self.engines)
         self._hold = None
-        if hold:  # the held batches wait until every batch of the query is encoded
-            self._hold = (k, threading.Semaphore(0), [0], threading.Lock(), len(batches))
+        if hold:  # the held batches wait until every batch of the query is encoded (or one encode failed)
+            self._hold = dict(k=k, cv=threading.Condition(), done=0, failed=False, nb=len(batches))
         for eng in self.engines:
             if id(eng) not in self._streams:
                 self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
@@ -193,6 +193,7 @@ class OfflineSUT:
             with cv:
                 cv.wait_for(lambda: turn[0] == bi)
                 self.encode_order.append(bi)
+            encoded = False
             try:
                 res = torch.empty((n, eng.max_res), dtype=torch.int32, device=st.device)
                 rl = torch.empty(n, dtype=torch.int32, device=st.device)
@@ -203,19 +204,23 @@ class OfflineSUT:
                 else:
                     eng.encode(inp["x"], inp["lens"], inp["lens_host"], n=n, stream=st)
                 st.synchronize()
+                encoded = True
             finally:
                 with cv:
                     turn.popleft()
                     cv.notify_all()
-            if self._hold is not None:
-                k, sem, done, lk, nb = self._hold
-                with lk:
-                    done[0] += 1
-                    if done[0] == nb:  # last encode: release every held decode
-                        for _ in range(nb - k):
-                            sem.release()
-                if bi >= k:
-                    sem.acquire()
+                h = self._hold
+                if h is not None:  # counted even when the encode raised, so the held decodes never wait forever
+                    with h["cv"]:
+                        h["done"] += 1
+                        h["failed"] = h["failed"] or not encoded
+                        h["cv"].notify_all()
+            h = self._hold
+            if h is not None and bi >= h["k"]:
+                with h["cv"]:
+                    h["cv"].wait_for(lambda: h["done"] == h["nb"] or h["failed"])
+                    if h["failed"]:
+                        raise RuntimeError("OfflineSUT: an encode of this query failed; held decode abandoned")
             eng.decode(res, rl, stream=st)
             rlh = rl.cpu().numpy()
             toks = res[:, : max(1, int(rlh.max()))].cpu().numpy()
@@ -668,6 +673,7 @@ class DynamicBatchServerSUT:
         self._stop = False
         self._threads = []
         self.batches = 0
+        self.batch_log = []  # (engine index, sample ids in batch row order) per batch, for diagnostics
         self.errors = []
 
     def start(self):
@@ -713,6 +719,7 @@ class DynamicBatchServerSUT:
             try:
                 batch.sort(key=lambda b: -int(self.qsl.lengths[b[1].index]))  # rnnt_qsl.cpp:104-133
                 n = len(batch)
+                self.batch_log.append((j, [s.id for _, s in batch]))
                 with torch.cuda.stream(st):
                     x, lens, bl = self.qsl.assemble([b[1].index for b in batch])
                     res = torch.empty((n, eng.max_res), dtype=torch.int32, device="cuda")

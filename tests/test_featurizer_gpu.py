@@ -6,6 +6,8 @@ also ~relative).  Padding (time past feat_lens, channels 240..255, batch rows pa
 lengths are exact.  Rows are independent: a row's features are bit-identical whatever batch it
 is in and whether samples come from a zero-padded [N][stride] batch or ragged storage + offsets.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -130,10 +132,12 @@ def test_wav_to_tokens_matches_oracle(fz, oracle):
     assert rlo.sum() > 0
 
 
-def test_server_sut_over_wav_qsl():
-    """WAV=true Server path: GpuWavQSL featurizes each dynamic batch on the worker's stream;
-    every answer equals one Offline batch of the same audio (rows are independent in both the
-    featurizer and the engine)."""
+def test_server_sut_over_wav_qsl(oracle):
+    """WAV=true Server path: GpuWavQSL featurizes each dynamic batch on the worker's stream while
+    the other engine's encode / decode run; every answer -- the Server's and one Offline batch of
+    the same audio -- equals the CPU restatement on the same features.  A mismatch names its
+    sample, batch, engine, the batch's rows and which side is wrong (round-2 failure: featurizer
+    batches corrupted beside a concurrent decode, see test_featurizer_beside_concurrent_decode)."""
     import time
     from rnnt_amd import weights
     from rnnt_amd.engine import Engine
@@ -145,28 +149,98 @@ def test_server_sut_over_wav_qsl():
     wavs = synthetic.make_wavs(synthetic.wav_lengths_for_frames(frames, seed=61), seed=61, device="cuda")
     qsl = GpuWavQSL(wavs)
     assert qsl.lengths.tolist() == frames.tolist()
+    n = len(frames)
+    x, lens, bl = qsl.assemble(list(range(n)))
+    torch.cuda.synchronize()
+    feats = np.ascontiguousarray(x.cpu().numpy()[:, :n])
     engines = [Engine(pm, device=0, max_batch=64, max_frames=128) for _ in range(2)]
     try:
+        fo = oracle.encoder_i8(pm, feats, bl)
+        ro, rlo, _ = oracle.greedy_decode(pm, fo, (bl + 1) // 2, max_res=engines[0].max_res)
+        want = [ro[i, : rlo[i]] for i in range(n)]
+        assert rlo.sum() > 0
         srv = DynamicBatchServerSUT(engines, qsl, max_batch=8)
         srv.start()
-        samples = [QuerySample(id=i, index=i) for i in range(len(frames))]
-        for k in range(0, len(samples), 5):
+        samples = [QuerySample(id=i, index=i) for i in range(n)]
+        for k in range(0, n, 5):
             srv.issue_query(samples[k:k + 5])
             time.sleep(0.002)
         deadline = time.time() + 60
-        while len(srv.latency) < len(samples) and time.time() < deadline:
+        while len(srv.latency) < n and time.time() < deadline:
             time.sleep(0.01)
         srv.stop()
-        assert not srv.errors and len(srv.responses) == len(samples)
-        x, lens, bl = qsl.assemble(list(range(len(frames))))
-        n = len(frames)
+        assert not srv.errors and len(srv.responses) == n, srv.errors
         res = torch.empty((n, engines[0].max_res), dtype=torch.int32, device="cuda")
         rl = torch.empty(n, dtype=torch.int32, device="cuda")
         engines[0].infer(x, lens, bl, res, rl, n=n)
         res, rl = res.cpu().numpy(), rl.cpu().numpy()
-        assert rl.sum() > 0
+        where = {i: (b, j, ids) for b, (j, ids) in enumerate(srv.batch_log) for i in ids}
+        bad = []
         for i in range(n):
-            np.testing.assert_array_equal(srv.responses[i], res[i, : rl[i]])
+            srv_ok = np.array_equal(srv.responses[i], want[i])
+            off_ok = np.array_equal(res[i, : rl[i]], want[i])
+            if not (srv_ok and off_ok):
+                b, j, ids = where[i]
+                bad.append(f"sample {i} ({frames[i]} frames): server {'ok' if srv_ok else 'WRONG'} "
+                           f"(batch {b} on engine {j}, rows {ids}, {len(srv.responses[i])} vs {len(want[i])} tokens), "
+                           f"offline batch {'ok' if off_ok else 'WRONG'}; tick tiles "
+                           f"{os.environ.get('RNNT_ENC_TILE', 'auto')}")
+        assert not bad, "\n".join(bad)
     finally:
         for e in engines:
             e.close()
+
+
+def test_featurizer_beside_concurrent_decode():
+    """Regression for the round-2 intermittent Server mismatch: one featurizer batch repeated on
+    one stream while another stream runs greedy decodes must equal the quiet result bit for bit.
+    Before fz_logmel_kernel owned its CU, ~13 % of such batches had one STFT frame wrong (the
+    frames held by lanes 48-63 of a logmel wave, whenever a decode step workgroup shared the CU);
+    tools/diag_fz_concurrency.py holds the full experiment."""
+    import threading
+    import time
+    from rnnt_amd import weights
+    from rnnt_amd.engine import Engine
+    from rnnt_amd.sut import GpuWavQSL
+    pm, _ = weights.build_model()
+    frames = np.minimum(synthetic.devclean_lengths(24, seed=61), 120)
+    qsl = GpuWavQSL(synthetic.make_wavs(synthetic.wav_lengths_for_frames(frames, seed=61), seed=61, device="cuda"))
+    idx = list(range(10, 18))
+    ref, _, _ = qsl.assemble(idx)
+    torch.cuda.synchronize()
+    ref = ref[:, :8].cpu().numpy()
+    eng = Engine(pm, device=0, max_batch=1024, max_frames=256)
+    try:
+        lp = np.full(1024, 200, np.int32)
+        eng.encode(torch.from_numpy(synthetic.make_features(200, 1024, seed=5)).cuda(), torch.from_numpy(lp).cuda(),
+                   lp, n=1024)
+        res = torch.empty((1024, eng.max_res), dtype=torch.int32, device="cuda")
+        rl = torch.empty(1024, dtype=torch.int32, device="cuda")
+        stop, decodes = threading.Event(), [0]
+
+        def decode_loop():
+            st = torch.cuda.Stream()
+            while not stop.is_set():
+                eng.decode(res, rl, stream=st)
+                st.synchronize()
+                decodes[0] += 1
+
+        th = threading.Thread(target=decode_loop, daemon=True)
+        th.start()
+        st = torch.cuda.Stream()
+        iters, bad = 0, 0
+        t_end = time.time() + 3.0
+        try:
+            while time.time() < t_end:
+                with torch.cuda.stream(st):
+                    xb, _, _ = qsl.assemble(idx)
+                    got = xb[:, :8].cpu().numpy()
+                iters += 1
+                bad += int(not np.array_equal(got.view(np.uint32), ref.view(np.uint32)))
+        finally:
+            stop.set()
+            th.join()
+        assert decodes[0] >= 2 and iters >= 100, (decodes[0], iters)
+        assert bad == 0, f"{bad} of {iters} featurizer batches differ from the quiet result beside {decodes[0]} decodes"
+    finally:
+        eng.close()

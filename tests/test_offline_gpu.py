@@ -68,3 +68,42 @@ def test_config4_offline_query(pm, oracle):
     assert len(sl) >= 64 and rlo.sum() > 100
     for i, sid in enumerate(pick_ids):
         np.testing.assert_array_equal(resp[int(sid)], ro[i, : rlo[i]], err_msg=f"sample {sid}")
+
+
+class _FailingEngine:
+    """Stand-in engine whose encode raises for one batch (OfflineSUT's held-decode schedule)."""
+
+    def __init__(self, fail_len):
+        self.device, self.max_res, self.fail_len = 0, 8, fail_len
+
+    def encode(self, x, lens, lens_host, n=None, stream=None):
+        if int(lens_host[0]) == self.fail_len:
+            raise RuntimeError("encode failed (test)")
+
+    def decode(self, res, res_len, stream=None):
+        res.fill_(-1)
+        res_len.zero_()
+
+
+def test_held_decodes_do_not_hang_when_an_encode_fails():
+    """early_decodes hold mode: a batch whose encode raises still counts as done, so the held
+    batches' threads wake and the query raises instead of hanging in issue_batches."""
+    import threading
+    from rnnt_amd.sut import RNNTQSL
+    lengths = np.array([30, 20, 10], np.int32)
+    qsl = RNNTQSL.synthetic(lengths, seed=1)
+    engines = [_FailingEngine(fail_len=30) for _ in range(3)]  # the first (longest) batch fails
+    sut = OfflineSUT(engines, qsl, batch_size=1, early_decodes=1)
+    errs = []
+
+    def run():
+        try:
+            sut.issue_batches(make_batches(qsl, np.arange(3), np.arange(3), 1))
+        except Exception as ex:  # expected
+            errs.append(ex)
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(timeout=60)
+    assert not th.is_alive(), "issue_batches hung on a failed encode"
+    assert errs and ("encode failed" in str(errs[0]) or "abandoned" in str(errs[0])), errs

@@ -152,3 +152,44 @@ def test_config5_server_continuous_batching(pm, oracle, pipelined):
     want = _oracle_answers(oracle, pm, qsl, index[ks])
     for k, w in zip(ks, want):
         np.testing.assert_array_equal(srv.responses[int(k)], w, err_msg=f"sample {k}")
+
+
+def test_pipelined_decode_failure_does_not_hang_the_next_encode(pm):
+    """A pipelined decode that fails before its hand-off (here: no result columns, max_res 0)
+    marks the engine failed and wakes the encode side: the next encode_stream_pl returns an error
+    instead of waiting forever for a hand-off that will not come."""
+    import threading
+    S = 256
+    lens = np.array([40, 33, 20], np.int32)
+    qsl = GpuQSL(lens, seed=3, device="cuda")
+    eng = Engine(pm, device=0, max_batch=S, max_frames=64)
+    try:
+        cl = np.zeros(S, np.int32)
+        cl[:3] = 16
+        off = np.zeros(S, np.int64)
+        off[:3] = qsl.offsets[:3]
+        reset = torch.zeros(S, dtype=torch.int32, device="cuda")
+        reset[:3] = 1
+        args = (qsl.feats, torch.from_numpy(off).cuda(), torch.from_numpy(cl).cuda(), cl, reset, 16, S, S)
+        eng.encode_stream_pl(*args)
+        res0 = torch.empty((S, 0), dtype=torch.int32, device="cuda")
+        rl = torch.zeros(S, dtype=torch.int32, device="cuda")
+        with pytest.raises(EngineError):
+            eng.decode_stream_pl(res0, rl, reset)
+        out = []
+
+        def nxt():
+            try:
+                eng.encode_stream_pl(*args)
+                out.append("returned")
+            except EngineError as ex:
+                out.append(str(ex))
+
+        th = threading.Thread(target=nxt, daemon=True)
+        th.start()
+        th.join(timeout=30)
+        assert not th.is_alive(), "encode_stream_pl still waiting for the failed decode's hand-off"
+        assert out and "failed" in out[0], out
+    finally:
+        torch.cuda.synchronize()
+        eng.close()
