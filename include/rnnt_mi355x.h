@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RNNT_ABI_VERSION 7
+#define RNNT_ABI_VERSION 8
 
 #define RNNT_OK 0
 #define RNNT_EINVAL (-22)
@@ -257,6 +257,39 @@ int rnnt_op_greedy_update(rnnt_engine* e, const void* symbols, int symbols_i64, 
                           int32_t* res_idx, const float* f, int f_batch, const int32_t* f_lens, int32_t* time_idx,
                           float* fi, int32_t* pre_g, uint16_t* const* pre_hg, float* const* pre_cg,
                           const uint16_t* const* hg, const float* const* cg, int n, int max_res, void* stream);
+
+/* ---- operator-level fp32 prediction LSTM (intel_mlperf::lstm, modeling_rnnt.py:204, the
+ * run_mode="f32" decoder): weights natural fp32 [1280][320] per layer (torch.nn.LSTM gate order
+ * i, f, g, o), b_ih / b_hh [1280].  The same k-ordered fp32 chains as rnnt_engine_decode_f32. */
+int rnnt_engine_load_f32_prediction(rnnt_engine* e, const float* const* w_ih, const float* const* w_hh,
+                                    const float* const* b_ih, const float* const* b_hh);
+/* x fp32 [n_pad][320] (embedding rows, zero for SOS), hx / cx fp32 [2][n_pad][320] -> hy, cy (same
+ * shapes, must not alias the inputs); g = hy[1].  n_pad a multiple of 64. */
+int rnnt_op_lstm_f32(rnnt_engine* e, const float* x, const float* hx, const float* cx, float* hy, float* cy,
+                     int n_pad, void* stream);
+
+/* ---- the audio processor's plugin operators one at a time (features.py:196-250; the graph
+ * processor_jit.pt binds to; the fused rnnt_featurizer_run below is the throughput path).  No
+ * engine needed; all device pointers, fp32 unless stated. */
+/* preemphasis(x, x_lens, coeff, pad_size): row n (len lens[n] <= stride, at x + n * stride) ->
+ * y [n][L_out]: y[p] = z[mirror(p - pad)] for p < len + 2 pad, z[0] = x[0], z[t] = x[t] - coeff
+ * x[t-1] (torch reflect padding, periodic for short rows), 0 past it. */
+int rnnt_op_preemphasis(const float* x, int64_t stride, const int32_t* lens, int n, int L_out, float coeff, int pad,
+                        float* y, void* stream);
+/* power_spectrum(x, x_lens): x [n][T][bins][2] (re, im) -> y [n][T][bins] = re^2 + im^2 for frames
+ * t < frames[n], 0 after. */
+int rnnt_op_power_spectrum(const float* x, const int32_t* frames, int n, int T, int bins, float* y, void* stream);
+/* frame_splicing(x, x_lens, factor): x [n][C][T] -> y [n][C factor][ceil(T / factor)],
+ * y[q C + m][t] = x[m][factor t + q] for stacked frames < frames[n], 0 otherwise. */
+int rnnt_op_frame_splicing(const float* x, const int32_t* frames, int n, int C, int T, int factor, float* y,
+                           void* stream);
+/* i_layernorm_pad(x, weight, bias, x_lens, eps, unbiased, output_shape): x [n][C][T], weight / bias
+ * [C_out][wt] -> y [n_out][C_out][T]: per row and channel over its lens[n] valid frames,
+ * (x - mean) / sqrt(var + eps) * weight + bias (var unbiased when asked; 0 for one frame), zero past
+ * the length, in channels >= C and rows >= n; lens_out int32 [n_out]. */
+int rnnt_op_layernorm_pad(const float* x, const float* weight, const float* bias, int wt, const int32_t* lens, int n,
+                          int C, int T, int n_out, int C_out, float eps, int unbiased, float* y, int32_t* lens_out,
+                          void* stream);
 
 /* ---- audio front end (the reference's AudioProcessor / FilterbankFeatures.forward,
  * datasets/parts/features.py:185-252, csrc/rnnt_processor.hpp:29-48; used when WAV=true,

@@ -191,6 +191,70 @@ __global__ void dec32_finish_kernel(DecF32Args a) {
   if (n < a.N) a.res_len[n] = a.s.idx[n] + 1;
 }
 
+// intel_mlperf::lstm, one layer (modeling_rnnt.py:204, the run_mode="f32" prediction LSTM) for
+// n_pad rows on natural-layout operands: the same two k-ordered chains as dec32_pred_kernel
+// (b_ih + x.W_ih^T and b_hh + h.W_hh^T, v_mfma_f32_16x16x4_f32), with each lane's chain-ordered
+// operands (natural k = 32 blk + 4 i + q, i = 0..7) gathered from the rows; then the cell.
+__global__ void __launch_bounds__(256) op_lstm_f32_kernel(DecF32Weights w, int L, const float* __restrict__ x,
+                                                          const float* __restrict__ h_in,
+                                                          const float* __restrict__ c_in, float* __restrict__ h_out,
+                                                          float* __restrict__ c_out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
+  const int gt = blockIdx.x * 4 + wave;
+  const int n0 = blockIdx.y * 64;
+  const float4 bi = *(const float4*)(w.bih[L] + gt * 16 + 4 * q);
+  const float4 bh = *(const float4*)(w.bhh[L] + gt * 16 + 4 * q);
+  v4f ax[4], ah[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ax[j] = v4f{bi.x, bi.y, bi.z, bi.w};
+    ah[j] = v4f{bh.x, bh.y, bh.z, bh.w};
+  }
+  const float* wx = w.wih[L] + (size_t)(gt * 16 + c) * P + 8 * q;
+  const float* wh = w.whh[L] + (size_t)(gt * 16 + c) * P + 8 * q;
+  for (int blk = 0; blk < P / 32; ++blk) {
+    const float4 x0 = *(const float4*)(wx + 32 * blk), x1 = *(const float4*)(wx + 32 * blk + 4);
+    const float4 h0 = *(const float4*)(wh + 32 * blk), h1 = *(const float4*)(wh + 32 * blk + 4);
+    const float wxv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    const float whv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const size_t r = (size_t)(n0 + j * 16 + c) * P + 32 * blk + q;
+      float xv[8], hv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xv[i] = x[r + 4 * i];
+        hv[i] = h_in[r + 4 * i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        ax[j] = MFMA4(wxv[i], xv[i], ax[j]);
+        ah[j] = MFMA4(whv[i], hv[i], ah[j]);
+      }
+    }
+  }
+  const int u = gt * 4 + q;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t o = (size_t)(n0 + j * 16 + c) * P + u;
+    const float ig = det_sigmoid(ax[j][0] + ah[j][0]);
+    const float fg = det_sigmoid(ax[j][1] + ah[j][1]);
+    const float gg = det_tanh(ax[j][2] + ah[j][2]);
+    const float og = det_sigmoid(ax[j][3] + ah[j][3]);
+    const float cn = fg * c_in[o] + ig * gg;
+    c_out[o] = cn;
+    h_out[o] = og * det_tanh(cn);
+  }
+}
+
+int launch_op_lstm_f32(const DecF32Weights& w, int layer, const float* x, const float* h_in, const float* c_in,
+                       float* h_out, float* c_out, int n_pad, hipStream_t st) {
+  if (n_pad <= 0 || n_pad % 64) return -1;
+  hipLaunchKernelGGL(op_lstm_f32_kernel, dim3(PG4 / 64, n_pad / 64), dim3(256), 0, st, w, layer, x, h_in, c_in, h_out,
+                     c_out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 // F[r][j] = b_t[j] + chain_k fc[r][k] W1t[j][k] for all rows r of [Tp][Npad]: wave = one 16-column
 // tile (A = W1t rows), 4 row tiles of 16 (B = frame rows).
 __global__ void __launch_bounds__(256) dec32_F_kernel(DecF32Weights w, const float* __restrict__ fc,

@@ -44,5 +44,9 @@ int launch_f32_joint_trans(const DecF32Weights& w, const float* fc, float* F, in
 // Lock-step greedy loop over the whole batch; polls the unfinished-row counter one 32-step
 // chunk behind (host_flags: 2 pinned words, evs: 2 events).  Returns the steps enqueued or -1.
 int launch_greedy_decode_f32(const DecF32Args& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st);
+// One fp32 prediction LSTM layer (intel_mlperf::lstm) over n_pad rows (a multiple of 64), natural
+// layouts: x / h_in / c_in / h_out / c_out fp32 [n_pad][320]; h_out, c_out must not alias inputs.
+int launch_op_lstm_f32(const DecF32Weights& w, int layer, const float* x, const float* h_in, const float* c_in,
+                       float* h_out, float* c_out, int n_pad, hipStream_t st);
 
 }  // namespace rnnt

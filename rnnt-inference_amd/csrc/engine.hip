@@ -105,7 +105,7 @@ struct rnnt_engine {
   float *f32_x = nullptr, *f32_ya = nullptr, *f32_xs = nullptr, *f32_yb = nullptr, *f32_yc = nullptr;
   float *f32_h[5][2] = {}, *f32_c[5] = {};  // per layer: the wavefront ticks run the layers concurrently
   // fp32 decoder (rnnt_engine_load_f32_decoder) and the last fp32 encode's outputs it decodes
-  bool f32_dec_loaded = false;
+  bool f32_dec_loaded = false, f32_pred_loaded = false;
   DecF32Weights dw32{};
   float *f32_fc = nullptr, *f32_F = nullptr;
   int32_t* f32_flen = nullptr;
@@ -1169,6 +1169,58 @@ extern "C" int rnnt_engine_encode_f32(rnnt_engine* e, const float* feats, const 
   return state_release(e, st);
 }
 
+// fp32 prediction LSTM weights (natural [1280][320] per layer, torch.nn.LSTM gate order) into the
+// fp32 decoder's layout: gate-interleaved rows, chain-permuted k; reloads overwrite in place
+static int load_f32_pred(rnnt_engine* e, const float* const* w_ih, const float* const* w_hh, const float* const* b_ih,
+                         const float* const* b_hh) {
+  auto mut = [](const float* q) { return const_cast<float*>(q); };
+  for (int l = 0; l < 2; ++l) {
+    if (!w_ih[l] || !w_hh[l] || !b_ih[l] || !b_hh[l]) return fail(RNNT_EINVAL, "null fp32 prediction weight");
+    std::vector<float> wi((size_t)PG4 * P), wh((size_t)PG4 * P), bi(PG4), bh(PG4);
+    for (int g = 0; g < 4; ++g)
+      for (int u = 0; u < P; ++u) {
+        const int src = g * P + u, dst = 4 * u + g;  // gate-interleaved rows
+        for (int k = 0; k < P; ++k) {
+          wi[(size_t)dst * P + chain_pos(k)] = w_ih[l][(size_t)src * P + k];
+          wh[(size_t)dst * P + chain_pos(k)] = w_hh[l][(size_t)src * P + k];
+        }
+        bi[dst] = b_ih[l][src];
+        bh[dst] = b_hh[l][src];
+      }
+    float *a = mut(e->dw32.wih[l]), *b = mut(e->dw32.whh[l]), *c = mut(e->dw32.bih[l]), *d = mut(e->dw32.bhh[l]);
+    int r;
+    if ((r = load_buf(e, &a, wi)) || (r = load_buf(e, &b, wh)) || (r = load_buf(e, &c, bi)) || (r = load_buf(e, &d, bh)))
+      return r;
+    e->dw32.wih[l] = a;
+    e->dw32.whh[l] = b;
+    e->dw32.bih[l] = c;
+    e->dw32.bhh[l] = d;
+  }
+  e->f32_pred_loaded = true;
+  return 0;
+}
+
+extern "C" int rnnt_engine_load_f32_prediction(rnnt_engine* e, const float* const* w_ih, const float* const* w_hh,
+                                               const float* const* b_ih, const float* const* b_hh) {
+  if (!e || !w_ih || !w_hh || !b_ih || !b_hh) return fail(RNNT_EINVAL, "null argument");
+  DEVICE_SCOPE(e->device);
+  return load_f32_pred(e, w_ih, w_hh, b_ih, b_hh);
+}
+
+extern "C" int rnnt_op_lstm_f32(rnnt_engine* e, const float* x, const float* hx, const float* cx, float* hy, float* cy,
+                                int n_pad, void* stream) {
+  if (!e || !x || !hx || !cx || !hy || !cy) return fail(RNNT_EINVAL, "null argument");
+  if (!e->f32_pred_loaded) return fail(RNNT_EINVAL, "fp32 prediction weights not loaded (rnnt_engine_load_f32_prediction)");
+  if (n_pad <= 0 || n_pad % 64) return fail(RNNT_EINVAL, "n_pad must be a positive multiple of 64");
+  DEVICE_SCOPE(e->device);
+  hipStream_t st = pick(e, stream);
+  const size_t NP = (size_t)n_pad * P;
+  if (launch_op_lstm_f32(e->dw32, 0, x, hx, cx, hy, cy, n_pad, st) ||
+      launch_op_lstm_f32(e->dw32, 1, hy, hx + NP, cx + NP, hy + NP, cy + NP, n_pad, st))
+    return fail(RNNT_EDEVICE, "lstm_f32 launch failed");
+  return 0;
+}
+
 extern "C" int rnnt_engine_load_f32_decoder(rnnt_engine* e, const rnnt_f32_decoder_desc* m) {
   if (!e || !m || !m->embed || !m->joint_w1t || !m->joint_w1p || !m->joint_bt || !m->joint_bp || !m->joint_w2 ||
       !m->joint_b2)
@@ -1183,28 +1235,7 @@ extern "C" int rnnt_engine_load_f32_decoder(rnnt_engine* e, const rnnt_f32_decod
   int r = load_buf(e, &p, emb);
   if (r) return r;
   e->dw32.emb = p;
-  for (int l = 0; l < 2; ++l) {
-    if (!m->pred_w_ih[l] || !m->pred_w_hh[l] || !m->pred_b_ih[l] || !m->pred_b_hh[l])
-      return fail(RNNT_EINVAL, "null fp32 prediction weight");
-    std::vector<float> wi((size_t)PG4 * P), wh((size_t)PG4 * P), bi(PG4), bh(PG4);
-    for (int g = 0; g < 4; ++g)
-      for (int u = 0; u < P; ++u) {
-        const int src = g * P + u, dst = 4 * u + g;  // gate-interleaved rows
-        for (int k = 0; k < P; ++k) {
-          wi[(size_t)dst * P + chain_pos(k)] = m->pred_w_ih[l][(size_t)src * P + k];
-          wh[(size_t)dst * P + chain_pos(k)] = m->pred_w_hh[l][(size_t)src * P + k];
-        }
-        bi[dst] = m->pred_b_ih[l][src];
-        bh[dst] = m->pred_b_hh[l][src];
-      }
-    float *a = mut(e->dw32.wih[l]), *b = mut(e->dw32.whh[l]), *c = mut(e->dw32.bih[l]), *d = mut(e->dw32.bhh[l]);
-    if ((r = load_buf(e, &a, wi)) || (r = load_buf(e, &b, wh)) || (r = load_buf(e, &c, bi)) || (r = load_buf(e, &d, bh)))
-      return r;
-    e->dw32.wih[l] = a;
-    e->dw32.whh[l] = b;
-    e->dw32.bih[l] = c;
-    e->dw32.bhh[l] = d;
-  }
+  if ((r = load_f32_pred(e, m->pred_w_ih, m->pred_w_hh, m->pred_b_ih, m->pred_b_hh))) return r;
   auto chained = [](const float* src, int rows, int rows_pad, int K) {
     std::vector<float> w((size_t)rows_pad * K, 0.0f);
     for (int i = 0; i < rows; ++i)

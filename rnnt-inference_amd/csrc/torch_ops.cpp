@@ -17,6 +17,17 @@
 //                        Tensor[] pre_cg, Tensor[] hg, Tensor[] cg) -> bool
 //   prepack_lstm_weights(Tensor w_ih, Tensor w_hh) -> (Tensor, Tensor)   (identity: the engine packs)
 //   prepack_linear_weight(Tensor w) -> Tensor                           (identity)
+//   lstm(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights) -> (Tensor, Tensor[], Tensor[])   (fp32,
+//        modeling_rnnt.py:204)
+// and the audio processor graph's plugin ops (datasets/parts/features.py:197, 215, 233, 242):
+//   preemphasis(Tensor x, Tensor x_lens, float coeff=0.97, int pad_size=0) -> Tensor
+//   power_spectrum(Tensor x, Tensor x_lens) -> Tensor
+//   frame_splicing(Tensor x, Tensor x_lens, int factor) -> Tensor
+//   i_layernorm_pad(Tensor x, Tensor weight, Tensor bias, Tensor x_lens, float eps, int unbiased,
+//                   Tensor output_shape) -> (Tensor, Tensor)
+// Every other name models/_C.py:15-51 resolves (the BERT kernels of the same plugin and the int8
+// LSTM's dead per-step decomposition, quant_lstm.py:222-264) is registered too, so `import _C`
+// binds; calling one raises a TORCH_CHECK naming the op that replaces it on this engine.
 //
 // Activations live on the GPU (CUDA dispatch key); weights may be host or device tensors.  The
 // ops compute with the weights they are passed: each distinct weight set (keyed by the tensors'
@@ -68,7 +79,7 @@ void key_add(Key& k, const at::Tensor& t) {
 struct OpEngine {
   rnnt_engine* e = nullptr;
   int max_batch = 0, max_frames = 0;
-  Key enc[5], pred, joint1, joint2;
+  Key enc[5], pred, pred32, joint1, joint2;
 };
 std::mutex g_mu;
 std::map<int, OpEngine> g_eng;
@@ -401,6 +412,124 @@ std::tuple<at::Tensor, at::Tensor> prepack_lstm_weights(const at::Tensor& w_ih, 
 }
 at::Tensor prepack_linear_weight(const at::Tensor& w) { return w; }
 
+// ---------------------------------------------------------------- lstm (fp32 prediction)
+// weights[l] = [w_ih, w_hh, b_ih, b_hh] fp32 (Prediction.prepack_weights' fp32 branch, modeling_rnnt.py:
+// 173-177, with prepack_lstm_weights the identity); x = the embedded labels [1, N, 320] (or [N, 320]).
+std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_f32(
+    const at::Tensor& x, at::TensorList hx, at::TensorList cx, const c10::List<c10::List<at::Tensor>>& weights) {
+  TORCH_CHECK(x.is_cuda(), "lstm: activations must be on the GPU");
+  TORCH_CHECK(weights.size() == 2 && hx.size() == 2 && cx.size() == 2, "lstm: the 2-layer prediction LSTM");
+  const at::Tensor x2 = x.reshape({-1, P});
+  const int64_t N = x2.size(0), n_pad = round_up(N, 64);
+  std::lock_guard<std::mutex> lock(g_mu);
+  OpEngine& oe = engine_for(x.device().index(), n_pad, 500);
+  Key k;
+  for (int l = 0; l < 2; ++l)
+    for (int j = 0; j < 4; ++j) key_add(k, weights.get(l).get(j));
+  if (k != oe.pred32) {
+    std::vector<float> w[4][2];
+    const float* pw[4][2];
+    for (int l = 0; l < 2; ++l) {
+      const c10::List<at::Tensor> wl = weights.get(l);
+      TORCH_CHECK(wl.size() == 4, "lstm: weights[l] = [w_ih, w_hh, b_ih, b_hh]");
+      for (int j = 0; j < 4; ++j) {
+        w[j][l] = host_vec<float>(wl.get(j), at::kFloat);
+        TORCH_CHECK(w[j][l].size() == (j < 2 ? (size_t)4 * P * P : (size_t)4 * P), "lstm: weight / bias shape");
+        pw[j][l] = w[j][l].data();
+      }
+    }
+    check_rc(rnnt_engine_load_f32_prediction(oe.e, pw[0], pw[1], pw[2], pw[3]), "lstm load");
+    oe.pred32 = k;
+  }
+  const auto opt = x.options().dtype(at::kFloat);
+  at::Tensor xp = at::zeros({n_pad, P}, opt);
+  xp.narrow(0, 0, N).copy_(x2);
+  at::Tensor h = at::zeros({2, n_pad, P}, opt), c = at::zeros({2, n_pad, P}, opt);
+  for (int l = 0; l < 2; ++l) {
+    h[l].narrow(0, 0, N).copy_(hx[l].reshape({-1, P}));
+    c[l].narrow(0, 0, N).copy_(cx[l].reshape({-1, P}));
+  }
+  at::Tensor hy = at::empty_like(h), cy = at::empty_like(c);
+  check_rc(rnnt_op_lstm_f32(oe.e, xp.data_ptr<float>(), h.data_ptr<float>(), c.data_ptr<float>(), hy.data_ptr<float>(),
+                            cy.data_ptr<float>(), (int)n_pad, stream_of(x)),
+           "lstm");
+  std::vector<at::Tensor> ho{hy[0].narrow(0, 0, N), hy[1].narrow(0, 0, N)};
+  std::vector<at::Tensor> co{cy[0].narrow(0, 0, N), cy[1].narrow(0, 0, N)};
+  return {ho[1].unsqueeze(0), ho, co};
+}
+
+// ---------------------------------------------------------------- audio processor ops
+at::Tensor lens_i32(const at::Tensor& lens, const at::Tensor& like) {
+  return lens.to(like.device(), at::kInt).contiguous();
+}
+
+at::Tensor preemphasis(const at::Tensor& x, const at::Tensor& x_lens, double coeff, int64_t pad_size) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 2, "preemphasis: x fp32 [N, L] on the GPU");
+  const at::Tensor xc = x.to(at::kFloat).contiguous(), lens = lens_i32(x_lens, x);
+  const int64_t N = xc.size(0), L_out = xc.size(1) + 2 * pad_size;
+  at::Tensor y = at::empty({N, L_out}, xc.options());
+  check_rc(rnnt_op_preemphasis(xc.data_ptr<float>(), xc.size(1), lens.data_ptr<int32_t>(), (int)N, (int)L_out,
+                               (float)coeff, (int)pad_size, y.data_ptr<float>(), stream_of(x)),
+           "preemphasis");
+  return y;
+}
+
+at::Tensor power_spectrum(const at::Tensor& x, const at::Tensor& x_lens) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(3) == 2, "power_spectrum: x fp32 [N, T, bins, 2] on the GPU");
+  const at::Tensor xc = x.to(at::kFloat).contiguous(), frames = lens_i32(x_lens, x);
+  const int64_t N = xc.size(0), T = xc.size(1), bins = xc.size(2);
+  at::Tensor y = at::empty({N, T, bins}, xc.options());
+  check_rc(rnnt_op_power_spectrum(xc.data_ptr<float>(), frames.data_ptr<int32_t>(), (int)N, (int)T, (int)bins,
+                                  y.data_ptr<float>(), stream_of(x)),
+           "power_spectrum");
+  return y;
+}
+
+at::Tensor frame_splicing(const at::Tensor& x, const at::Tensor& x_lens, int64_t factor) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 3, "frame_splicing: x fp32 [N, C, T] on the GPU");
+  const at::Tensor xc = x.to(at::kFloat).contiguous(), frames = lens_i32(x_lens, x);
+  const int64_t N = xc.size(0), C = xc.size(1), T = xc.size(2);
+  at::Tensor y = at::empty({N, C * factor, (T + factor - 1) / factor}, xc.options());
+  check_rc(rnnt_op_frame_splicing(xc.data_ptr<float>(), frames.data_ptr<int32_t>(), (int)N, (int)C, (int)T,
+                                  (int)factor, y.data_ptr<float>(), stream_of(x)),
+           "frame_splicing");
+  return y;
+}
+
+std::tuple<at::Tensor, at::Tensor> i_layernorm_pad(const at::Tensor& x, const at::Tensor& weight,
+                                                   const at::Tensor& bias, const at::Tensor& x_lens, double eps,
+                                                   int64_t unbiased, const at::Tensor& output_shape) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 3, "i_layernorm_pad: x fp32 [N, C, T] on the GPU");
+  const at::Tensor xc = x.to(at::kFloat).contiguous(), lens = lens_i32(x_lens, x);
+  const std::vector<int32_t> os = host_vec<int32_t>(output_shape, at::kInt);
+  TORCH_CHECK(os.size() == 3, "i_layernorm_pad: output_shape (N, C, T_max)");
+  const int64_t N = xc.size(0), C = xc.size(1), T = xc.size(2);
+  const int64_t n_out = std::max<int64_t>(os[0], N), c_out = std::max<int64_t>(os[1], C);
+  TORCH_CHECK(T <= os[2] || os[2] <= 0, "i_layernorm_pad: more frames than output_shape[2]");
+  const at::Tensor w = weight.to(x.device(), at::kFloat).contiguous(), b = bias.to(x.device(), at::kFloat).contiguous();
+  TORCH_CHECK(w.numel() == b.numel() && w.numel() % c_out == 0, "i_layernorm_pad: weight / bias [1, C_out, T_max]");
+  const int wt = (int)(w.numel() / c_out);
+  at::Tensor y = at::empty({n_out, c_out, T}, xc.options());
+  at::Tensor lo = at::empty({n_out}, xc.options().dtype(at::kInt));
+  check_rc(rnnt_op_layernorm_pad(xc.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), wt,
+                                 lens.data_ptr<int32_t>(), (int)N, (int)C, (int)T, (int)n_out, (int)c_out, (float)eps,
+                                 (int)unbiased, y.data_ptr<float>(), lo.data_ptr<int32_t>(), stream_of(x)),
+           "i_layernorm_pad");
+  return {y, lo};
+}
+
+// ---------------------------------------------------------------- names bound but not served
+// models/_C.py:15-51 resolves these at import; the RNN-T graph never calls them (BERT kernels of the
+// same plugin; quant_lstm.py's dead per-step decomposition).  Registered so the module binds; a call
+// fails loudly.
+[[noreturn]] void not_served(const char* op, const char* instead) {
+  TORCH_CHECK(false, "intel_mlperf::", op, " is not served by the MI355X engine (", instead, ")");
+}
+void boxed_not_served(const c10::OperatorHandle& op, torch::jit::Stack*) {
+  const std::string& full = op.schema().name();  // "intel_mlperf::name"
+  not_served(full.substr(full.rfind(':') + 1).c_str(), "not on the RNN-T path");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(intel_mlperf, m) {
@@ -415,6 +544,42 @@ TORCH_LIBRARY(intel_mlperf, m) {
         "Tensor(i!)[] pre_cg, Tensor[] hg, Tensor[] cg) -> bool");
   m.def("prepack_lstm_weights(Tensor w_ih, Tensor w_hh) -> (Tensor, Tensor)");
   m.def("prepack_linear_weight(Tensor w) -> Tensor");
+  m.def("lstm(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights) -> (Tensor, Tensor[], Tensor[])");
+  m.def("preemphasis(Tensor x, Tensor x_lens, float coeff=0.97, int pad_size=0) -> Tensor");
+  m.def("power_spectrum(Tensor x, Tensor x_lens) -> Tensor");
+  m.def("frame_splicing(Tensor x, Tensor x_lens, int factor) -> Tensor");
+  m.def("i_layernorm_pad(Tensor x, Tensor weight, Tensor bias, Tensor x_lens, float eps, int unbiased, "
+        "Tensor output_shape) -> (Tensor, Tensor)");
+  // bound, not served (see not_served): the int8 LSTM's per-step decomposition (quant_lstm.py:222-264)
+  m.def("linear(Tensor x, Tensor weight, Tensor? bias, float scale, float? o_scale=None) -> Tensor",
+        [](const at::Tensor&, const at::Tensor&, const c10::optional<at::Tensor>&, double,
+           c10::optional<double>) -> at::Tensor { not_served("linear", "lstm_amx_int8 runs the whole layer"); });
+  m.def("lstm_postop(Tensor it, Tensor ft, Tensor gt, Tensor ot, Tensor cx, float in_scale, float out_scale, "
+        "bool skip_quant_y) -> (Tensor, Tensor, Tensor, Tensor)",
+        [](const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, double, double,
+           bool) -> std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> {
+          not_served("lstm_postop", "the cell is fused into lstm_amx_int8");
+        });
+  m.def("lstm_layer_amx_int8(Tensor x, Tensor hx, Tensor cx, Tensor w_ih, Tensor w_hh, Tensor b_ih, Tensor b_hh, "
+        "float rb_scale, float in_scale, float out_scale, bool skip_quant_y) -> (Tensor, Tensor, Tensor)",
+        [](const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
+           const at::Tensor&, const at::Tensor&, double, double, double,
+           bool) -> std::tuple<at::Tensor, at::Tensor, at::Tensor> {
+          not_served("lstm_layer_amx_int8", "use lstm_amx_int8 over the stack");
+        });
+  m.def("lstm_layer_amx_bf16(Tensor x, Tensor hx, Tensor cx, Tensor w_ih, Tensor w_hh, Tensor b_ih, Tensor b_hh) -> "
+        "(Tensor, Tensor, Tensor)",
+        [](const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&, const at::Tensor&,
+           const at::Tensor&, const at::Tensor&) -> std::tuple<at::Tensor, at::Tensor, at::Tensor> {
+          not_served("lstm_layer_amx_bf16", "use lstm_amx_bf16");
+        });
+  // BERT kernels and elementwise helpers of the same plugin (no call site in the RNN-T tree)
+  for (const char* name : {"linear_gelu", "amx_linear", "amx_linear_i8o32", "baddbmm_out_", "matmul_out_", "reorder_test",
+                           "i_softmax", "i_softmax_u", "i_gelu", "i_identity", "i_identity_cin", "i_identity_",
+                           "i_layernorm", "i_residual_layernorm", "i_residual_layernorm_", "i_residual_layernorm_cin_",
+                           "amx_mha", "amx_mha_concat", "tanh", "sigmoid", "tanh_f16"})
+    m.def((std::string(name) + "(Tensor x) -> Tensor").c_str(),
+          torch::CppFunction::makeFromBoxedFunction<&boxed_not_served>());
 }
 
 TORCH_LIBRARY_IMPL(intel_mlperf, CUDA, m) {
@@ -424,6 +589,11 @@ TORCH_LIBRARY_IMPL(intel_mlperf, CUDA, m) {
   m.impl("amx_linear_bf16_accum_relu", amx_linear_bf16_accum_relu);
   m.impl("amx_linear_i16o32", amx_linear_i16o32);
   m.impl("greedy_decode_update", greedy_decode_update);
+  m.impl("lstm", lstm_f32);
+  m.impl("preemphasis", preemphasis);
+  m.impl("power_spectrum", power_spectrum);
+  m.impl("frame_splicing", frame_splicing);
+  m.impl("i_layernorm_pad", i_layernorm_pad);
 }
 
 TORCH_LIBRARY_IMPL(intel_mlperf, CompositeExplicitAutograd, m) {

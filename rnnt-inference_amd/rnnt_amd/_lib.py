@@ -102,6 +102,16 @@ _SIGS = {
                                     C.c_void_p, C.c_void_p, C.c_void_p]),
     "rnnt_op_stack_time": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                      C.c_void_p]),
+    "rnnt_engine_load_f32_prediction": (C.c_int, [C.c_void_p] + [C.POINTER(C.c_void_p)] * 4),
+    "rnnt_op_lstm_f32": (C.c_int, [C.c_void_p] * 6 + [C.c_int, C.c_void_p]),
+    "rnnt_op_preemphasis": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_int, C.c_float, C.c_int,
+                                      C.c_void_p, C.c_void_p]),
+    "rnnt_op_power_spectrum": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+    "rnnt_op_frame_splicing": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                         C.c_void_p]),
+    "rnnt_op_layernorm_pad": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                        C.c_int, C.c_int, C.c_int, C.c_float, C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]),
 }
 
 _lib = None

@@ -22,7 +22,7 @@ def test_exports_every_header_symbol():
 
 def test_abi_version_and_error_path():
     lib = _lib.lib()
-    assert lib.rnnt_abi_version() == 7
+    assert lib.rnnt_abi_version() == 8
     rc = lib.rnnt_engine_create(None, 0, None, None)
     assert rc == _lib.RNNT_EINVAL
     assert b"null" in lib.rnnt_last_error()

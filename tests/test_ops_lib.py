@@ -28,7 +28,22 @@ SCHEMAS = {
     "amx_linear_i16o32": "(Tensor y, Tensor w2, Tensor b2) -> Tensor",
     "prepack_lstm_weights": "(Tensor w_ih, Tensor w_hh) -> (Tensor, Tensor)",
     "prepack_linear_weight": "(Tensor w) -> Tensor",
+    "lstm": "(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights) -> (Tensor, Tensor[], Tensor[])",
+    "preemphasis": "(Tensor x, Tensor x_lens, float coeff=0.96999999999999997, int pad_size=0) -> Tensor",
+    "power_spectrum": "(Tensor x, Tensor x_lens) -> Tensor",
+    "frame_splicing": "(Tensor x, Tensor x_lens, int factor) -> Tensor",
+    "i_layernorm_pad": "(Tensor x, Tensor weight, Tensor bias, Tensor x_lens, float eps, int unbiased, "
+                       "Tensor output_shape) -> (Tensor, Tensor)",
 }
+
+# every name the reference's operator module resolves at import (models/_C.py:15-51), in its order
+REFERENCE_C_NAMES = [
+    "linear", "linear_gelu", "amx_linear", "amx_linear_i8o32", "amx_linear_bf16_accum_relu", "amx_linear_i16o32",
+    "baddbmm_out_", "prepack_linear_weight", "matmul_out_", "reorder_test", "i_softmax", "i_softmax_u", "i_gelu",
+    "i_identity", "i_identity_cin", "i_identity_", "i_layernorm", "i_layernorm_pad", "i_residual_layernorm",
+    "i_residual_layernorm_", "i_residual_layernorm_cin_", "amx_mha", "amx_mha_concat", "preemphasis",
+    "frame_splicing", "stack_time", "prepack_lstm_weights", "tanh", "sigmoid", "tanh_f16", "lstm_postop",
+    "lstm_layer_amx_int8", "lstm_amx_int8", "lstm_layer_amx_bf16", "lstm_amx_bf16", "greedy_decode_update", "lstm"]
 
 
 @pytest.fixture(scope="module")
@@ -42,6 +57,22 @@ def test_library_registers_reference_schemas(lib):
         assert schema == f"intel_mlperf::{name}{sig}", schema
     s = str(lib.greedy_decode_update.default._schema)
     assert s.endswith("-> bool") and s.count("Tensor") == 13, s  # 13 operands, finish kept internal
+
+
+def test_reference_operator_module_binds(lib):
+    """`import _C` (models/_C.py:15-51) resolves 37 names; all bind here, plus power_spectrum
+    (datasets/parts/features.py:215).  The names the RNN-T graph never calls fail loudly, naming
+    the op."""
+    assert len(REFERENCE_C_NAMES) == 37
+    for name in REFERENCE_C_NAMES + ["power_spectrum"]:
+        assert hasattr(lib, name), name
+        assert getattr(lib, name).default._schema.name == f"intel_mlperf::{name}"
+    for name in ("amx_mha", "i_softmax", "tanh_f16"):
+        with pytest.raises(RuntimeError, match=f"intel_mlperf::{name} is not served"):
+            getattr(lib, name)(torch.zeros(2))
+    with pytest.raises(RuntimeError, match="lstm_postop is not served"):
+        z = torch.zeros(2, 4)
+        lib.lstm_postop(z, z, z, z, z, 1.0, 1.0, False)
 
 
 def test_reference_tile_layouts(pm_golden):
@@ -87,7 +118,25 @@ def test_torchscript_binds_the_ops(lib):
             y = torch.ops.intel_mlperf.amx_linear_bf16_accum_relu(f, w1t, g, w1p, b)
             return torch.ops.intel_mlperf.amx_linear_i16o32(y, w2, b2)
 
-    for m in (Update(), Stack(), Joint()):
+    class Prediction32(torch.nn.Module):  # Prediction.forward, run_mode f32 (modeling_rnnt.py:183-205)
+        def forward(self, g: torch.Tensor, hg: List[torch.Tensor], cg: List[torch.Tensor],
+                    weights: List[List[torch.Tensor]]):
+            return torch.ops.intel_mlperf.lstm(g, hg, cg, weights)
+
+    class Processor(torch.nn.Module):  # FilterbankFeatures.forward's plugin ops (features.py:185-252)
+        def forward(self, x: torch.Tensor, x_lens: torch.Tensor, window: torch.Tensor, fb: torch.Tensor,
+                    fb_bias: torch.Tensor, w: torch.Tensor, b: torch.Tensor, shape: torch.Tensor):
+            x = torch.ops.intel_mlperf.preemphasis(x, x_lens, coeff=0.97, pad_size=256)
+            x = torch.stft(x, n_fft=512, hop_length=160, win_length=320, center=False, window=window,
+                           return_complex=False).permute(0, 2, 1, 3)
+            x_lens = torch.floor(x_lens / 160 + 1).to(dtype=torch.int32)
+            x = torch.ops.intel_mlperf.power_spectrum(x, x_lens).permute(0, 2, 1)
+            x = torch.log(torch.baddbmm(fb_bias, fb, x))
+            x = torch.ops.intel_mlperf.frame_splicing(x, x_lens, 3)
+            x_lens = torch.ceil(x_lens / 3).to(dtype=torch.int32)
+            return torch.ops.intel_mlperf.i_layernorm_pad(x, w, b, x_lens, 1e-12, unbiased=1, output_shape=shape)
+
+    for m in (Update(), Stack(), Joint(), Prediction32(), Processor()):
         g = torch.jit.script(m).graph
         assert "intel_mlperf::" in str(g)
 
