@@ -213,6 +213,11 @@ typedef struct {
   int64_t encode_calls, decode_calls;
 } rnnt_stats;
 int rnnt_engine_set_profiling(rnnt_engine* e, int on);
+/* Tick tile shape of the int8 encoder: "auto" (per tick, the cost model; the default), or pinned
+ * to "big" (256 x 256), "small" (128 x 128, 2-deep ring), "tiny" (128 x 128, 4-deep) or "mini"
+ * (64 x 128, 4-deep) -- results are identical (int32 accumulation); for tests and sweeps.  The
+ * environment variable RNNT_ENC_TILE sets an engine's initial value at create. */
+int rnnt_engine_set_tile(rnnt_engine* e, const char* tile);
 int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset);
 
 /* ---- operator-level entry points (torch.ops.intel_mlperf mirror, rnnt_amd/ops.py) ---- */

@@ -343,30 +343,15 @@ constexpr int PRED_THREADS = 256;  // 4 waves, one gate tile each: 40 KB of weig
 // rows per workgroup iteration of the prediction / G kernels: 32 (two MFMA row tiles per weight
 // fragment) with 24 / 48 row groups -- isolated greedy 69.5 -> 66.7 ms per query vs 16 rows and
 // 48 / 96 groups (64 rows: 82 ms); the joint keeps 16-row tiles (JRT)
-#ifndef RNNT_DEC_RT
-#define RNNT_DEC_RT 32
-#endif
-constexpr int DEC_RT = RNNT_DEC_RT;
+constexpr int DEC_RT = 32;
 constexpr int DEC_SUB = DEC_RT / 16;
-#ifndef RNNT_PRED_RG
-#define RNNT_PRED_RG 24
-#endif
-#ifndef RNNT_G_RG
-#define RNNT_G_RG 48
-#endif
-#ifndef RNNT_JOINT_G
-#define RNNT_JOINT_G 512
-#endif
-constexpr int PRED_ROW_GROUPS = RNNT_PRED_RG;
-#ifndef RNNT_PRED_WIDE_MIN  // live-row bound from which the prediction launches use 8-wave workgroups (0: never)
-#define RNNT_PRED_WIDE_MIN 0
-#endif
-constexpr int G_ROW_GROUPS = RNNT_G_RG;
-constexpr int JOINT_GROUPS = RNNT_JOINT_G;
+// row groups (grid y) of the prediction / G launches and workgroups of the joint, at most: round-2
+// sweeps of 12-96 / 24-96 / 256-512 measured within +-1.5 %
+constexpr int PRED_ROW_GROUPS = 24;
+constexpr int G_ROW_GROUPS = 48;
+constexpr int JOINT_GROUPS = 512;
 
-// NW waves per workgroup (NW gate tiles): 4 by default; 8 while the emit lists are long (the
-// staged rows then feed twice the gate tiles, halving the row re-reads across column groups, at
-// the price of a 2x weight slice per launch -- which only the short tail steps notice)
+// NW waves per workgroup (NW gate tiles; 4: 8-wave workgroups measured no faster)
 template <int LAYER, int NW>
 __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity) {
   constexpr int PRED_THREADS = NW * 64;
@@ -595,13 +580,11 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
 // joint (y1 = bf16(relu(F[t] + G)), logits = b2 + y1.W2^T) + argmax + greedy_decode_update
 // (decoder.py:137-167) for JRT live-list rows per workgroup tile.  A blank (or a forced advance
 // after max_symbols_per_step) moves the row to its next frame with the SAME prediction, so the
-// workgroup evaluates up to RNNT_JOINT_ITERS frames per launch, stopping a row at its first
+// workgroup evaluates up to JOINT_ITERS frames per launch, stopping a row at its first
 // emission (it then needs a new prediction: next step's emit list) or at its last frame; rows
 // not finished go to the next step's live list.  Identical results for any cap; the cap
 // trades lock-step steps against the length of each step.
-#ifndef RNNT_JOINT_ITERS
-#define RNNT_JOINT_ITERS 2
-#endif
+constexpr int JOINT_ITERS = 2;  // 1 / 3 / 4 measured slower
 
 constexpr int YP = J + 8;
 constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 waves x 4 rows x 16 lanes onto it
@@ -657,7 +640,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
 #endif
     constexpr int NIT = JRT * (J / 8) / 256;
     float4 gl4[NIT][2];
-    for (int it = 0; it < RNNT_JOINT_ITERS; ++it) {
+    for (int it = 0; it < JOINT_ITERS; ++it) {
       bool any = false;
       for (int m = 0; m < JRT; ++m) any |= walking[m] != 0;
       if (!any) break;
@@ -827,15 +810,10 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_joint = ljt < JOINT_GROUPS ? ljt : JOINT_GROUPS;
     for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      if (RNNT_PRED_WIDE_MIN > 0 && live_bound >= RNNT_PRED_WIDE_MIN) {
-        hipLaunchKernelGGL((dec_pred_kernel<0, 8>), dim3(xcd_grid_size(PG4 / (16 * 8), rg_pred)), dim3(512), 0, st, a, p);
-        hipLaunchKernelGGL((dec_pred_kernel<1, 8>), dim3(xcd_grid_size(PG4 / (16 * 8), rg_pred)), dim3(512), 0, st, a, p);
-      } else {
-        hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                           dim3(PRED_THREADS), 0, st, a, p);
-        hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                           dim3(PRED_THREADS), 0, st, a, p);
-      }
+      hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                         dim3(PRED_THREADS), 0, st, a, p);
+      hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                         dim3(PRED_THREADS), 0, st, a, p);
       hipLaunchKernelGGL(dec_g_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), rg_g)), dim3(G_THREADS), 0, st, a,
                          p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
@@ -861,10 +839,7 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
 int launch_joint_trans(const DecWeights& w, const uint16_t* fbf, const int32_t* f_lens, float* F, int Tp, int Npad,
                        hipStream_t st) {
   if (Tp <= 0) return 0;
-#ifndef RNNT_JT_GEMM
-#define RNNT_JT_GEMM 1
-#endif
-  if (RNNT_JT_GEMM && Npad % 256 == 0) {
+  if (Npad % 256 == 0) {  // the engine's batches; op-level callers with other row counts: 64-column kernel
     static std::atomic<uint64_t> gattr{0};
     if (set_smem_attr_once((const void*)joint_trans_gemm_kernel, JG_SMEM, gattr)) return -1;
     const int nrt = Tp * Npad / 256;

@@ -484,18 +484,9 @@ int launch_quantize_gather(const float* store, const int64_t* offsets, const int
 // section 4): a full round of small tiles (two per CU) costs ENC_SMALL_ROUND of it, and a
 // small-tile launch takes at least ENC_SMALL_FLOOR (its K loop's latency); the small tile must
 // win by ENC_SMALL_MARGIN (its co-resident workgroups also leave room for the overlapped
-// decode's, which slows the encoder).  RNNT_ENC_TILE=big|small|tiny|mini forces a shape.
+// decode's, which slows the encoder).  `forced` (the engine's rnnt_engine_set_tile) pins a shape.
 constexpr int ENC_CUS = 256;
 constexpr float ENC_SMALL_ROUND = 0.59f, ENC_SMALL_FLOOR = 0.5f, ENC_SMALL_MARGIN = 0.9f;
-static int enc_tile_choice() {  // read per launch (a test may switch it between calls)
-  const char* s = getenv("RNNT_ENC_TILE");
-  if (!s) return 0;
-  if (!strcmp(s, "big")) return 1;
-  if (!strcmp(s, "small")) return 2;
-  if (!strcmp(s, "tiny")) return 3;
-  if (!strcmp(s, "mini")) return 5;
-  return 0;
-}
 template <class C>
 static int tick_grid(const EncTickArgs& a) {  // workgroups: 8 XCDs x the batch-half-0 XCDs' (larger) share
   int per_xcd = 0;
@@ -513,26 +504,26 @@ static int launch_tick(const EncTickArgs& a, int grid, hipStream_t st) {
   hipLaunchKernelGGL((lstm_i8_tick_kernel<C::BM / 64, C::BN / 32, C::NBUF>), dim3(grid), dim3(NWAVE * 64), C::SMEM, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st) {
+int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st, int forced) {
   // shapes the kernel's staging assumes (checked on the host: a mismatch would read out of bounds)
   for (int j = 0; j < a.njobs; ++j)
     if (a.job[j].I % 128 != 0 || a.nbt[j] < 0) return -1;
   const int gb = tick_grid<BigTile>(a), gs = tick_grid<SmallTile>(a), gm = tick_grid<MiniTile>(a);
   if (gb <= 0) return 0;
-  int choice = enc_tile_choice();
-  if (choice == 0) {
+  int choice = forced;
+  if (choice == ENC_TILE_AUTO) {
     const float rb = (float)((gb + ENC_CUS - 1) / ENC_CUS);
     const float rs = fmaxf((float)gs / (2 * ENC_CUS) * ENC_SMALL_ROUND, ENC_SMALL_FLOOR);
-    choice = rs < ENC_SMALL_MARGIN * rb ? 2 : 1;
-    if (choice == 2 && gs <= ENC_CUS) {  // at most one small workgroup per CU: a deep ring
+    choice = rs < ENC_SMALL_MARGIN * rb ? ENC_TILE_SMALL : ENC_TILE_BIG;
+    if (choice == ENC_TILE_SMALL && gs <= ENC_CUS) {  // at most one small workgroup per CU: a deep ring
       bool one_tile = true;
       for (int j = 0; j < a.njobs; ++j) one_tile = one_tile && a.nbt[j] <= 1;
-      choice = one_tile && gm <= ENC_CUS ? 5 : 3;  // still one per CU with half the gate rows: mini
+      choice = one_tile && gm <= ENC_CUS ? ENC_TILE_MINI : ENC_TILE_TINY;  // one per CU with half the gate rows: mini
     }
   }
-  if (choice == 1) return launch_tick<BigTile>(a, gb, st);
-  if (choice == 5) return launch_tick<MiniTile>(a, gm, st);
-  return choice == 3 ? launch_tick<TinyTile>(a, gs, st) : launch_tick<SmallTile>(a, gs, st);
+  if (choice == ENC_TILE_BIG) return launch_tick<BigTile>(a, gb, st);
+  if (choice == ENC_TILE_MINI) return launch_tick<MiniTile>(a, gm, st);
+  return choice == ENC_TILE_TINY ? launch_tick<TinyTile>(a, gs, st) : launch_tick<SmallTile>(a, gs, st);
 }
 
 }  // namespace rnnt

@@ -56,6 +56,8 @@ int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStrea
 // t < lens[i]; out int8 [T][n_pad][256], zero past the length, in channels 240..255 and rows >= n.
 int launch_quantize_gather(const float* store, const int64_t* offsets, const int32_t* lens, int T, int n, int n_pad,
                            float s, int8_t* out, hipStream_t st);
-int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st);
+// tick tile shape: chosen per tick by the cost model (ENC_TILE_AUTO) or pinned (tests, sweeps)
+enum { ENC_TILE_AUTO = 0, ENC_TILE_BIG = 1, ENC_TILE_SMALL = 2, ENC_TILE_TINY = 3, ENC_TILE_MINI = 5 };
+int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st, int forced = ENC_TILE_AUTO);
 
 }  // namespace rnnt

@@ -5,6 +5,7 @@
 // csrc/rnnt_model.hpp:62-124).  No torch types anywhere: plain pointers and sizes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -50,6 +51,7 @@ struct rnnt_engine {
   hipStream_t stream = nullptr;
   rnnt_opts opts{};
   int np_max = 0, tp_max = 0;
+  int tile = ENC_TILE_AUTO;  // tick tile shape (rnnt_engine_set_tile; RNNT_ENC_TILE at create)
   // packed weights
   int8_t* enc_w[5] = {};
   float* enc_bq[5] = {};
@@ -360,6 +362,23 @@ extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
   delete e;
 }
 
+static int tile_code(const char* s) {
+  if (!strcmp(s, "auto")) return ENC_TILE_AUTO;
+  if (!strcmp(s, "big")) return ENC_TILE_BIG;
+  if (!strcmp(s, "small")) return ENC_TILE_SMALL;
+  if (!strcmp(s, "tiny")) return ENC_TILE_TINY;
+  if (!strcmp(s, "mini")) return ENC_TILE_MINI;
+  return -1;
+}
+
+extern "C" int rnnt_engine_set_tile(rnnt_engine* e, const char* tile) {
+  if (!e || !tile) return fail(RNNT_EINVAL, "null argument");
+  const int v = tile_code(tile);
+  if (v < 0) return fail(RNNT_EINVAL, std::string("unknown tick tile '") + tile + "': auto|big|small|tiny|mini");
+  e->tile = v;
+  return 0;
+}
+
 extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, const rnnt_opts* opts,
                                   rnnt_engine** out) {
   if (!out) return fail(RNNT_EINVAL, "null argument");
@@ -381,6 +400,11 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   if (!r && !dscope.ok) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
   if (!r && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
+  if (const char* t = getenv("RNNT_ENC_TILE")) {  // development default, read once per engine
+    const int v = tile_code(t);
+    if (v < 0) r = fail(RNNT_EINVAL, std::string("RNNT_ENC_TILE=") + t + ": auto|big|small|tiny|mini");
+    e->tile = v < 0 ? ENC_TILE_AUTO : v;
+  }
   if (!r && model) r = pack_model(e, model);
   if (!r) r = alloc_workspace(e);
   if (r) {
@@ -567,7 +591,7 @@ struct TickBuilder {
     if (n == 0) return 0;
     args.njobs = n;
     e->step_launches++;
-    return launch_lstm_i8_tick(args, st) ? fail(RNNT_EDEVICE, "lstm tick launch failed") : 0;
+    return launch_lstm_i8_tick(args, st, e->tile) ? fail(RNNT_EDEVICE, "lstm tick launch failed") : 0;
   }
 };
 

@@ -213,6 +213,11 @@ class Engine:
     def set_profiling(self, on=True):
         _lib.check(self._lib.rnnt_engine_set_profiling(self._h, int(bool(on))), "rnnt_engine_set_profiling")
 
+    def set_tile(self, tile="auto"):
+        """Pin the int8 encoder's tick tile ("big" / "small" / "tiny" / "mini") or restore the
+        per-tick choice ("auto"); results are bit-identical either way (rnnt_engine_set_tile)."""
+        _lib.check(self._lib.rnnt_engine_set_tile(self._h, str(tile).encode()), "rnnt_engine_set_tile")
+
     def stats(self, reset=True):
         st = _lib.RnntStats()
         _lib.check(self._lib.rnnt_engine_get_stats(self._h, C.byref(st), int(bool(reset))), "rnnt_engine_get_stats")

@@ -6,8 +6,6 @@ also ~relative).  Padding (time past feat_lens, channels 240..255, batch rows pa
 lengths are exact.  Rows are independent: a row's features are bit-identical whatever batch it
 is in and whether samples come from a zero-padded [N][stride] batch or ragged storage + offsets.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -183,8 +181,7 @@ def test_server_sut_over_wav_qsl(oracle):
                 b, j, ids = where[i]
                 bad.append(f"sample {i} ({frames[i]} frames): server {'ok' if srv_ok else 'WRONG'} "
                            f"(batch {b} on engine {j}, rows {ids}, {len(srv.responses[i])} vs {len(want[i])} tokens), "
-                           f"offline batch {'ok' if off_ok else 'WRONG'}; tick tiles "
-                           f"{os.environ.get('RNNT_ENC_TILE', 'auto')}")
+                           f"offline batch {'ok' if off_ok else 'WRONG'}; tick tiles auto (per tick)")
         assert not bad, "\n".join(bad)
     finally:
         for e in engines:

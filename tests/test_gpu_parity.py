@@ -28,12 +28,13 @@ def engine(model):
 
 
 @pytest.fixture(params=["big", "small", "tiny", "mini"])
-def tile(request, monkeypatch):
+def tile(request, engine):
     """Every encoder tile variant (256 x 256; 128 x 128 with a 2- and a 4-deep stage ring;
-    64 x 128 with a 4-deep ring, encoder.hip) forced in turn; the engine otherwise picks one per
-    tick."""
-    monkeypatch.setenv("RNNT_ENC_TILE", request.param)
-    return request.param
+    64 x 128 with a 4-deep ring, encoder.hip) pinned in turn (rnnt_engine_set_tile); the engine
+    otherwise picks one per tick."""
+    engine.set_tile(request.param)
+    yield request.param
+    engine.set_tile("auto")
 
 
 def _cuda(a):
@@ -138,7 +139,7 @@ def test_config3_int8_full_batch128(engine, model, oracle, tile):
     assert 0.02 < emit_rate < 5, emit_rate
 
 
-def test_large_batch_rows_match_small_batch(engine, model, oracle, monkeypatch):
+def test_large_batch_rows_match_small_batch(engine, model, oracle):
     """N=4096 (16 batch tiles: several tiles per workgroup / CU, every tick schedule path) on the
     256 x 256 tile vs the same rows run as small batches on the 128 x 128 tile: the int8 encoder
     is exact and row-independent, so encoder frames must be bit-identical and tokens identical
@@ -150,7 +151,7 @@ def test_large_batch_rows_match_small_batch(engine, model, oracle, monkeypatch):
     x = synthetic.make_features(T, n, seed=11, lens=lens)
     Tp = (T + 1) // 2
     big = Engine(model, device=0, max_batch=n, max_frames=T)
-    monkeypatch.setenv("RNNT_ENC_TILE", "big")
+    big.set_tile("big")
     try:
         f = torch.zeros((Tp, n, 1024), dtype=torch.float32, device="cuda")
         res = torch.empty((n, big.max_res), dtype=torch.int32, device="cuda")
@@ -161,27 +162,30 @@ def test_large_batch_rows_match_small_batch(engine, model, oracle, monkeypatch):
         fg, res_g, rl_g = f.cpu().numpy(), res.cpu().numpy(), rl.cpu().numpy()
     finally:
         big.close()
-    monkeypatch.setenv("RNNT_ENC_TILE", "small")
-    for lo in (0, 1800, 4096 - 200):
-        rows = np.arange(lo, lo + 200)
-        sl = lens[rows]
-        xs = np.zeros((T, 256, x.shape[2]), np.float32)
-        xs[:, :200] = x[:, rows]
-        lp = np.zeros(256, np.int32)
-        lp[:200] = sl
-        fs = torch.zeros((Tp, 256, 1024), dtype=torch.float32, device="cuda")
-        rs = torch.empty((200, res_g.shape[1]), dtype=torch.int32, device="cuda")
-        rls = torch.empty(200, dtype=torch.int32, device="cuda")
-        engine.encode(_cuda(xs), _cuda(lp), sl, n=200, f_out=fs)
-        engine.decode(rs, rls)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(_valid(fs.cpu().numpy()[:, :200], sl).view(np.uint32),
-                                      _valid(fg[:, rows], sl).view(np.uint32))
-        np.testing.assert_array_equal(rls.cpu().numpy(), rl_g[rows])
-        np.testing.assert_array_equal(rs.cpu().numpy(), res_g[rows])
-        if lo == 0:
-            fo = oracle.encoder_i8(model, xs[:, :8], lp[:8])
-            np.testing.assert_array_equal(_valid(fg[:, :8], lens[:8]).view(np.uint32), _valid(fo, lens[:8]).view(np.uint32))
+    engine.set_tile("small")
+    try:
+        for lo in (0, 1800, 4096 - 200):
+            rows = np.arange(lo, lo + 200)
+            sl = lens[rows]
+            xs = np.zeros((T, 256, x.shape[2]), np.float32)
+            xs[:, :200] = x[:, rows]
+            lp = np.zeros(256, np.int32)
+            lp[:200] = sl
+            fs = torch.zeros((Tp, 256, 1024), dtype=torch.float32, device="cuda")
+            rs = torch.empty((200, res_g.shape[1]), dtype=torch.int32, device="cuda")
+            rls = torch.empty(200, dtype=torch.int32, device="cuda")
+            engine.encode(_cuda(xs), _cuda(lp), sl, n=200, f_out=fs)
+            engine.decode(rs, rls)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(_valid(fs.cpu().numpy()[:, :200], sl).view(np.uint32),
+                                          _valid(fg[:, rows], sl).view(np.uint32))
+            np.testing.assert_array_equal(rls.cpu().numpy(), rl_g[rows])
+            np.testing.assert_array_equal(rs.cpu().numpy(), res_g[rows])
+            if lo == 0:
+                fo = oracle.encoder_i8(model, xs[:, :8], lp[:8])
+                np.testing.assert_array_equal(_valid(fg[:, :8], lens[:8]).view(np.uint32), _valid(fo, lens[:8]).view(np.uint32))
+    finally:
+        engine.set_tile("auto")
 
 
 @pytest.mark.gpu

@@ -168,10 +168,8 @@ def main():
 
     summary = dict(oracle_res_len=rlo.tolist(), featurizer_batch_mismatch=fz_mismatch, variants={})
     for var in args.variants.split(","):
-        if var == "small_tile":
-            os.environ["RNNT_ENC_TILE"] = "small"
-        else:
-            os.environ.pop("RNNT_ENC_TILE", None)
+        for e in engines:
+            e.set_tile("small" if var == "small_tile" else "auto")
         engs = engines[:1] if var == "one_engine" else engines
         q = pre if var == "prefeat" else qsl
         warm = {"warm_create": "create", "warm_full": "full", "nanfill": "nanfill"}.get(var, "none")
@@ -264,7 +262,6 @@ def main():
                                         first_diff=first_diff(res[i, : rl[i]], oracle_rows[i])))
             print(f"[{var}] rep {rep}: server mismatches {len(bad_srv)}, infer mismatches {len(bad_inf)}", flush=True)
         summary["variants"][var] = dict(reps=args.reps, server_bad=bad_srv, infer_bad=bad_inf)
-    os.environ.pop("RNNT_ENC_TILE", None)
     for e in engines:
         e.close()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
