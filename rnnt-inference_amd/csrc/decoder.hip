@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(128) dec_xtab_kernel(DecWeights w, float* __re
 // 64 output columns j and 256 rows: the 64 x 1024 W1t slice is staged in LDS once and read as
 // A fragments by 4 waves of 4 row tiles each (16 MFMA tiles per wave).
 constexpr int JT_ROWS = 256;
-constexpr int JT_PITCH = H + 8;  // bf16 elements per staged W1t row: +16 B, conflict-free b128 reads
+constexpr int JT_PITCH = H + 16;  // bf16 per staged W1t row: +32 B, conflict-free ds_read_b128 (16-lane groups)
 __global__ void __launch_bounds__(256) joint_trans_kernel(DecWeights w, const uint16_t* __restrict__ fbf,
                                                           const int32_t* __restrict__ f_lens,
                                                           float* __restrict__ F, int Npad, int nrows) {
@@ -357,7 +357,10 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   constexpr int PRED_THREADS = NW * 64;
   constexpr int NT = 1;                  // gate tiles per wave
   constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
-  constexpr int XP = KX + 8;             // bf16 pitch: +16 B per row (conflict-free b128 reads)
+  // bf16 pitch +32 B per row: every ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows c, 16-B
+  // column q) lands on 16 distinct bank quads; the round-2 +16 B pitch put rows c and c+8 on the same
+  // quads (2-way, 36-37 % of the LDS cycles of these kernels in the r02 PMC pass)
+  constexpr int XP = KX + 16;
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][XP];
   constexpr int NK = PRED_THREADS / DEC_RT;  // row tiles whose list entries load up front
   __shared__ int ents_all[NK][DEC_RT];
@@ -491,7 +494,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
 // tile (10 KB of W1p) per wave in registers: grid x = 8 column groups, y = row groups striding
 // over the emit list's tiles.  Also clears the next step's emit and live lists for the joint
 // that follows.
-constexpr int GXP = P + 8;
+constexpr int GXP = P + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
 constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each; grid x = 8 column groups
 __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
@@ -586,7 +589,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
 // trades lock-step steps against the length of each step.
 constexpr int JOINT_ITERS = 2;  // 1 / 3 / 4 measured slower
 
-constexpr int YP = J + 8;
+constexpr int YP = J + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
 constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 waves x 4 rows x 16 lanes onto it
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[JRT][YP];

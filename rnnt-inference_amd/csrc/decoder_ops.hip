@@ -26,10 +26,10 @@ __device__ __forceinline__ v4f chain_blocks(const uint16_t* w, const uint16_t* x
   return acc;
 }
 
-constexpr int OXP = 640 + 8;   // LDS pitch (bf16) of staged [x | h] rows
-constexpr int OFP = 1024 + 8;  // staged f rows
-constexpr int OGP = 320 + 8;   // staged g rows
-constexpr int OYP = 512 + 8;   // staged y1 rows
+constexpr int OXP = 640 + 16;  // LDS pitch (bf16) of staged [x | h] rows (+32 B: conflict-free b128 reads)
+constexpr int OFP = 1024 + 16;  // staged f rows
+constexpr int OGP = 320 + 16;   // staged g rows
+constexpr int OYP = 512 + 16;  // staged y1 rows (+32 B: conflict-free ds_read_b128 fragments)
 
 // one prediction LSTM layer: gates = (b_ih + x.W_ih) + (b_hh + h.W_hh); c fp32, h bf16.
 // Grid: x = 10 groups of 8 gate tiles (2 per wave), y = 16-row tiles.
