@@ -333,6 +333,13 @@ int64_t rnnt_featurizer_frames(int64_t wav_len);
 int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
                         const int32_t* wav_lens, const int32_t* wav_lens_host, int n, int n_pad, float* feats,
                         int32_t* feat_lens, int T_out, void* stream);
+/* Ragged variant for a feature store (the Server producer: featurize arriving samples once, the
+ * consumer encodes from the store, rnnt_engine_encode_stream): the same features, frame t of row
+ * n written as 240 fp32 at feats + (row_off[n] + t) * 240 (row_off device int64 [n]), nothing
+ * else touched; feat_lens device int32 [n].  Every row's frames <= max_frames (else RNNT_EINVAL). */
+int rnnt_featurizer_run_rows(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
+                             const int32_t* wav_lens, const int32_t* wav_lens_host, int n, float* feats,
+                             const int64_t* row_off, int32_t* feat_lens, int max_frames, void* stream);
 
 #ifdef __cplusplus
 }

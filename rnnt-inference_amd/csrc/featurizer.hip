@@ -104,6 +104,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ int stft_frames(int L) { return L > 0 ? 1 + L / FZ_HOP : 0; }  // features.py:212
 
+// feature frame t of row n: a [T_out][n_pad][256] batch, or ragged rows of 240 channels
+__device__ __forceinline__ float* feat_row(const FzArgs& a, int n, int t) {
+  return a.row_off ? a.feats + (size_t)(a.row_off[n] + t) * FZ_FEAT
+                   : a.feats + ((size_t)t * a.n_pad + n) * FZ_FEAT_PAD;
+}
+
 // (utterance, chunk) of every fz_logmel workgroup: exclusive scan of ceil(F_n / 16), then scatter
 __global__ __launch_bounds__(1024) void fz_plan_kernel(FzArgs a) {
   __shared__ int part[1024];
@@ -258,29 +264,32 @@ __global__ __launch_bounds__(NT * FZ_NSUB, 1) void fz_logmel_kernel(FzArgs a) {
     for (int i = 0; i < 4; ++i) {
       const int f = f0 + 4 * slot + i;  // D row 4 slot + i = frame, column j = filter 16 c + j
       const int t = f / FZ_SPLICE;
-      if (f < F && t < a.T_out)
-        a.feats[((size_t)t * a.n_pad + n) * FZ_FEAT_PAD + FZ_NMEL * (f - FZ_SPLICE * t) + 16 * c + j] =
-            logf(acc[i] + a.k.log_guard);
+      if (f < F && t < a.T_out) feat_row(a, n, t)[FZ_NMEL * (f - FZ_SPLICE * t) + 16 * c + j] = logf(acc[i] + a.k.log_guard);
     }
   }
   // spliced channels of frames past F (the last row's missing 3j+1 / 3j+2 frames) are zero
   if (f0 + FZ_CHUNK >= F && tid < 2 * FZ_NMEL) {
     const int Tn = (F + FZ_SPLICE - 1) / FZ_SPLICE;
     const int q = 1 + tid / FZ_NMEL;
-    if (FZ_SPLICE * (Tn - 1) + q >= F && Tn - 1 < a.T_out)
-      a.feats[((size_t)(Tn - 1) * a.n_pad + n) * FZ_FEAT_PAD + FZ_NMEL * q + tid % FZ_NMEL] = 0.0f;
+    if (FZ_SPLICE * (Tn - 1) + q >= F && Tn - 1 < a.T_out) feat_row(a, n, Tn - 1)[FZ_NMEL * q + tid % FZ_NMEL] = 0.0f;
   }
 }
 
+// per-feature normalisation, one workgroup per row, thread c = channel.  Padded output: the
+// row's [T_out] column of the [T_out][n_pad][256] batch, zero past its length and in channels
+// 240..255 and rows >= n.  Ragged output (grid n): the row's Tn x 240 frames only.
 __global__ __launch_bounds__(NT) void fz_norm_kernel(FzArgs a) {
   const int n = blockIdx.x, c = threadIdx.x;
+  const bool ragged = a.row_off != nullptr;
   int Tn = 0;
   if (n < a.n) Tn = (stft_frames(a.wav_lens[n]) + FZ_SPLICE - 1) / FZ_SPLICE;
   Tn = min(Tn, a.T_out);
   if (c == 0) a.feat_lens[n] = Tn;
   const bool live = c < FZ_FEAT;
-  float* col = a.feats + (size_t)n * FZ_FEAT_PAD + c;
-  const size_t rs = (size_t)a.n_pad * FZ_FEAT_PAD;
+  if (ragged && !live) return;
+  float* col = feat_row(a, n, 0) + c;
+  const size_t rs = ragged ? (size_t)FZ_FEAT : (size_t)a.n_pad * FZ_FEAT_PAD;
+  const int T_end = ragged ? Tn : a.T_out;
   float mean = 0.0f, rstd = 0.0f;
   if (live && Tn > 0) {
     double s = 0.0, s2 = 0.0;
@@ -306,14 +315,14 @@ __global__ __launch_bounds__(NT) void fz_norm_kernel(FzArgs a) {
     rstd = 1.0f / sqrtf((float)var + a.k.eps);
   }
   int t = 0;
-  for (; t + 4 <= a.T_out; t += 4) {
+  for (; t + 4 <= T_end; t += 4) {
     float x[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) x[u] = (live && t + u < Tn) ? col[(t + u) * rs] : 0.0f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) col[(t + u) * rs] = (live && t + u < Tn) ? (x[u] - mean) * rstd : 0.0f;
   }
-  for (; t < a.T_out; ++t) col[t * rs] = (live && t < Tn) ? (col[t * rs] - mean) * rstd : 0.0f;
+  for (; t < T_end; ++t) col[t * rs] = (live && t < Tn) ? (col[t * rs] - mean) * rstd : 0.0f;
 }
 
 }  // namespace
@@ -457,11 +466,10 @@ static int launch_logmel(const FzArgs& a, size_t chunks, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
-                                   const int32_t* wav_lens, const int32_t* wav_lens_host, int n, int n_pad,
-                                   float* feats, int32_t* feat_lens, int T_out, void* stream) {
-  if (!f || !wav || !wav_lens || !wav_lens_host || !feats || !feat_lens) return fz_fail(RNNT_EINVAL, "null argument");
-  if (n < 0 || n_pad < n || n_pad <= 0 || T_out <= 0) return fz_fail(RNNT_EINVAL, "bad n / n_pad / T_out");
+// row_off == nullptr: padded [T_out][n_pad][256] output; else ragged rows (n_pad == n)
+static int featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
+                          const int32_t* wav_lens, const int32_t* wav_lens_host, int n, int n_pad, float* feats,
+                          const int64_t* row_off, int32_t* feat_lens, int T_out, void* stream) {
   if (!offsets && stride <= 0 && n > 0) return fz_fail(RNNT_EINVAL, "need offsets or a positive stride");
   int64_t tmax = 0;
   for (int i = 0; i < n; ++i) {
@@ -489,6 +497,7 @@ extern "C" int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const i
   a.stride = stride;
   a.wav_lens = wav_lens;
   a.feats = feats;
+  a.row_off = row_off;
   a.feat_lens = feat_lens;
   a.plan = f->plan;
   a.n = n;
@@ -500,7 +509,26 @@ extern "C" int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const i
     hipLaunchKernelGGL(fz_plan_kernel, dim3(1), dim3(1024), 0, st, a);
     if (launch_logmel(a, chunks, st)) return fz_fail(RNNT_EDEVICE, "fz_logmel launch failed");
   }
-  hipLaunchKernelGGL(fz_norm_kernel, dim3(n_pad), dim3(NT), 0, st, a);
+  if (n_pad > 0) hipLaunchKernelGGL(fz_norm_kernel, dim3(n_pad), dim3(NT), 0, st, a);
   FZCHK(hipGetLastError());
   return 0;
+}
+
+extern "C" int rnnt_featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
+                                   const int32_t* wav_lens, const int32_t* wav_lens_host, int n, int n_pad,
+                                   float* feats, int32_t* feat_lens, int T_out, void* stream) {
+  if (!f || !wav || !wav_lens || !wav_lens_host || !feats || !feat_lens) return fz_fail(RNNT_EINVAL, "null argument");
+  if (n < 0 || n_pad < n || n_pad <= 0 || T_out <= 0) return fz_fail(RNNT_EINVAL, "bad n / n_pad / T_out");
+  return featurizer_run(f, wav, offsets, stride, wav_lens, wav_lens_host, n, n_pad, feats, nullptr, feat_lens, T_out,
+                        stream);
+}
+
+extern "C" int rnnt_featurizer_run_rows(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
+                                        const int32_t* wav_lens, const int32_t* wav_lens_host, int n, float* feats,
+                                        const int64_t* row_off, int32_t* feat_lens, int max_frames, void* stream) {
+  if (!f || !wav || !wav_lens || !wav_lens_host || !feats || !row_off || !feat_lens)
+    return fz_fail(RNNT_EINVAL, "null argument");
+  if (n < 0 || max_frames <= 0) return fz_fail(RNNT_EINVAL, "bad n / max_frames");
+  return featurizer_run(f, wav, offsets, stride, wav_lens, wav_lens_host, n, n, feats, row_off, feat_lens, max_frames,
+                        stream);
 }

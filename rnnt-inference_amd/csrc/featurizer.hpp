@@ -41,8 +41,9 @@ struct FzArgs {
   const int64_t* off;       // [n] or nullptr
   int64_t stride;
   const int32_t* wav_lens;  // [n]
-  float* feats;             // [T_out][n_pad][256]
-  int32_t* feat_lens;       // [n_pad]
+  float* feats;             // [T_out][n_pad][256], or ragged rows (row_off)
+  const int64_t* row_off;   // ragged output: frame t of row n at feats + (row_off[n] + t) * 240 (nullptr: padded)
+  int32_t* feat_lens;       // [n_pad] ([n] ragged)
   int2* plan;               // [chunks] (utterance, chunk) per fz_logmel workgroup (fz_plan_kernel)
   int n, n_pad, T_out;
   int n_chunks;             // plan entries (fz_logmel sub-groups past it idle)

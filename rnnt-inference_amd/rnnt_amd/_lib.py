@@ -59,6 +59,8 @@ _SIGS = {
     "rnnt_featurizer_frames": (C.c_int64, [C.c_int64]),
     "rnnt_featurizer_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
+    "rnnt_featurizer_run_rows": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                           C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "rnnt_engine_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "rnnt_engine_set_tile": (C.c_int, [C.c_void_p, C.c_char_p]),
     "rnnt_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(RnntStats), C.c_int]),

@@ -17,6 +17,7 @@ filterbank values are "parity unpinned"; callers holding librosa's matrix can pa
 """
 import ctypes as C
 import math
+from contextlib import nullcontext as _nullctx
 
 import numpy as np
 
@@ -146,6 +147,42 @@ class FilterbankFeatures:
                                                   _ptr(feat_lens), T_out, _stream_handle(stream)),
                    "rnnt_featurizer_run")
         return out, feat_lens
+
+    def featurize_rows(self, wav, wav_lens, wav_lens_host, out, row_off, max_frames, offsets=None, feat_lens=None,
+                       stream=None):
+        """Ragged entry for a feature store (rnnt_featurizer_run_rows): sample i's frames written as
+        240-channel rows out[row_off[i] + t] (out cuda fp32 [rows][240]; row_off host int64 [n],
+        bounds-checked against out here, then uploaded), nothing else touched; each sample's frames
+        <= max_frames.  Returns feat_lens cuda int32 [n]."""
+        import torch
+        lh = np.ascontiguousarray(np.asarray(wav_lens_host, dtype=np.int32))
+        n = len(lh)
+        dev = wav.device
+        if feat_lens is None:
+            feat_lens = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        assert out.is_contiguous() and out.dim() == 2 and out.shape[1] == 240 and out.dtype == torch.float32
+        assert wav.dtype == torch.float32 and wav.is_contiguous() and wav_lens.dtype == torch.int32
+        ro = np.ascontiguousarray(np.asarray(row_off, dtype=np.int64))
+        if ro.shape != (n,):
+            raise ValueError("row_off must hold one row offset per sample")
+        fr = np.array([feature_frames(int(v)) for v in lh], np.int64)
+        if n and fr.max() > max_frames:
+            raise ValueError("a sample's feature frames exceed max_frames")
+        if n and (ro.min() < 0 or (ro + fr).max() > out.shape[0]):
+            raise ValueError("row_off places a sample outside the store")
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():  # ordered before the kernels
+            row_off = torch.from_numpy(ro).to(dev)
+        if offsets is not None:
+            assert offsets.dtype == torch.int64 and offsets.numel() >= n
+            stride = 0
+        else:
+            assert wav.dim() == 2 and wav.shape[0] >= n
+            stride = wav.shape[1]
+        _lib.check(_lib.lib().rnnt_featurizer_run_rows(self._h, _ptr(wav), _ptr(offsets), stride, _ptr(wav_lens),
+                                                       lh.ctypes.data_as(C.c_void_p), n, _ptr(out), _ptr(row_off),
+                                                       _ptr(feat_lens), int(max_frames), _stream_handle(stream)),
+                   "rnnt_featurizer_run_rows")
+        return feat_lens
 
     def forward(self, x, x_lens, pad_batch_size):
         """features.py:185-252: x cuda fp32 [N][max_len] (zero-padded), x_lens int32 [N] ->

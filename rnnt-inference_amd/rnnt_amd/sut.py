@@ -358,6 +358,108 @@ class GpuWavQSL(_SortedQSL):
         return dict(x=x, lens=lens, lens_host=bl, T=x.shape[0])
 
 
+class FeatureStore:
+    """One device's Server feature store: ``slots`` fixed ranges of ``max_frames`` 240-channel fp32
+    rows in HBM -- the reference's per-sample processed feature tensors (torch_sut.cpp:454-461, one
+    [T][1][C] tensor per sample on mProcessedQueue_) kept resident instead.  A producer featurizes
+    an arriving sample into a free slot (rnnt_featurizer_run_rows), the engines of its lane encode
+    it from there chunk by chunk (rnnt_engine_encode_stream, offset = slot row + position) and the
+    slot is released once the sample's last chunk is encoded.  Fixed slots (O(1) alloc / release,
+    no fragmentation): 2048-slot stores of 35 s samples are ~2 GB, small beside 288 GB of HBM.
+    The free list is host-side; ``alloc=False`` keeps the bookkeeping alone (CPU tests)."""
+
+    def __init__(self, slots, max_frames, device="cuda", alloc=True):
+        if int(slots) <= 0 or int(max_frames) <= 0:
+            raise ValueError("a feature store needs slots > 0 and max_frames > 0")
+        self.slots, self.max_frames = int(slots), int(max_frames)
+        self._free = list(range(self.slots - 1, -1, -1))  # a stack: released slots are reused first
+        self._used = set()
+        self._lock = threading.Lock()
+        self.feats = None
+        if alloc:
+            import torch
+            self.feats = torch.empty((self.slots * self.max_frames, R.trans_input_size), dtype=torch.float32,
+                                     device=device)
+
+    @property
+    def free(self):
+        return len(self._free)
+
+    def alloc(self, k):
+        """Up to k free slots (fewer when the store is short)."""
+        with self._lock:
+            out = [self._free.pop() for _ in range(min(int(k), len(self._free)))]
+            self._used.update(out)
+            return out
+
+    def release(self, slots):
+        with self._lock:
+            for s in slots:
+                if s not in self._used:
+                    raise ValueError(f"feature store slot {s} released while not in use")
+                self._used.remove(s)
+                self._free.append(s)
+
+    def row(self, slot):
+        return int(slot) * self.max_frames
+
+
+class WavFeed:
+    """The producer stage of one Server lane over WAV input (reference ServerSUT::thProducer,
+    torch_sut.cpp:354-468: take up to pro_batch_size queued samples, AssembleSamples +
+    AudioProcessor, enqueue each sample's features for the consumers).  Here the QSL's audio is
+    resident in the lane's device HBM (GpuWavQSL, LoadSamplesToRam), the samples a producer takes
+    are featurized in one launch straight into the lane's FeatureStore, and handed to the lane's
+    engines.  ``ServerSUT(feeds=[...])`` runs one producer thread per feed; feeds on several
+    devices (or several on one) serve one Server instance, each pulling from the shared queue only
+    while its own backlog is short (``ahead``), so work goes where an engine will take it soon.
+
+    qsl: GpuWavQSL on this lane's device; store_slots: FeatureStore size (default: ServerSUT
+    sizes it to the lane's engine slots + ahead); max_frames: a store slot's rows (default the
+    QSL's longest sample)."""
+
+    def __init__(self, qsl, store_slots=None, pro_batch=64, ahead=None, max_frames=None, alloc=True):
+        self.qsl, self.pro_batch, self.ahead = qsl, int(pro_batch), ahead
+        self.store_slots, self.alloc = store_slots, alloc
+        self.max_frames = int(max_frames or max(int(np.max(qsl.lengths)), 1))
+        self.store = None
+        self.batches = 0
+
+    @property
+    def device(self):
+        import torch
+        return torch.device(self.qsl.device).index or 0
+
+    def open(self, slots, ahead):
+        """Sizes the lane (called by ServerSUT once engines are assigned)."""
+        if self.ahead is None:
+            self.ahead = int(ahead)
+        if self.store is None:
+            n = int(self.store_slots or slots + self.ahead)
+            self.store = FeatureStore(n, self.max_frames, device=self.qsl.device, alloc=self.alloc)
+
+    def make_stream(self):
+        import torch
+        return torch.cuda.Stream(device=torch.device("cuda", self.device))
+
+    def featurize(self, indices, slots, stream):
+        """Featurize QSL samples ``indices`` into store ``slots`` (one launch), wait for it; ->
+        their feature lengths (host int32)."""
+        import torch
+        idx = np.asarray(indices, np.int64)
+        wl = self.qsl.wav_lengths[idx].astype(np.int32)
+        dev = self.qsl.store.device
+        with torch.cuda.device(dev), torch.cuda.stream(stream):
+            off = torch.from_numpy(self.qsl.offsets[idx]).to(dev)
+            wld = torch.from_numpy(wl).to(dev)
+            rows = np.array([self.store.row(s) for s in slots], np.int64)
+            self.qsl._featurizer().featurize_rows(self.qsl.store, wld, wl, self.store.feats, rows,
+                                                  self.store.max_frames, offsets=off, stream=stream)
+            stream.synchronize()
+        self.batches += 1
+        return self.qsl.lengths[idx]
+
+
 class ServerSUT:
     """Server scenario SUT with continuous batching (reference ServerSUT, csrc/torch_sut.cpp:238-571,
     PipelineState, csrc/metadata.cpp:97-194; TorchModel::encode's split_len loop, rnnt_model.hpp:62-90).
@@ -379,9 +481,17 @@ class ServerSUT:
     ``flush_queries`` (LoadGen's FlushQueries, lStop_) and then run after the regular queue.
     ``response_size`` of the reference (the minimum number of finished rows per consumer
     iteration, which amortises its CPU iteration) is subsumed: a round is one chunk and answers
-    every slot that finished in it.  Latency per sample = completion - issue time."""
+    every slot that finished in it.  Latency per sample = completion - issue time.
 
-    def __init__(self, engines, qsl, slots=2048, split_len=128, qos_len=None, on_complete=None, pipelined=False):
+    Inputs: ``qsl`` is a feature QSL with an HBM-resident store (GpuQSL), or {device: GpuQSL}
+    replicas for engines on several GPUs.  Over WAV (the reference's processor=true Server,
+    thProducer, torch_sut.cpp:354-468), pass ``feeds``: WavFeed producers, each with its own
+    per-device FeatureStore; engine j is served by feed ``lanes[j]`` (default: the feeds of the
+    engine's device, round-robin), the producers featurize arriving samples into their stores and
+    the engines of a lane take only their lane's samples.  Latency then includes featurization."""
+
+    def __init__(self, engines, qsl=None, slots=2048, split_len=128, qos_len=None, on_complete=None, pipelined=False,
+                 feeds=None, lanes=None):
         import threading
         from .engine import pad_batch
         if split_len <= 0 or split_len % 2:
@@ -392,10 +502,28 @@ class ServerSUT:
         for e in self.engines:
             if e.max_batch < self.slots:
                 raise ValueError(f"engine max_batch {e.max_batch} < {self.slots} slots")
+        self.feeds = list(feeds) if feeds else []
+        if self.feeds:
+            self.lengths = np.asarray(self.feeds[0].qsl.lengths)
+            if any(not np.array_equal(f.qsl.lengths, self.lengths) for f in self.feeds):
+                raise ValueError("every feed must hold the same samples")
+            self.lanes = self._assign_lanes(lanes)
+            for f in range(len(self.feeds)):
+                nl = sum(1 for x in self.lanes if x == f)
+                self.feeds[f].open(nl * self.slots, self.slots)
+        else:
+            if qsl is None:
+                raise ValueError("ServerSUT needs a feature QSL or WAV feeds")
+            self._meta_qsl = next(iter(qsl.values())) if isinstance(qsl, dict) else qsl
+            self.lengths = np.asarray(self._meta_qsl.lengths)
+            self.lanes = [None] * len(self.engines)
         self.on_complete = on_complete
         self.pipelined = bool(pipelined)
         self.responses, self.latency = {}, {}
         self._pending, self._qos = [], []  # (issue_time, QuerySample)
+        self._ready = [collections.deque() for _ in self.feeds]  # per feed: (t0, sample, row, length, slot)
+        self._prod_live = [False] * len(self.feeds)
+        self._lane_workers = collections.Counter(x for x in self.lanes if x is not None)
         self._cv = threading.Condition()
         self._enc_locks = {}
         self._stop = self._flushed = False
@@ -403,13 +531,50 @@ class ServerSUT:
         self.rounds = 0
         self.errors = []
 
+    def _assign_lanes(self, lanes):
+        if lanes is not None:
+            lanes = [int(x) for x in lanes]
+            if len(lanes) != len(self.engines) or any(not 0 <= x < len(self.feeds) for x in lanes):
+                raise ValueError("lanes: one feed index per engine")
+        else:
+            lanes, turn = [], collections.Counter()
+            for e in self.engines:
+                mine = [f for f, fd in enumerate(self.feeds) if fd.device == e.device]
+                if not mine:
+                    raise ValueError(f"no WAV feed on device {e.device}")
+                lanes.append(mine[turn[e.device] % len(mine)])
+                turn[e.device] += 1
+        for e, f in zip(self.engines, lanes):
+            if self.feeds[f].device != e.device:
+                raise ValueError(f"engine on device {e.device} assigned to a feed on device {self.feeds[f].device}")
+        if set(lanes) != set(range(len(self.feeds))):
+            raise ValueError("every feed needs at least one engine")
+        return lanes
+
+    def _store_for(self, j):
+        """(feature store tensor, lane) of engine j."""
+        f = self.lanes[j]
+        if f is not None:
+            return self.feeds[f].store.feats, f
+        q = self.qsl[self.engines[j].device] if isinstance(self.qsl, dict) else self.qsl
+        return q.feats, None
+
     # LoadGen-facing surface -------------------------------------------------------------
     def start(self):
         import threading
         for e in self.engines:
             self._enc_locks.setdefault(e.device, threading.Lock())
+        self._start_producers()
         for j in range(len(self.engines)):
             t = threading.Thread(target=self._worker_pl if self.pipelined else self._worker, args=(j,), daemon=True)
+            t.start()
+            self._threads.append(t)
+
+    def _start_producers(self):
+        import threading
+        for f in range(len(self.feeds)):
+            self._prod_live[f] = True
+            t = threading.Thread(target=self._producer, args=(f,), daemon=True)
             t.start()
             self._threads.append(t)
 
@@ -418,7 +583,7 @@ class ServerSUT:
         now = time.perf_counter() if now is None else now
         with self._cv:
             for s in samples:
-                long_ = self.qos_len is not None and int(self.qsl.lengths[s.index]) > self.qos_len
+                long_ = self.qos_len is not None and int(self.lengths[s.index]) > self.qos_len
                 (self._qos if long_ else self._pending).append((now, s))
             self._cv.notify_all()
 
@@ -435,31 +600,103 @@ class ServerSUT:
         for t in self._threads:
             t.join()
 
+    # producers (WAV feeds) ------------------------------------------------------------------
+    def _source(self):
+        """The queue samples are taken from now: regular first, deferred QoS samples once issuing
+        stopped (torch_sut.cpp:408-414); None when both are empty / held."""
+        if self._pending:
+            return self._pending
+        if self._flushed and self._qos:
+            return self._qos
+        return None
+
+    def _producer(self, f):
+        """thProducer (torch_sut.cpp:354-468) of feed f: while the lane's backlog of featurized,
+        not yet taken samples is under ``ahead`` and its store has room, take up to pro_batch
+        queued samples (a burst is split over the feeds), featurize them into the store in one
+        launch and hand them to the lane's engines."""
+        feed = self.feeds[f]
+        store, ready = feed.store, self._ready[f]
+        try:
+            st = feed.make_stream()
+            while True:
+                with self._cv:
+                    while True:
+                        if self._lane_workers[f] <= 0:  # the lane's engines failed
+                            return
+                        src = self._source()
+                        room = min(store.free, feed.ahead - len(ready))
+                        if src and room > 0:
+                            share = -(-len(src) // len(self.feeds))
+                            k = max(1, min(room, feed.pro_batch, share))
+                            items = src[:k]
+                            del src[:k]
+                            break
+                        if self._stop and src is None:
+                            return
+                        self._cv.wait()
+                slots = store.alloc(len(items))  # only this thread allocates: room >= len(items)
+                try:
+                    lens = feed.featurize([s.index for _, s in items], slots, st)
+                except Exception as ex:  # surface in the caller, never hang the query
+                    store.release(slots)
+                    self.errors.append(ex)
+                    for t0, s in items:
+                        self.latency[s.id] = float("inf")
+                    continue
+                with self._cv:
+                    ready.extend((t0, s, store.row(sl), int(L), sl) for (t0, s), sl, L in zip(items, slots, lens))
+                    self._cv.notify_all()
+        except Exception as ex:
+            self.errors.append(ex)
+        finally:
+            with self._cv:
+                self._prod_live[f] = False
+                self._cv.notify_all()
+
+    def _release(self, lane, slots):
+        """Store slots whose samples are fully encoded go back to the lane's producer."""
+        if lane is None or not len(slots):
+            return
+        self.feeds[lane].store.release(slots)
+        with self._cv:
+            self._cv.notify_all()
+
     # consumer -----------------------------------------------------------------------------
-    def _take(self, k, busy):
-        """Up to k waiting samples for free slots; blocks only while this engine has no busy slot.
-        None: stopped and nothing left for this engine."""
+    def _take(self, k, busy, lane=None):
+        """Up to k samples for free slots, as (issue_time, QuerySample, first store row, frames,
+        store slot or None); blocks only while this engine has no busy slot.  With feeds: the
+        lane's featurized samples.  None: stopped and nothing left for this engine."""
         with self._cv:
             while True:
-                if self._pending:
-                    out = self._pending[:k]
-                    del self._pending[:k]
-                    return out
-                if self._flushed and self._qos:  # torch_sut.cpp:408-414: QoS samples once issuing stopped
-                    out = self._qos[:k]
-                    del self._qos[:k]
-                    return out
-                if busy or k == 0:
-                    return []
-                if self._stop:
-                    return None
+                if lane is not None:
+                    rd = self._ready[lane]
+                    if rd and k > 0:
+                        out = [rd.popleft() for _ in range(min(k, len(rd)))]
+                        self._cv.notify_all()  # the producer may have room again
+                        return out
+                    if busy or k == 0:
+                        return []
+                    if self._stop and not self._prod_live[lane]:
+                        return None
+                else:
+                    src = self._source()
+                    if src and k > 0:
+                        out = src[:k]
+                        del src[:k]
+                        q = self._meta_qsl  # replicas share offsets / lengths
+                        return [(t0, s, int(q.offsets[s.index]), int(q.lengths[s.index]), None) for t0, s in out]
+                    if busy or k == 0:
+                        return []
+                    if self._stop:
+                        return None
                 self._cv.wait()
 
     def _worker(self, j):
         import time
         import torch
         eng = self.engines[j]
-        S, L, qsl = self.slots, self.split_len, self.qsl
+        S, L = self.slots, self.split_len
         dev = torch.device("cuda", eng.device)
         with torch.cuda.device(eng.device):
             st = torch.cuda.Stream(device=dev)
@@ -472,23 +709,23 @@ class ServerSUT:
             d_reset = torch.zeros(S, dtype=torch.int32, device=dev)
             d_lens = torch.zeros(S, dtype=torch.int32, device=dev)
             d_off = torch.zeros(S, dtype=torch.int64, device=dev)
-        store = qsl.feats
+        store, lane = self._store_for(j)
         sample = [None] * S               # (issue_time, QuerySample) per slot
         pos = np.zeros(S, np.int64)       # next frame of the slot's sample
         remain = np.zeros(S, np.int32)    # frames left
         base = np.zeros(S, np.int64)      # first stored row of the slot's sample
+        sslot = [None] * S                # the sample's feature store slot (WAV feeds)
         try:
             while True:
                 free = [i for i in range(S) if sample[i] is None]
-                new = self._take(len(free), busy=len(free) < S)
+                new = self._take(len(free), busy=len(free) < S, lane=lane)
                 if new is None:
                     return
                 rs = h_reset.numpy()
                 rs[:] = 0
-                for i, item in zip(free, new):
-                    sample[i] = item
-                    idx = item[1].index
-                    pos[i], remain[i], base[i] = 0, int(qsl.lengths[idx]), int(qsl.offsets[idx])
+                for i, (t0, smp, row, nfr, sl) in zip(free, new):
+                    sample[i], sslot[i] = (t0, smp), sl
+                    pos[i], remain[i], base[i] = 0, nfr, row
                     rs[i] = 1
                 busy = np.array([x is not None for x in sample])
                 if not busy.any():
@@ -504,10 +741,14 @@ class ServerSUT:
                     with self._enc_locks[eng.device]:  # encoders on one GPU take turns
                         eng.encode_stream(store, d_off, d_lens, cl, d_reset, T, S, S, stream=st)
                         st.synchronize()
-                    eng.decode_stream(res, rl, d_reset, stream=st)
                     pos += cl
                     remain -= cl
                     done = np.nonzero(busy & (remain == 0))[0]
+                    rel = [sslot[i] for i in done]
+                    for i in done:
+                        sslot[i] = None
+                    self._release(lane, rel)  # their features are read
+                    eng.decode_stream(res, rl, d_reset, stream=st)
                     if len(done):
                         di = torch.from_numpy(done).to(dev)
                         lens_d = rl.index_select(0, di)
@@ -530,6 +771,24 @@ class ServerSUT:
             for item in sample:
                 if item is not None:
                     self.latency[item[1].id] = float("inf")
+            self._fail_worker(lane, sslot)
+
+    def _fail_worker(self, lane, held):
+        """A failed engine: its store slots go back; when it was its lane's last engine, what is
+        queued for the lane is answered (latency inf) and the lane's producer stops taking work,
+        so the query still ends."""
+        if lane is None:
+            return
+        self._release(lane, [sl for sl in held if sl is not None])
+        with self._cv:
+            self._lane_workers[lane] -= 1
+            if self._lane_workers[lane] <= 0:
+                rd = self._ready[lane]
+                while rd:
+                    t0, s, _, _, sl = rd.popleft()
+                    self.latency[s.id] = float("inf")
+                    self.feeds[lane].store.release([sl])
+            self._cv.notify_all()
 
 
     def _worker_pl(self, j):
@@ -544,7 +803,7 @@ class ServerSUT:
         import time
         import torch
         eng = self.engines[j]
-        S, L, qsl = self.slots, self.split_len, self.qsl
+        S, L = self.slots, self.split_len
         dev = torch.device("cuda", eng.device)
         NR = 4  # reset-flag ring: round k's flags live until its decode completed (k+3 reuses them)
         with torch.cuda.device(eng.device):
@@ -557,11 +816,12 @@ class ServerSUT:
             d_reset = [torch.zeros(S, dtype=torch.int32, device=dev) for _ in range(NR)]
             d_lens = torch.zeros(S, dtype=torch.int32, device=dev)
             d_off = torch.zeros(S, dtype=torch.int64, device=dev)
-        store = qsl.feats
+        store, lane = self._store_for(j)
         sample = [None] * S
         pos = np.zeros(S, np.int64)
         remain = np.zeros(S, np.int32)
         base = np.zeros(S, np.int64)
+        sslot = [None] * S
         rounds = queue.Queue(maxsize=2)  # (reset ring index, [(slot, (issue_time, QuerySample))])
         started = [0]  # rounds whose decode has been called
         scv = threading.Condition()
@@ -608,15 +868,14 @@ class ServerSUT:
         try:
             while True:
                 free = [i for i in range(S) if sample[i] is None]
-                new = self._take(len(free), busy=len(free) < S)
+                new = self._take(len(free), busy=len(free) < S, lane=lane)
                 if new is None:
                     return
                 rs = h_reset.numpy()
                 rs[:] = 0
-                for i, item in zip(free, new):
-                    sample[i] = item
-                    idx = item[1].index
-                    pos[i], remain[i], base[i] = 0, int(qsl.lengths[idx]), int(qsl.offsets[idx])
+                for i, (t0, smp, row, nfr, sl) in zip(free, new):
+                    sample[i], sslot[i] = (t0, smp), sl
+                    pos[i], remain[i], base[i] = 0, nfr, row
                     rs[i] = 1
                 busy = np.array([x is not None for x in sample])
                 if not busy.any():
@@ -639,8 +898,10 @@ class ServerSUT:
                 pos += cl
                 remain -= cl
                 done = [(int(i), sample[i]) for i in np.nonzero(busy & (remain == 0))[0]]
+                rel = [sslot[i] for i, _ in done]
                 for i, _ in done:
-                    sample[i] = None
+                    sample[i], sslot[i] = None, None
+                self._release(lane, rel)  # their features are read
                 rounds.put((r, done))
                 k += 1
         except Exception as ex:  # surface in the caller, never hang the query
@@ -648,6 +909,7 @@ class ServerSUT:
             for item in sample:
                 if item is not None:
                     self.latency[item[1].id] = float("inf")
+            self._fail_worker(lane, sslot)
         finally:
             rounds.put(None)
             dthread.join()

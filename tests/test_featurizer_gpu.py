@@ -81,6 +81,41 @@ def test_offsets_and_batch_invariance(fz):
     np.testing.assert_array_equal(c.cpu().numpy()[:, 0].view(np.uint32), a.cpu().numpy()[:, 4].view(np.uint32))
 
 
+def test_ragged_rows_equal_padded_batch(fz):
+    """rnnt_featurizer_run_rows (the Server feature store's entry): each sample's frames land as
+    240-channel rows at its row offset, bit-identical to its column of the padded batch, and no
+    other store row is touched (sentinel)."""
+    from rnnt_amd._lib import EngineError
+    L = [48000, 3200, 0, 777, 150000, 1]
+    wavs = synthetic.make_wavs(L, seed=26)
+    flat = torch.cat([w.cuda() for w in wavs] + [torch.zeros(1, device="cuda")])
+    off = torch.tensor(np.concatenate([[0], np.cumsum(L)[:-1]]), dtype=torch.int64, device="cuda")
+    lens = torch.tensor(L, dtype=torch.int32)
+    fr = [OF.frames(v)[1] for v in L]
+    a, al = fz.featurize(flat, lens.cuda(), lens.numpy(), n_pad=8, T_out=max(fr), offsets=off)
+    store = torch.full((4000, 240), 7.25, device="cuda")
+    rows = np.array([3000, 10, 2000, 400, 1000, 3990], np.int64)  # out of order, gaps between
+    fl = fz.featurize_rows(flat, lens.cuda(), lens.numpy(), store, rows, max_frames=max(fr), offsets=off)
+    torch.cuda.synchronize()
+    assert fl.cpu().tolist()[:len(L)] == fr == al.cpu().tolist()[:len(L)]
+    s, g = store.cpu().numpy(), a.cpu().numpy()
+    used = np.zeros(len(s), bool)
+    for i, (r, T) in enumerate(zip(rows, fr)):
+        np.testing.assert_array_equal(s[r:r + T].view(np.uint32), g[:T, i, :240].view(np.uint32), err_msg=f"row {i}")
+        used[r:r + T] = True
+    assert np.all(s[~used] == 7.25)
+    with pytest.raises(ValueError, match="outside the store"):
+        fz.featurize_rows(flat, lens.cuda(), lens.numpy(), store, rows + 600, max_frames=max(fr), offsets=off)
+    with pytest.raises(ValueError, match="max_frames"):
+        fz.featurize_rows(flat, lens.cuda(), lens.numpy(), store, rows, max_frames=max(fr) - 1, offsets=off)
+    with pytest.raises(EngineError):  # the C ABI's own check
+        from rnnt_amd import _lib
+        _lib.check(_lib.lib().rnnt_featurizer_run_rows(fz._h, flat.data_ptr(), off.data_ptr(), 0, lens.cuda().data_ptr(),
+                                                       lens.numpy().ctypes.data, len(L), store.data_ptr(),
+                                                       torch.zeros(len(L), dtype=torch.int64, device="cuda").data_ptr(),
+                                                       fl.data_ptr(), max(fr) - 1, None), "run_rows")
+
+
 def test_forward_mirror_layout(fz):
     wavs = synthetic.make_wavs([16000, 8000, 4000], seed=23)
     x, lens = _batch(wavs)
