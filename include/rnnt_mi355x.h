@@ -215,7 +215,9 @@ typedef struct {
 int rnnt_engine_set_profiling(rnnt_engine* e, int on);
 /* Tick tile shape of the int8 encoder: "auto" (per tick, the cost model; the default), or pinned
  * to "big" (256 x 256), "small" (128 x 128, 2-deep ring), "tiny" (128 x 128, 4-deep) or "mini"
- * (64 x 128, 4-deep) -- results are identical (int32 accumulation); for tests and sweeps.  The
+ * (64 x 128, 4-deep) -- results are identical (int32 accumulation); for tests and sweeps.  "flow":
+ * whole-call encodes of batches with n_pad <= 256 run as one persistent dataflow launch (opt-in:
+ * measured slower than the ticks on config 3); "ticks" = "auto".  The
  * environment variable RNNT_ENC_TILE sets an engine's initial value at create. */
 int rnnt_engine_set_tile(rnnt_engine* e, const char* tile);
 int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset);

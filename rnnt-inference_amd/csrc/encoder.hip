@@ -115,6 +115,8 @@ using MiniTile = TileCfg<1, 4, 4>;
 // workgroup per CU: a K loop with one stage in flight is latency-bound there (weights stream
 // from MALL / HBM at small batch)
 using TinyTile = TileCfg<2, 4, 4>;
+// the flow kernel's task tile: 128 gate x 128 batch rows, 4-deep ring (one workgroup per CU)
+using FlowTile = TinyTile;
 static_assert(BigTile::BN == ENC_BATCH_TILE && SmallTile::BN == ENC_ROW_TILE, "engine batch tiles");
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -143,12 +145,35 @@ __device__ __forceinline__ void wait_stage(int later) {
   }
 }
 
-template <int WMT, int WNT, int NBUF>
+// 16-byte copy-out store: plain, or write-through (WT: `sc1`, the line leaves the XCD's L2 at
+// once) for outputs another workgroup of the same launch reads -- the flow kernel's hand-offs,
+// which then need no release fence before the completion count (guide R1 publish)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <bool WT>
+__device__ __forceinline__ void st16(void* base, size_t off, uint4 v) {
+  if (WT) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7ffffff0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{v.x, v.y, v.z, v.w}, r, (int)off, 0, 16);  // aux 16 = sc1
+  } else {
+    *(uint4*)((char*)base + off) = v;
+  }
+}
+struct NoWait {
+  __device__ void operator()() const {}
+};
+
+// One (gate tile mt, batch tile nt) of a layer-step.  WT: write-through hand-off stores (flow
+// kernel); hwait() runs (uniformly, every wave) right before the first stage of the recurrent
+// half [h_{t-1}] is issued -- the flow kernel's wait for the previous step of the layer.
+template <int WMT, int WNT, int NBUF, bool WT = false, class HWait = NoWait>
 __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int nt, int8_t* smem,
-                                             unsigned long long st_t0) {
+                                             unsigned long long st_t0, HWait&& hwait = HWait{},
+                                             unsigned long long st_t1 = 0ull, unsigned long long st_tag = 0ull) {
   using C = TileCfg<WMT, WNT, NBUF>;
   constexpr int BM = C::BM, BN = C::BN, STAGE = C::STAGE;
   (void)st_t0;
+  (void)st_t1;
+  (void)st_tag;
 #ifdef RNNT_DEV_STAMPS
   unsigned est_k;
   {
@@ -207,6 +232,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
         __builtin_amdgcn_global_load_lds((glb_void*)(xbase + (size_t)(8 * j) * a.I + k + ((j & 1) ? oX1 : oX0)),
                                          (lds_void*)(st + j * 1024), 16, 0, 0);
     } else {
+      if (k == a.I) {
+        hwait();
+        if (WT) EST_PUT(7, __builtin_amdgcn_s_memrealtime());  // flow: its recurrent state was ready
+      }
 #pragma unroll
       for (int j = 0; j < C::PB; ++j)
         __builtin_amdgcn_global_load_lds((glb_void*)(hbase + (size_t)(8 * j) * H + k + ((j & 1) ? oH1 : oH0)),
@@ -253,7 +282,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 #ifdef RNNT_DEV_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stamps only: stage 0 landed (this wave)
   EST_PUT(3, __builtin_amdgcn_s_memrealtime());
-  EST_PUT(6, __builtin_amdgcn_s_memtime());
+  EST_PUT(6, WT ? st_t1 : __builtin_amdgcn_s_memtime());  // flow: its input frame was ready
 #endif
   for (int s = 0; s < nS; ++s) {
     // this wave's DMA of stage s has landed (only later stages' pieces may be outstanding) and
@@ -288,7 +317,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #ifdef RNNT_DEV_STAMPS
   EST_PUT(4, __builtin_amdgcn_s_memrealtime());
-  EST_PUT(7, __builtin_amdgcn_s_memtime());
+  if (!WT) EST_PUT(7, __builtin_amdgcn_s_memtime());
 #endif
 
   // ---- fused LSTM cell epilogue (quant_lstm.py:162-183 semantics; oracle_enc_cell)
@@ -370,32 +399,32 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   for (int it = 0; it < (BN * C::CPR + NWAVE * 64 - 1) / (NWAVE * 64); ++it) {  // c (and bf16 f): BN rows x CROW bytes
     const int idx = it * NWAVE * 64 + tid, r = idx / C::CPR, ch = idx % C::CPR;
     if ((BN * C::CPR) % (NWAVE * 64) != 0 && idx >= BN * C::CPR) break;
-    *(uint4*)(a.c + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(smem + cbuf + cimg_off<C::CROW>(r, ch * 16));
-    if (a.mode == ENC_OUT_FINAL)
+    st16<WT>(a.c, ((size_t)(n0 + r) * H + um + ch * 8) * 2, *(const uint4*)(smem + cbuf + cimg_off<C::CROW>(r, ch * 16)));
+    if (a.mode == ENC_OUT_FINAL)  // read after the launch only: plain
       *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + cimg_off<C::CROW>(r, ch * 16));
   }
 #pragma unroll
   for (int it = 0; it < (BN * C::HC + NWAVE * 64 - 1) / (NWAVE * 64); ++it) {  // h, y: BN rows x BM / 4 bytes
     const int idx = it * NWAVE * 64 + tid, r = idx / C::HC, ch = idx % C::HC, n = n0 + r;
     if ((BN * C::HC) % (NWAVE * 64) != 0 && idx >= BN * C::HC) break;
-    *(uint4*)(a.h_out + (size_t)n * H + um + ch * 16) = *(const uint4*)(hs + r * HP + ch * 16);
+    st16<WT>(a.h_out, (size_t)n * H + um + ch * 16, *(const uint4*)(hs + r * HP + ch * 16));
     if (a.mode == ENC_OUT_I8) {
-      *(uint4*)(a.y8 + (size_t)n * H + um + ch * 16) = *(const uint4*)(ys + r * HP + ch * 16);
+      st16<WT>(a.y8, (size_t)n * H + um + ch * 16, *(const uint4*)(ys + r * HP + ch * 16));
     } else if (a.mode == ENC_OUT_STACKED) {
       // StackTime (modeling_rnnt.py:314-324): frame t -> stacked frame t/2, half t%2;
       // frames t >= x_lens[n] are zeroed; the odd-T pad frame is zero too.
-      int8_t* dst = a.y8 + (size_t)n * (2 * H) + um + ch * 16;
+      const size_t dst = (size_t)n * (2 * H) + um + ch * 16;
       uint4 v = *(const uint4*)(ys + r * HP + ch * 16);
       if (a.t >= a.lens[n]) v = uint4{0u, 0u, 0u, 0u};  // a value select: no pointer select into a stack temporary
-      *(uint4*)(dst + a.half * H) = v;
-      if (a.zero_next) *(uint4*)(dst + H) = uint4{0u, 0u, 0u, 0u};
+      st16<WT>(a.y8, dst + a.half * H, v);
+      if (a.zero_next) st16<WT>(a.y8, dst + H, uint4{0u, 0u, 0u, 0u});
     }
   }
 #ifdef RNNT_DEV_STAMPS
   EST_PUT(5, __builtin_amdgcn_s_memrealtime());
   EST_PUT(0, (unsigned long long)K | ((unsigned long long)mt << 16) | ((unsigned long long)nt << 24) |
                  ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 32));  // HW_REG_HW_ID
-  EST_PUT(1, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20));        // HW_REG_XCC_ID
+  EST_PUT(1, WT ? st_tag : (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20));  // flow: step; XCC_ID
 #endif
 }
 
@@ -457,7 +486,113 @@ __global__ void __launch_bounds__(NWAVE * 64) lstm_i8_tick_kernel(EncTickArgs ar
                          __builtin_amdgcn_readfirstlane(nt), smem, st_t0);
 }
 
+// ---------------------------------------------------------------- persistent dataflow encoder
+// Small batches (config 3: N = 128, T <= 500) are latency-bound on the tick path: ~505 dependent
+// launches whose every workgroup re-stages its operands from a cold start.  Here one launch holds
+// one workgroup per CU; each takes tasks (layer-step, 128-row gate tile, 128-row batch tile) from a
+// device queue in tick order and runs the tick kernel's step body on them.  A task waits for the
+// completion counter of the step that wrote its input frame before it starts, and for the counter
+// of its layer's previous step only right before the first recurrent [h_{t-1}] stage is issued, so
+// the input half of the K loop runs while the previous step finishes.
+// Hand-offs (MI355X guide, Guideline 16): outputs read inside the launch (h, c, the int8 frame)
+// are stored write-through (`sc1`); every wave drains its stores, the workgroup meets at a
+// barrier and lane 0 adds 1 to the step's counter (relaxed, agent scope).  A waiting workgroup
+// polls one counter from one lane (relaxed, `s_sleep` between polls), then ONE agent-scope
+// acquire, its drain and a barrier, before any load of the handed-off bytes.
+// Progress needs no dispatch-order assumption: a task depends only on steps of earlier ticks,
+// whose tasks were dequeued earlier by workgroups that are running.  Every wait is bounded: past
+// the timeout it raises the launch's abort word and every workgroup drains (the host reports it).
+// Control flow around the waits is wave-uniform: wave 0 polls as a whole (every lane loads the
+// same word; the value is made uniform with readfirstlane), so no lane-divergent branch encloses a
+// barrier or the task loop's back edge (a lane-0-only branch there let the compiler's CFG
+// structurizer run lanes 1-63 of wave 0 into the next iteration's barrier ahead of lane 0).
+__device__ __forceinline__ unsigned flow_load(const uint32_t* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// wave 0: poll until step dep has `need` completed tasks (or the launch aborts / this wait times out)
+__device__ __forceinline__ void flow_spin(const EncFlowArgs& f, int dep, unsigned need) {
+  uint32_t* abort_w = f.ctr + f.n_steps + 1;
+  const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + f.timeout;
+  while (flow_load(f.ctr + dep) < need) {
+    if (flow_load(abort_w)) return;
+    if (__builtin_amdgcn_s_memrealtime() > t_end) {
+      __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+__device__ __forceinline__ void flow_acquire() {  // wave 0; the other waves meet it at a barrier
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int WMT, int WNT, int NBUF>
+__global__ void __launch_bounds__(NWAVE * 64) lstm_i8_flow_kernel(EncFlowArgs f) {
+  using C = TileCfg<WMT, WNT, NBUF>;
+  static_assert(C::NGT == ENC_FLOW_NGT, "flow task blocks");
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  // [0] task index, [1] recurrent input ready (an LDS pointer: ds ops, not flat)
+  volatile __attribute__((address_space(3))) int* slot =
+      (volatile __attribute__((address_space(3))) int*)((lds_char*)(lds_void*)smem + C::SMEM);
+  const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;  // wave-uniform
+  const bool l0 = (threadIdx.x & 63) == 0;
+#pragma unroll
+  for (int i = 0; i < ENC_TAB_N / (2 * NWAVE * 64); ++i)  // sigma table: once per workgroup
+    ((float4*)(smem + C::TAB_OFF))[i * NWAVE * 64 + threadIdx.x] = ((const float4*)g_act_tab)[i * NWAVE * 64 + threadIdx.x];
+  uint32_t* head = f.ctr + f.n_steps;
+  // the next task index is taken from the queue while the current task runs (wave 0, lane 0)
+  unsigned nxt = 0;
+  if (w0 && l0) nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (w0) slot[0] = flow_load(head + 1) ? f.n_tasks : (int)__builtin_amdgcn_readfirstlane(nxt);
+    __syncthreads();
+    const int ti = __builtin_amdgcn_readfirstlane(slot[0]);
+    if (ti >= f.n_tasks) return;
+    unsigned long long t_deq = 0ull, t_x = 0ull;
+    EST_MARK(t_deq);
+    const uint32_t blk = f.blocks[ti / C::NGT];
+    const int si = __builtin_amdgcn_readfirstlane((int)(blk & 0xffffu));
+    const int nt = __builtin_amdgcn_readfirstlane((int)(blk >> 16)), mt = ti % C::NGT;
+    const EncFlowStep S = f.steps[si];
+    // the input frame: wait; the recurrent state: note whether it is ready already (then one
+    // acquire covers both and the mid-loop wait is skipped)
+    if (w0) {
+      if (S.dep_x >= 0) flow_spin(f, S.dep_x, S.need_x);
+      const bool hr = S.dep_h < 0 || flow_load(f.ctr + S.dep_h) >= S.need_h;
+      if (S.dep_x >= 0 || (S.dep_h >= 0 && hr)) flow_acquire();
+      slot[1] = hr;
+    }
+    __syncthreads();
+    const bool h_ready = __builtin_amdgcn_readfirstlane(slot[1]) != 0;
+    EST_MARK(t_x);
+    if (w0 && l0) nxt = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lstm_i8_step<WMT, WNT, NBUF, true>(S.a, mt, nt, smem, t_deq, [&]() {
+      if (h_ready) return;
+      if (w0) {
+        flow_spin(f, S.dep_h, S.need_h);
+        flow_acquire();
+      }
+      __builtin_amdgcn_s_barrier();  // no LDS / memory wait: the other waves' stage DMA stays in flight
+    }, t_x, (unsigned long long)si);
+    // publish: every wave's write-through stores have landed, then one count
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (w0 && l0) __hip_atomic_fetch_add(f.ctr + si, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
+int launch_lstm_i8_flow(const EncFlowArgs& f, int grid, hipStream_t st) {
+  using C = FlowTile;
+  static std::atomic<uint64_t> attr{0};
+  const void* fn = (const void*)lstm_i8_flow_kernel<C::BM / 64, C::BN / 32, C::NBUF>;
+  if (set_smem_attr_once(fn, C::SMEM + 16, attr)) return -1;
+  hipLaunchKernelGGL((lstm_i8_flow_kernel<C::BM / 64, C::BN / 32, C::NBUF>), dim3(grid), dim3(NWAVE * 64), C::SMEM + 16,
+                     st, f);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStream_t st) {
   const int64_t n4 = n / 4;
   int grid = (int)((n4 + 255) / 256);
@@ -510,7 +645,7 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st, int forced) {
     if (a.job[j].I % 128 != 0 || a.nbt[j] < 0) return -1;
   const int gb = tick_grid<BigTile>(a), gs = tick_grid<SmallTile>(a), gm = tick_grid<MiniTile>(a);
   if (gb <= 0) return 0;
-  int choice = forced;
+  int choice = forced == ENC_TILE_FLOW || forced == ENC_TILE_TICKS ? ENC_TILE_AUTO : forced;  // (flow: engine-level)
   if (choice == ENC_TILE_AUTO) {
     const float rb = (float)((gb + ENC_CUS - 1) / ENC_CUS);
     const float rs = fmaxf((float)gs / (2 * ENC_CUS) * ENC_SMALL_ROUND, ENC_SMALL_FLOOR);

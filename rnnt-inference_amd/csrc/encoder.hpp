@@ -56,8 +56,32 @@ int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStrea
 // t < lens[i]; out int8 [T][n_pad][256], zero past the length, in channels 240..255 and rows >= n.
 int launch_quantize_gather(const float* store, const int64_t* offsets, const int32_t* lens, int T, int n, int n_pad,
                            float s, int8_t* out, hipStream_t st);
-// tick tile shape: chosen per tick by the cost model (ENC_TILE_AUTO) or pinned (tests, sweeps)
-enum { ENC_TILE_AUTO = 0, ENC_TILE_BIG = 1, ENC_TILE_SMALL = 2, ENC_TILE_TINY = 3, ENC_TILE_MINI = 5 };
+// tick tile shape: chosen per tick by the cost model (ENC_TILE_AUTO) or pinned (tests, sweeps);
+// ENC_TILE_FLOW: a whole-call encode of a small batch runs as one persistent dataflow launch
+// (lstm_i8_flow_kernel) instead of one launch per tick (the tick path treats it as AUTO)
+enum { ENC_TILE_AUTO = 0, ENC_TILE_BIG = 1, ENC_TILE_SMALL = 2, ENC_TILE_TINY = 3, ENC_TILE_MINI = 5, ENC_TILE_FLOW = 6,
+       ENC_TILE_TICKS = 7 };
 int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st, int forced = ENC_TILE_AUTO);
+
+// ---- persistent dataflow encoder (small batches: at most ENC_FLOW_MAX_TILES active 128-row tiles)
+// The wavefront schedule's layer-steps become tasks of one launch: task = (layer-step, 128-row gate
+// tile, 128-row batch tile), dealt from a device queue in tick order; a task waits on per-step
+// completion counters for its input frame (layer l-1) and its recurrent h (layer l at t-1), and
+// publishes its outputs write-through before counting itself done.
+constexpr int ENC_FLOW_NGT = 32;        // gate tiles per layer-step (the 128 x 128 tile)
+constexpr int ENC_FLOW_MAX_TILES = 2;   // batch tiles (n_pad <= 256)
+struct EncFlowStep {
+  EncStepArgs a;
+  int dep_x, dep_h;       // step whose completion the input frame / the recurrent state needs (-1: none)
+  unsigned need_x, need_h;  // its task count
+};
+struct EncFlowArgs {
+  const EncFlowStep* steps;   // [n_steps], tick order
+  const uint32_t* blocks;     // [n_tasks / ENC_FLOW_NGT]: step | batch tile << 16 (gate tile = task % NGT)
+  uint32_t* ctr;              // [n_steps] done tasks, [n_steps] queue head, [n_steps + 1] abort flag
+  int n_tasks, n_steps;
+  unsigned long long timeout; // s_memrealtime ticks (100 MHz) one wait may spin before it aborts the launch
+};
+int launch_lstm_i8_flow(const EncFlowArgs& f, int grid, hipStream_t st);
 
 }  // namespace rnnt

@@ -51,7 +51,7 @@ struct rnnt_engine {
   hipStream_t stream = nullptr;
   rnnt_opts opts{};
   int np_max = 0, tp_max = 0;
-  int tile = ENC_TILE_AUTO;  // tick tile shape (rnnt_engine_set_tile; RNNT_ENC_TILE at create)
+  int tile = ENC_TILE_AUTO;  // tick tile shape / flow (rnnt_engine_set_tile; RNNT_ENC_TILE at create)
   // packed weights
   int8_t* enc_w[5] = {};
   float* enc_bq[5] = {};
@@ -113,6 +113,17 @@ struct rnnt_engine {
   int32_t* f32_flen = nullptr;
   DecF32State ds32{};
   int last32_T = 0, last32_n = 0, last32_npad = 0;
+  // persistent dataflow encoder (small batches, lstm_i8_flow_kernel): step table + task blocks on
+  // the device (flow_dev), staged through pinned host memory (flow_host; flow_up_ev: the last
+  // upload has consumed it), per-step counters (flow_ctr) and the last launch's abort word read
+  // back into flow_abort (flow_done_ev)
+  char *flow_dev = nullptr, *flow_host = nullptr;
+  uint32_t* flow_ctr = nullptr;
+  uint32_t* flow_abort = nullptr;
+  size_t flow_cap = 0;  // steps
+  hipEvent_t flow_up_ev = nullptr, flow_done_ev = nullptr;
+  bool flow_up_pending = false, flow_check = false;
+  int64_t flow_launches = 0;
   // operator-level decode: unfinished-row counter for greedy_decode_update's return value
   int32_t* op_count = nullptr;
   int32_t* op_count_host = nullptr;
@@ -350,6 +361,13 @@ extern "C" void rnnt_engine_destroy(rnnt_engine* e) {
   for (void* p : e->f32_ws) (void)hipFree(p);
   if (e->op_count_host) (void)hipHostFree(e->op_count_host);
   if (e->host_flags) (void)hipHostFree(e->host_flags);
+  for (auto ev : {e->flow_up_ev, e->flow_done_ev})
+    if (ev) {
+      (void)hipEventSynchronize(ev);
+      (void)hipEventDestroy(ev);
+    }
+  if (e->flow_host) (void)hipHostFree(e->flow_host);
+  if (e->flow_abort) (void)hipHostFree(e->flow_abort);
   for (auto ev : e->poll_ev)
     if (ev) (void)hipEventDestroy(ev);
   for (auto ev : {e->pl_copy_ev[0], e->pl_copy_ev[1], e->pl_handoff_ev})
@@ -368,13 +386,15 @@ static int tile_code(const char* s) {
   if (!strcmp(s, "small")) return ENC_TILE_SMALL;
   if (!strcmp(s, "tiny")) return ENC_TILE_TINY;
   if (!strcmp(s, "mini")) return ENC_TILE_MINI;
+  if (!strcmp(s, "flow")) return ENC_TILE_FLOW;
+  if (!strcmp(s, "ticks")) return ENC_TILE_TICKS;
   return -1;
 }
 
 extern "C" int rnnt_engine_set_tile(rnnt_engine* e, const char* tile) {
   if (!e || !tile) return fail(RNNT_EINVAL, "null argument");
   const int v = tile_code(tile);
-  if (v < 0) return fail(RNNT_EINVAL, std::string("unknown tick tile '") + tile + "': auto|big|small|tiny|mini");
+  if (v < 0) return fail(RNNT_EINVAL, std::string("unknown tick tile '") + tile + "': auto|ticks|flow|big|small|tiny|mini");
   e->tile = v;
   return 0;
 }
@@ -402,7 +422,7 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
   if (const char* t = getenv("RNNT_ENC_TILE")) {  // development default, read once per engine
     const int v = tile_code(t);
-    if (v < 0) r = fail(RNNT_EINVAL, std::string("RNNT_ENC_TILE=") + t + ": auto|big|small|tiny|mini");
+    if (v < 0) r = fail(RNNT_EINVAL, std::string("RNNT_ENC_TILE=") + t + ": auto|ticks|flow|big|small|tiny|mini");
     e->tile = v < 0 ? ENC_TILE_AUTO : v;
   }
   if (!r && model) r = pack_model(e, model);
@@ -645,6 +665,122 @@ struct EncInput {
   const int64_t* offsets = nullptr;
 };
 
+// ---- persistent dataflow encode (lstm_i8_flow_kernel, encoder.hpp): the wavefront schedule's
+// layer-steps as one launch's task list.  Used for small batches (n_pad <= 256) when the engine's
+// tile setting is "flow" (or "auto", see flow_wanted).
+static bool flow_wanted(const rnnt_engine* e, int n_pad) {
+  return e->tile == ENC_TILE_FLOW && n_pad <= ENC_FLOW_MAX_TILES * ENC_ROW_TILE;
+}
+
+static int flow_alloc(rnnt_engine* e) {
+  if (e->flow_dev) return 0;
+  const size_t cap = 2 * (size_t)e->opts.max_frames + 3 * (size_t)e->tp_max + 8;
+  const size_t bytes = cap * sizeof(EncFlowStep) + cap * ENC_FLOW_MAX_TILES * sizeof(uint32_t);
+  int r = dev_alloc(e, &e->flow_dev, bytes);
+  if (!r) r = dev_alloc(e, &e->flow_ctr, cap + 4);
+  if (r) return r;
+  HIPCHK(hipHostMalloc((void**)&e->flow_host, bytes, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void**)&e->flow_abort, sizeof(uint32_t), hipHostMallocDefault));
+  *e->flow_abort = 0;
+  HIPCHK(hipEventCreateWithFlags(&e->flow_up_ev, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&e->flow_done_ev, hipEventDisableTiming));
+  e->flow_cap = cap;
+  return 0;
+}
+
+// the last flow launch's abort word, once its read-back has landed (non-blocking)
+static int flow_poll(rnnt_engine* e) {
+  if (!e->flow_check || hipEventQuery(e->flow_done_ev) != hipSuccess) return 0;
+  e->flow_check = false;
+  if (*e->flow_abort) {
+    *e->flow_abort = 0;
+    return fail(RNNT_EDEVICE, "encoder flow launch aborted: a task waited past its timeout (its outputs are invalid)");
+  }
+  return 0;
+}
+
+template <class Tiles>
+static int run_flow(rnnt_engine* e, int T, int n_pad, const int32_t* lens, float* f_out, Tiles tiles, hipStream_t st) {
+  int r = flow_alloc(e);
+  if (r) return r;
+  if (e->flow_up_pending) HIPCHK(hipEventSynchronize(e->flow_up_ev));  // the staging buffer is free again
+  e->flow_up_pending = false;
+  const int Tp = (T + 1) / 2;
+  EncFlowStep* steps = (EncFlowStep*)e->flow_host;
+  uint32_t* blocks = (uint32_t*)(e->flow_host + e->flow_cap * sizeof(EncFlowStep));
+  std::vector<int> sid[5];  // step index of (layer, frame), -1: no tasks
+  std::vector<int> snbt;
+  for (int l = 0; l < 5; ++l) sid[l].assign(l < 2 ? T : Tp, -1);
+  int ns = 0, nb = 0;
+  const unsigned NGT = ENC_FLOW_NGT;
+  auto need = [&](int s) { return s < 0 ? 0u : NGT * (unsigned)snbt[s]; };
+  struct Job { int l, t; EncStepArgs a; int nbt; };
+  const int n_ticks = std::max(T + 1, 2 * Tp + 4);
+  for (int tau = 0; tau < n_ticks; ++tau) {
+    Job jobs[5];
+    int nj = 0;
+    // the tick loop's jobs (encode_impl), ordered by K descending like TickBuilder
+    if (tau < T) jobs[nj++] = {0, tau, make_job(e, 0, tau, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, lens, T), tiles(2 * (tau / 2))};
+    if (tau >= 1 && tau - 1 < T)
+      jobs[nj++] = {1, tau - 1, make_job(e, 1, tau - 1, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, lens, T),
+                    tiles(2 * ((tau - 1) / 2))};
+    for (int l = 2; l < 5; ++l) {
+      const int d = tau - (l + 1);
+      if (d >= 0 && (d & 1) == 0 && d / 2 < Tp) {
+        const int tp = d / 2;
+        EncStepArgs a = l == 2   ? make_job(e, 2, tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, lens, T)
+                        : l == 3 ? make_job(e, 3, tp, n_pad, e->yB, ENC_OUT_I8, e->yC, nullptr, lens, T)
+                                 : make_job(e, 4, tp, n_pad, e->yC, ENC_OUT_FINAL, e->fbf, f_out, lens, T);
+        jobs[nj++] = {l, tp, a, tiles(2 * tp)};
+      }
+    }
+    std::stable_sort(jobs, jobs + nj, [](const Job& x, const Job& y) { return x.a.I > y.a.I; });
+    for (int j = 0; j < nj; ++j) {
+      const Job& jb = jobs[j];
+      if (jb.nbt <= 0) continue;
+      if (jb.nbt > ENC_FLOW_MAX_TILES || ns >= (int)e->flow_cap) return fail(RNNT_EINVAL, "flow encode: batch too large");
+      // input frame: layer l-1 at the same frame (layer 2: the odd half of stacked frame t', i.e.
+      // feature frame 2t'+1, or 2t' for an odd-T pad; its completion implies 2t''s); recurrent
+      // state: layer l at t-1
+      int dx = -1;
+      if (jb.l == 1) dx = sid[0][jb.t];
+      else if (jb.l == 2) dx = sid[1][std::min(2 * jb.t + 1, T - 1)];
+      else if (jb.l > 2) dx = sid[jb.l - 1][jb.t];
+      const int dh = jb.t > 0 ? sid[jb.l][jb.t - 1] : -1;
+      EncFlowStep& s = steps[ns];
+      s.a = jb.a;
+      s.dep_x = dx;
+      s.need_x = need(dx);
+      s.dep_h = dh;
+      s.need_h = need(dh);
+      for (int nt = 0; nt < jb.nbt; ++nt) blocks[nb++] = (uint32_t)ns | ((uint32_t)nt << 16);
+      sid[jb.l][jb.t] = ns++;
+      snbt.push_back(jb.nbt);
+    }
+  }
+  if (ns == 0) return 0;
+  EncFlowArgs f{};
+  f.steps = (const EncFlowStep*)e->flow_dev;
+  f.blocks = (const uint32_t*)(e->flow_dev + e->flow_cap * sizeof(EncFlowStep));
+  f.ctr = e->flow_ctr;
+  f.n_steps = ns;
+  f.n_tasks = nb * ENC_FLOW_NGT;
+  f.timeout = 200000000ull;  // 2 s at 100 MHz: a config-3 encode takes a few ms
+  HIPCHK(hipMemcpyAsync(e->flow_dev, e->flow_host, (size_t)ns * sizeof(EncFlowStep), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync((void*)f.blocks, blocks, (size_t)nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  HIPCHK(hipEventRecord(e->flow_up_ev, st));
+  e->flow_up_pending = true;
+  HIPCHK(hipMemsetAsync(e->flow_ctr, 0, ((size_t)ns + 2 + 3) / 4 * 16, st));
+  const int grid = std::min(f.n_tasks, 256);
+  if (launch_lstm_i8_flow(f, grid, st)) return fail(RNNT_EDEVICE, "flow encode launch failed");
+  HIPCHK(hipMemcpyAsync(e->flow_abort, e->flow_ctr + ns + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(e->flow_done_ev, st));
+  e->flow_check = true;
+  e->flow_launches++;
+  e->step_launches++;
+  return 0;
+}
+
 // reset == nullptr: a batch of whole utterances (every row's state starts at zero); otherwise a
 // stream chunk (rnnt_engine_encode_stream): rows keep their state unless flagged.
 static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, const int32_t* lens_host, int T, int n,
@@ -655,6 +791,7 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
   if (r) return r;
   DEVICE_SCOPE(e->device);
   hipStream_t st = pick(e, stream);
+  if ((r = flow_poll(e))) return r;
   if (!pl && (r = state_acquire(e, st))) return r;
   const int Tp = (T + 1) / 2;
   const std::vector<int> tm = tile_maxima(lens_host, n, n_pad);
@@ -682,7 +819,8 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
   // their inputs exist.  Every job of a tick is independent (inputs come from earlier ticks).
   const int nt_all = n_pad / ENC_ROW_TILE;
   auto tiles = [&](int thr) { return tm.empty() ? nt_all : active_tiles(tm, thr); };
-  const int n_ticks = std::max(T + 1, 2 * Tp + 4);
+  const int n_ticks = flow_wanted(e, n_pad) ? 0 : std::max(T + 1, 2 * Tp + 4);
+  if (!n_ticks && (r = run_flow(e, T, n_pad, lens, f_out, tiles, st))) return r;
   for (int tau = 0; tau < n_ticks; ++tau) {
     TickBuilder tb;
     if (tau < T) tb.add(make_job(e, 0, tau, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, lens, T), tiles(2 * (tau / 2)));
@@ -789,7 +927,7 @@ static int decode_core(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
   e->decode_steps += steps;
   if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});
   e->decode_calls++;
-  return 0;
+  return flow_poll(e);  // the greedy loop has synchronised with the encode: report an aborted flow launch
 }
 
 static int decode_impl(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_res, void* stream,

@@ -214,8 +214,10 @@ class Engine:
         _lib.check(self._lib.rnnt_engine_set_profiling(self._h, int(bool(on))), "rnnt_engine_set_profiling")
 
     def set_tile(self, tile="auto"):
-        """Pin the int8 encoder's tick tile ("big" / "small" / "tiny" / "mini") or restore the
-        per-tick choice ("auto"); results are bit-identical either way (rnnt_engine_set_tile)."""
+        """Pin the int8 encoder's tick tile ("big" / "small" / "tiny" / "mini"), restore the
+        per-tick choice ("auto" = "ticks"), or run whole-call encodes of small batches (n_pad <= 256)
+        as one persistent dataflow launch ("flow"); results are bit-identical
+        either way (rnnt_engine_set_tile)."""
         _lib.check(self._lib.rnnt_engine_set_tile(self._h, str(tile).encode()), "rnnt_engine_set_tile")
 
     def stats(self, reset=True):

@@ -27,7 +27,7 @@ def engine(model):
     e.close()
 
 
-@pytest.fixture(params=["big", "small", "tiny", "mini"])
+@pytest.fixture(params=["big", "small", "tiny", "mini", "flow"])
 def tile(request, engine):
     """Every encoder tile variant (256 x 256; 128 x 128 with a 2- and a 4-deep stage ring;
     64 x 128 with a 4-deep ring, encoder.hip) pinned in turn (rnnt_engine_set_tile); the engine

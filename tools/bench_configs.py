@@ -50,10 +50,23 @@ def main():
     ap.add_argument("--concurrent", type=int, default=8,
                     help="config 3 also with this many 128-row batches in flight (one engine, HIP stream and host "
                          "thread each, like the reference's concurrent SUT instances); 0: skip")
+    ap.add_argument("--tiles", default="auto",
+                    help="config 3 encoder settings to time, comma-separated (rnnt_engine_set_tile: auto, ticks = "
+                         "one launch per tick, flow = the persistent dataflow launch); tokens must agree")
+    ap.add_argument("--skip-config2", action="store_true")
     args = ap.parse_args()
     pm, ckpt = weights.build_model()
     out = {}
     # ---- config 2: fp32 encoder, N=32, T=500
+    if not args.skip_config2:
+        config2(pm, ckpt, args, out)
+    config3(pm, args, out)
+    if args.concurrent > 0:
+        out["config3_int8_full_n128_concurrent"] = concurrent_config3(pm, args.concurrent, args.reps)
+    print(json.dumps(out))
+
+
+def config2(pm, ckpt, args, out):
     sd = weights.migrate_state_dict(ckpt)
     n, T = 32, 500
     n_pad = pad_batch(n)
@@ -71,7 +84,10 @@ def main():
                                            "ms_median": round(med * 1e3, 2), "achieved_tflops": round(tf, 2),
                                            "frac_fp32_mfma_peak": round(tf / FP32_MFMA_PEAK_TF, 4)}
     e.close()
-    # ---- config 3: int8 enc + bf16 pred/joint greedy, N=128, U{47..500}
+
+
+def config3(pm, args, out):
+    """int8 enc + bf16 pred/joint greedy, N=128, U{47..500}, under each --tiles setting."""
     n = 128
     n_pad = pad_batch(n)
     lens = np.sort(synthetic.uniform_lengths(n, seed=3))[::-1].astype(np.int32).copy()
@@ -83,23 +99,31 @@ def main():
     ld = torch.from_numpy(lp).cuda()
     res = torch.empty((n, e.max_res), dtype=torch.int32, device="cuda")
     rl = torch.empty(n, dtype=torch.int32, device="cuda")
-    best, med = timed(lambda: e.infer(x, ld, lens, res, rl, n=n), args.reps)
-    e.set_profiling(True)
-    e.stats(reset=True)
-    e.infer(x, ld, lens, res, rl, n=n)
-    torch.cuda.synchronize()
-    st = e.stats(reset=True)
-    ops = float(sum(enc_ops(int(t)) for t in lens))
-    out["config3_int8_full_n128"] = {"utt_per_s": round(n / best, 1), "ms_per_batch": round(best * 1e3, 2),
-                                     "ms_median": round(med * 1e3, 2), "encode_ms": round(st["encode_ms"], 3),
-                                     "joint_trans_ms": round(st["joint_trans_ms"], 3),
-                                     "greedy_ms": round(st["greedy_ms"], 3),
-                                     "encoder_int8_frac": round(ops / (st["encode_ms"] * 1e-3) / 5e15, 4),
-                                     "emitted": int(rl.cpu().numpy().sum())}
+    ref = None
+    for tile in args.tiles.split(","):
+        e.set_tile(tile)
+        best, med = timed(lambda: e.infer(x, ld, lens, res, rl, n=n), args.reps)
+        e.set_profiling(True)
+        e.stats(reset=True)
+        encs = []
+        for _ in range(max(3, args.reps)):  # encode time: the best of a few profiled passes
+            e.infer(x, ld, lens, res, rl, n=n)
+            torch.cuda.synchronize()
+            encs.append(e.stats(reset=True))
+        e.set_profiling(False)
+        st = min(encs, key=lambda d: d["encode_ms"])
+        ops = float(sum(enc_ops(int(t)) for t in lens))
+        toks = (res.cpu().numpy().copy(), rl.cpu().numpy().copy())
+        if ref is None:
+            ref = toks
+        same = bool(np.array_equal(ref[0], toks[0]) and np.array_equal(ref[1], toks[1]))
+        key = "config3_int8_full_n128" + ("" if tile == "auto" else "_" + tile)
+        out[key] = {"utt_per_s": round(n / best, 1), "ms_per_batch": round(best * 1e3, 2),
+                    "ms_median": round(med * 1e3, 2), "encode_ms": round(st["encode_ms"], 3),
+                    "joint_trans_ms": round(st["joint_trans_ms"], 3), "greedy_ms": round(st["greedy_ms"], 3),
+                    "encoder_int8_frac": round(ops / (st["encode_ms"] * 1e-3) / 5e15, 4),
+                    "emitted": int(toks[1].sum()), "tokens_equal_first_setting": same}
     e.close()
-    if args.concurrent > 0:
-        out["config3_int8_full_n128_concurrent"] = concurrent_config3(pm, args.concurrent, args.reps)
-    print(json.dumps(out))
 
 
 def concurrent_config3(pm, k, reps):

@@ -10,7 +10,7 @@ HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contr
 build() {
   local name=$1; shift
   local objs=""
-  for src in engine encoder encoder_f32 decoder decoder_f32 decoder_ops featurizer; do
+  for src in engine encoder encoder_f32 decoder decoder_f32 decoder_ops featurizer processor_ops; do
     local extra=""
     [ $src = encoder ] && extra="-fno-slp-vectorize"
     $HIPCC $extra "$@" -c $src.hip -o $OUTD/${src}_$name.o &
