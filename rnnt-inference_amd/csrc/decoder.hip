@@ -799,11 +799,17 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     if (hipMemsetAsync(a.res, 0xff, (size_t)a.N * a.max_res * sizeof(int32_t), st) != hipSuccess) return -1;
     hipLaunchKernelGGL(dec_init_kernel, dim3((a.Npad + 255) / 256), dim3(256), 0, st, a);
   }
-  constexpr int CHUNK = 32;
+  // Steps are enqueued in chunks and the host reads the live count one chunk behind, so a decode
+  // ends with the rest of the chunk holding its last step plus one more chunk of (cheap, but still
+  // ~20 us each: four dependent launches) empty steps.  Once few rows are left -- the long-tail
+  // rows whose last emission ends the loop -- chunks shrink to 8 steps: the overshoot falls from
+  // ~48 to ~12 steps while the host (~3.5 us per launch) still stays ahead of the GPU.
+  constexpr int CHUNK = 32, TAIL_CHUNK = 8, TAIL_ROWS = 64;
   int step = 0, chunk = 0;
   int live_bound = a.N;  // unfinished rows at the end of the last chunk read back (an upper bound)
   bool done = false;
   while (!done && step < a.max_iter) {
+    const int csz = live_bound > TAIL_ROWS ? CHUNK : TAIL_CHUNK;
     // row-tile workgroups per launch: one resident round, and no more than the live rows need
     const int lt = (live_bound + DEC_RT - 1) / DEC_RT < rt ? (live_bound + DEC_RT - 1) / DEC_RT : rt;
     const int lt1 = lt > 0 ? lt : 1;
@@ -811,7 +817,7 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_g = lt1 < G_ROW_GROUPS ? lt1 : G_ROW_GROUPS;
     const int ljt = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
     const int rg_joint = ljt < JOINT_GROUPS ? ljt : JOINT_GROUPS;
-    for (int i = 0; i < CHUNK && step < a.max_iter; ++i, ++step) {
+    for (int i = 0; i < csz && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
       hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
                          dim3(PRED_THREADS), 0, st, a, p);
