@@ -418,8 +418,10 @@ class WavFeed:
     sizes it to the lane's engine slots + ahead); max_frames: a store slot's rows (default the
     QSL's longest sample)."""
 
-    def __init__(self, qsl, store_slots=None, pro_batch=64, ahead=None, max_frames=None, alloc=True):
+    def __init__(self, qsl, store_slots=None, pro_batch=512, ahead=None, max_frames=None, alloc=True, cu_mask=None):
         self.qsl, self.pro_batch, self.ahead = qsl, int(pro_batch), ahead
+        self.cu_mask = cu_mask  # featurize on this CU set only (engine.cu_mask_words); None: any CU
+        self._pstreams = []
         self.store_slots, self.alloc = store_slots, alloc
         self.max_frames = int(max_frames or max(int(np.max(qsl.lengths)), 1))
         self.store = None
@@ -439,8 +441,11 @@ class WavFeed:
             self.store = FeatureStore(n, self.max_frames, device=self.qsl.device, alloc=self.alloc)
 
     def make_stream(self):
-        import torch
-        return torch.cuda.Stream(device=torch.device("cuda", self.device))
+        """The producer's stream (one per feed, kept across Server instances)."""
+        if not self._pstreams:
+            from .engine import PartitionedStream
+            self._pstreams.append(PartitionedStream(self.device, self.cu_mask))
+        return self._pstreams[0].stream
 
     def featurize(self, indices, slots, stream):
         """Featurize QSL samples ``indices`` into store ``slots`` (one launch), wait for it; ->
@@ -491,7 +496,7 @@ class ServerSUT:
     the engines of a lane take only their lane's samples.  Latency then includes featurization."""
 
     def __init__(self, engines, qsl=None, slots=2048, split_len=128, qos_len=None, on_complete=None, pipelined=False,
-                 feeds=None, lanes=None):
+                 feeds=None, lanes=None, engine_cu_mask=None):
         import threading
         from .engine import pad_batch
         if split_len <= 0 or split_len % 2:
@@ -519,6 +524,8 @@ class ServerSUT:
             self.lanes = [None] * len(self.engines)
         self.on_complete = on_complete
         self.pipelined = bool(pipelined)
+        self.engine_cu_mask = engine_cu_mask  # engines' streams on this CU set (engine.cu_mask_words)
+        self._pstreams = []
         self.responses, self.latency = {}, {}
         self._pending, self._qos = [], []  # (issue_time, QuerySample)
         self._ready = [collections.deque() for _ in self.feeds]  # per feed: (t0, sample, row, length, slot)
@@ -550,6 +557,15 @@ class ServerSUT:
         if set(lanes) != set(range(len(self.feeds))):
             raise ValueError("every feed needs at least one engine")
         return lanes
+
+    def _new_stream(self, device):
+        import torch
+        if self.engine_cu_mask is None:
+            return torch.cuda.Stream(device=torch.device("cuda", device))
+        from .engine import PartitionedStream
+        ps = PartitionedStream(device, self.engine_cu_mask)
+        self._pstreams.append(ps)
+        return ps.stream
 
     def _store_for(self, j):
         """(feature store tensor, lane) of engine j."""
@@ -599,6 +615,9 @@ class ServerSUT:
             self._cv.notify_all()
         for t in self._threads:
             t.join()
+        for ps in self._pstreams:
+            ps.close()
+        self._pstreams = []
 
     # producers (WAV feeds) ------------------------------------------------------------------
     def _source(self):
@@ -699,7 +718,7 @@ class ServerSUT:
         S, L = self.slots, self.split_len
         dev = torch.device("cuda", eng.device)
         with torch.cuda.device(eng.device):
-            st = torch.cuda.Stream(device=dev)
+            st = self._new_stream(eng.device)
             res = torch.empty((S, eng.max_res), dtype=torch.int32, device=dev)
             rl = torch.zeros(S, dtype=torch.int32, device=dev)
             # per-round host -> device inputs: reset flags, chunk lengths, row offsets (pinned)
@@ -807,7 +826,7 @@ class ServerSUT:
         dev = torch.device("cuda", eng.device)
         NR = 4  # reset-flag ring: round k's flags live until its decode completed (k+3 reuses them)
         with torch.cuda.device(eng.device):
-            est, dst = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+            est, dst = self._new_stream(eng.device), self._new_stream(eng.device)
             res = torch.empty((S, eng.max_res), dtype=torch.int32, device=dev)
             rl = torch.zeros(S, dtype=torch.int32, device=dev)
             h_reset = torch.zeros(S, dtype=torch.int32).pin_memory()

@@ -26,19 +26,20 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from rnnt_amd import synthetic, weights  # noqa: E402
-from rnnt_amd.engine import Engine  # noqa: E402
-from rnnt_amd.sut import DynamicBatchServerSUT, GpuQSL, QuerySample, ServerSUT  # noqa: E402
+from rnnt_amd.engine import Engine, cu_mask_words  # noqa: E402
+from rnnt_amd.sut import DynamicBatchServerSUT, GpuQSL, GpuWavQSL, QuerySample, ServerSUT, WavFeed  # noqa: E402
 
 TARGET_LATENCY_S = 1.0   # mlperf.conf rnnt.Server.target_latency (ms) / 1000
 PERCENTILE = 99.0        # mlperf.conf *.Server.target_latency_percentile
 
 
-def run_point(engines, qsl, qps, duration, max_batch, seed, args):
+def run_point(engines, qsl, qps, duration, max_batch, seed, args, feeds=None):
     if args.mode == "dynamic":
         sut = DynamicBatchServerSUT(engines, qsl, max_batch=max_batch)
     else:
-        sut = ServerSUT(engines, qsl, slots=max_batch, split_len=args.split_len, qos_len=args.qos_len,
-                        pipelined=args.pipelined)
+        sut = ServerSUT(engines, None if feeds else qsl, slots=max_batch, split_len=args.split_len, qos_len=args.qos_len,
+                        pipelined=args.pipelined, feeds=feeds,
+                        engine_cu_mask=cu_mask_words(args.fz_cus) if feeds and args.fz_cus else None)
     sut.start()
     rng = np.random.default_rng(seed)
     n = max(1, int(qps * duration))
@@ -90,19 +91,42 @@ def main():
     ap.add_argument("--qsl", type=int, default=2513)
     ap.add_argument("--search", action="store_true", help="largest QPS with p99 <= 1000 ms")
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--wav", action="store_true",
+                    help="continuous, audio input (the reference's processor=true Server): --feeds WAV feeds, each "
+                         "with its own audio copy and feature store, featurize arriving samples (ServerSUT feeds)")
+    ap.add_argument("--feeds", type=int, default=2, help="--wav: producer lanes on the GPU (engines dealt round-robin)")
+    ap.add_argument("--pro-batch", type=int, default=512,
+                    help="--wav: at most this many queued samples featurized per launch (64: the producers fall "
+                         "behind under load, 70k QPS target -> 39.5k completed; 512: 57k; profiles/r03/server_wav_*)")
+    ap.add_argument("--fz-cus", type=int, default=0,
+                    help="--wav: reserve this many CUs per XCD for the featurizer and keep the engines off them "
+                         "(CU-masked streams); 0: shared CUs")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     pm, _ = weights.build_model()
     engines = [Engine(pm, device=0, max_batch=args.max_batch, max_frames=500) for _ in range(args.inflight)]
-    qsl = GpuQSL(synthetic.devclean_lengths(args.qsl, seed=args.seed), seed=args.seed)
-    run_point(engines, qsl, 2000.0, 1.0, args.max_batch, 1, args)  # warm-up
+    feeds = None
+    if args.wav:
+        if args.mode != "continuous":
+            raise SystemExit("--wav runs the continuous ServerSUT")
+        frames = synthetic.devclean_lengths(args.qsl, seed=args.seed)
+        wavs = synthetic.make_wavs(synthetic.wav_lengths_for_frames(frames, seed=args.seed), seed=args.seed,
+                                   device="cuda")
+        fz_mask = cu_mask_words(args.fz_cus, reserved=True) if args.fz_cus else None
+        feeds = [WavFeed(GpuWavQSL(wavs), pro_batch=args.pro_batch, cu_mask=fz_mask) for _ in range(args.feeds)]
+        del wavs
+        qsl = feeds[0].qsl
+    else:
+        qsl = GpuQSL(synthetic.devclean_lengths(args.qsl, seed=args.seed), seed=args.seed)
+    rp = lambda q, d, s: run_point(engines, qsl, q, d, args.max_batch, s, args, feeds)  # noqa: E731
+    rp(2000.0, 1.0, 1)  # warm-up
     points = []
     if not args.search:
-        points.append(run_point(engines, qsl, args.qps, args.duration, args.max_batch, args.seed, args))
+        points.append(rp(args.qps, args.duration, args.seed))
     else:
         lo, hi, q = 0.0, None, 10000.0
         while hi is None and q < 1e6:
-            p = run_point(engines, qsl, q, args.duration, args.max_batch, args.seed, args)
+            p = rp(q, args.duration, args.seed)
             points.append(p)
             print(json.dumps(p), flush=True)
             if p["valid"]:
@@ -111,7 +135,7 @@ def main():
                 hi = q
         for _ in range(4 if hi else 0):
             q = 0.5 * (lo + hi)
-            p = run_point(engines, qsl, q, args.duration, args.max_batch, args.seed, args)
+            p = rp(q, args.duration, args.seed)
             points.append(p)
             print(json.dumps(p), flush=True)
             lo, hi = (q, hi) if p["valid"] else (lo, q)
@@ -119,7 +143,8 @@ def main():
     print(json.dumps({"scenario": "Server", "target_latency_ms": TARGET_LATENCY_S * 1e3, "percentile": PERCENTILE,
                       "duration_s": args.duration, "mode": args.mode, "slots_or_max_batch": args.max_batch,
                       "split_len": args.split_len if args.mode == "continuous" else None, "inflight": args.inflight,
-                      "pipelined": args.pipelined,
+                      "pipelined": args.pipelined, "input": (f"wav ({args.feeds} feeds, pro_batch {args.pro_batch}, featurizer CUs/XCD {args.fz_cus or 'shared'})"
+                                                             if args.wav else "features (GpuQSL store)"),
                       "best_valid_qps_per_gpu": best["target_qps"] if best else None, "points": points}))
     for e in engines:
         e.close()
