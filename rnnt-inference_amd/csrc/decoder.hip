@@ -78,6 +78,12 @@ __device__ unsigned int g_st_n;
 #define ST_FLUSH(kid, a0, a1, a2, a3)
 #endif
 
+// Workgroup barrier over LDS only: waits for this wave's LDS operations, not for its global loads
+// and stores (a __syncthreads fence waits for every outstanding memory operation: in the step
+// kernels that serialised the weight-slice loads behind the list / staging round trips and
+// drained each tile's global stores).  Uniform control flow only.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // XCD-aware decomposition of a 1-D grid of 8 * X * Y8 workgroups into (column group x, row group
 // y < 8 * Y8): workgroup id goes to XCD id & 7 (round-robin dispatch), and all X column groups
 // of a row group run on one XCD, so a row tile's inputs are fetched into one L2 (measured before:
@@ -378,25 +384,15 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
   const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
+  // the weight slice (10 / 20 x 16 B per lane) is issued after the first tile's input loads:
+  // vmcnt retires in order, so loads issued first would hold up the staging that needs the inputs
   uint4 wh[NT][P / 32], wx[NT][LAYER ? P / 32 : 1];
   float4 bh[NT], bx[NT];
-#pragma unroll
-  for (int tt = 0; tt < NT; ++tt) {
-    const uint16_t* wr = a.w.wp[LAYER] + (size_t)((t0 + tt) * 16 + c) * 640 + 8 * q;
-#pragma unroll
-    for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
-    if (LAYER) {
-#pragma unroll
-      for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
-      bx[tt] = *(const float4*)(a.w.bih_p[LAYER] + (t0 + tt) * 16 + 4 * q);
-    }
-    bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
-  }
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT)  // past the prefetched tiles (the slot's tile is done)
       ents[tid] = rt * DEC_RT + tid < cnt ? list[rt * DEC_RT + tid] : -1;
-    __syncthreads();
+    lds_barrier();
     ST_MARK(st1);
     // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and, layer 0, its
     // label-table input halves, fetched beside the input staging
@@ -435,6 +431,21 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
         xv[u] = *(const uint4*)src;
       }
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
+    if (it == 0) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        const uint16_t* wr = a.w.wp[LAYER] + (size_t)((t0 + tt) * 16 + c) * 640 + 8 * q;
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
+        if (LAYER) {
+#pragma unroll
+          for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
+          bx[tt] = *(const float4*)(a.w.bih_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+        }
+        bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int i = tid + PRED_THREADS * u;
@@ -443,7 +454,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
         *(uint4*)&X[m][k] = emv[u] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
       }
     }
-    __syncthreads();
+    lds_barrier();
     ST_MARK(st2);
     // the chains of every sub-tile (h, and x on layer 1) advance together, one k block at a
     // time, so each block's fragment reads overlap the previous block's MFMAs (sub-tiles past the
@@ -485,7 +496,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
         }
       }
     }
-    __syncthreads();  // X (and this entry slot, NK tiles on) are restaged by the next tile
+    lds_barrier();  // X (and this entry slot, NK tiles on) are restaged by the next tile
     ST_FLUSH(LAYER, st0, st1, st2, 0ull);
   }
 }
@@ -516,20 +527,12 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
   constexpr int NJ = 1;  // column tiles per wave
-  uint4 wv[NJ][P / 32];
+  uint4 wv[NJ][P / 32];  // issued after the first tile's input loads (see dec_pred_kernel)
   float4 b0[NJ];
-#pragma unroll
-  for (int jj = 0; jj < NJ; ++jj) {
-    const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
-    const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
-#pragma unroll
-    for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
-    b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
-  }
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt ? list[rt * DEC_RT + tid] : -1;
-    __syncthreads();
+    lds_barrier();
     ST_MARK(st1);
     constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
     uint4 xv[NIT];
@@ -547,6 +550,17 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
         xv[u] = *(const uint4*)(h_bf(a.hc, em >= 0 ? entry_row(em) : 0, em >= 0 ? entry_slot(em) ^ 1 : 0, 1) + k);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
+    if (it == 0) {
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
+        const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
+        b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int i = tid + G_THREADS * u;
@@ -555,7 +569,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
         *(uint4*)&X[m][k] = emv[u] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
       }
     }
-    __syncthreads();
+    lds_barrier();
     ST_MARK(st2);
     // every sub-tile's chain advances one k block at a time (fragment reads overlap MFMAs)
     static_assert(NJ == 1, "one column tile per wave");
@@ -575,7 +589,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       if (ec >= 0)
         *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
     }
-    __syncthreads();
+    lds_barrier();
     ST_FLUSH(2, st0, st1, st2, 0ull);
   }
 }
@@ -608,20 +622,9 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   // logits = ((s0 + s1) + s2) + s3, s_b = y1[128b : 128b+128] . W2^T (s0 from b2): wave w runs
   // label half w&1 over k blocks 2(w>>1) and 2(w>>1)+1 as two independent 4-instruction chains
   const int lh = wave & 1, kb0 = 2 * (wave >> 1);
-  uint4 wv[8];
-  {
-    const uint16_t* wr = a.w.w2 + (size_t)(lh * 16 + c) * J + 8 * q;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      wv[b] = *(const uint4*)(wr + 128 * kb0 + 32 * b);
-      wv[4 + b] = *(const uint4*)(wr + 128 * (kb0 + 1) + 32 * b);
-    }
-  }
+  uint4 wv[8];  // W2 fragments: issued after the first tile's F / G loads (see dec_pred_kernel)
   v4f bias = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-  if (kb0 == 0) {
-    const float4 b0 = *(const float4*)(a.w.b2 + lh * 16 + 4 * q);
-    bias = v4f{b0.x, b0.y, b0.z, b0.w};
-  }
+  bool w_loaded = false;
   for (int rt = blockIdx.x; rt < ntiles; rt += gridDim.x) {
     if (tid < JRT) {
       const int i = rt * JRT + tid;
@@ -636,7 +639,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       flen_[tid] = (e.y >> 16) & 0xffff;
       idx_[tid] = e.z;
     }
-    __syncthreads();
+    lds_barrier();
     ST_MARK(st1);
 #ifdef RNNT_DEV_STAMPS
     unsigned long long st2 = 0ull;
@@ -666,6 +669,20 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           gl4[u][1] = *(const float4*)(gr + 4);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
+      if (!w_loaded) {
+        w_loaded = true;
+        const uint16_t* wr = a.w.w2 + (size_t)(lh * 16 + c) * J + 8 * q;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          wv[b] = *(const uint4*)(wr + 128 * kb0 + 32 * b);
+          wv[4 + b] = *(const uint4*)(wr + 128 * (kb0 + 1) + 32 * b);
+        }
+        if (kb0 == 0) {
+          const float4 b0 = *(const float4*)(a.w.b2 + lh * 16 + 4 * q);
+          bias = v4f{b0.x, b0.y, b0.z, b0.w};
+        }
+      }
 #pragma unroll
       for (int u = 0; u < NIT; ++u) {
         const int i = tid + 256 * u, m = i / (J / 8), k = (i % (J / 8)) * 8;
@@ -683,7 +700,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
         *(uint4*)&X[m][k] = wk[u] ? pack8(float4{y[0], y[1], y[2], y[3]}, float4{y[4], y[5], y[6], y[7]})
                                   : uint4{0u, 0u, 0u, 0u};
       }
-      __syncthreads();
+      lds_barrier();
       ST_SET(st2);
 #pragma unroll
       for (int st = 0; st < 1; ++st) {
@@ -701,7 +718,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           Lp[kb0 + 1][16 * st + c][lh * 16 + 4 * q + r] = s1[r];
         }
       }
-      __syncthreads();
+      lds_barrier();
       // logits = ((s0 + s1) + s2) + s3 and the argmax over the 29 real labels: wave w takes rows
       // 4w .. 4w+3, 16 lanes per row with labels 2l, 2l+1, merged by cross-lane moves (larger
       // value, ties to the smaller label: torch.argmax's first maximum); the row's first lane
@@ -760,7 +777,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
     // the tile's emitting rows -> next emit list, its unfinished rows -> next live list: ONE
     // 64-bit atomic on the adjacent (emit, live) counters of the next parity returns both bases
@@ -779,7 +796,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
         nlist[(int)(base >> 32) + __popcll(mr & below)] =
             live_entry(r, slot_[lane], add_[lane], tidx[lane], flen_[lane], idx_[lane]);
     }
-    __syncthreads();  // rows / walking / tidx / X are reused by the next row tile
+    lds_barrier();  // rows / walking / tidx / X are reused by the next row tile
     ST_FLUSH(3, st0, st1, st2, 0ull);
   }
 }
