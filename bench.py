@@ -106,10 +106,19 @@ def mock_main(args):
 
     def step():
         mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world)
-        my_ids = np.concatenate([b[0] for b in mine]) if mine else np.zeros(0, np.int64)
-        rl = (my_ids % 7).astype(np.int32)
-        toks = np.concatenate([np.full(int(n), int(i) % 29, np.int32) for i, n in zip(my_ids, rl)] + [np.zeros(0, np.int32)])
-        return dist.gather_responses(my_ids, rl, toks, world, group)
+        stream = dist.ResponseStream(world, group) if world > 1 else None
+        got = []
+        for b_ids, _ in mine:  # stand-in responses, shipped batch by batch like the SUT's completions
+            rl = (b_ids % 7).astype(np.int32)
+            toks = np.concatenate([np.full(int(n), int(i) % 29, np.int32) for i, n in zip(b_ids, rl)] +
+                                  [np.zeros(0, np.int32)])
+            if stream:
+                stream.push(b_ids, rl, toks)
+            else:
+                got.append((b_ids, rl, toks))
+        if stream:
+            return stream.finish()
+        return tuple(np.concatenate([g[k] for g in got]) for k in range(3))
 
     for _ in range(args.warmup):
         step()
@@ -269,11 +278,14 @@ def main():
     sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None
 
     def step():
-        """One Offline query: sort + batch + deal, this rank's share through the SUT, gather."""
+        """One Offline query: sort + batch + deal, this rank's share through the SUT, every batch's
+        responses streamed to rank 0 as it completes (dist.ResponseStream)."""
         mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world, sizes)
+        stream = dist.ResponseStream(world, ggroup) if world > 1 else None
+        sut.on_batch = stream.push if stream else None
         sut.issue_batches(mine)
         local = sut.take_completed()
-        got = dist.gather_responses(*local, world, ggroup)
+        got = stream.finish() if stream else local
         return mine, got, int(local[1].sum())
 
     for _ in range(args.warmup):

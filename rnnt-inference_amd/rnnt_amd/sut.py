@@ -38,8 +38,13 @@ class _SortedQSL:
         return self.count
 
     def sort_indices(self, indices):
-        """Positions of `indices` in longest-first order, stable (the bucket sort's order)."""
-        return np.argsort(-self.lengths[np.asarray(indices, np.int64)], kind="stable")
+        """Positions of `indices` in longest-first order, stable (the bucket sort's order).  The key
+        is the length's distance from the longest as uint16, which numpy's stable sort orders by
+        radix sort (O(n): 196k query samples at 8 GPUs in ~5 ms instead of ~20)."""
+        lens = self.lengths[np.asarray(indices, np.int64)]
+        if len(lens) and int(self.lengths.max()) - int(self.lengths.min()) < 65536:
+            return np.argsort((np.int64(self.lengths.max()) - lens).astype(np.uint16), kind="stable")
+        return np.argsort(-lens, kind="stable")
 
     def sort(self, samples, reverse=True):
         """Bucket sort by feature length, longest first (rnnt_qsl.cpp:104-133)."""
@@ -118,6 +123,7 @@ class OfflineSUT:
         self.engine = self.engines[0]
         self.qsl, self.batch_size, self.batch_sizes = qsl, batch_size, batch_sizes
         self.on_complete = on_complete
+        self.on_batch = None  # called with (ids, lens, tokens) of every completed batch
         self._done_lock = threading.Lock()
         self.completed = []  # per batch: (sample ids int64 [n], lengths int32 [n], tokens int32 [sum])
         self._streams = {}
@@ -229,6 +235,8 @@ class OfflineSUT:
     def query_samples_complete(self, ids, idx, toks, lens):
         """Response = int32 tokens [res_len] per sample (torch_sut.cpp:221-236)."""
         flat = toks[np.arange(toks.shape[1])[None, :] < lens[:, None]]
+        if self.on_batch is not None:  # e.g. dist.ResponseStream.push: ship the batch to rank 0 now
+            self.on_batch(ids, lens.astype(np.int32), flat.astype(np.int32))
         with self._done_lock:
             self.completed.append((ids, lens.astype(np.int32), flat.astype(np.int32)))
             if self.on_complete:

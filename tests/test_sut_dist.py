@@ -127,3 +127,73 @@ def test_two_rank_query_shard_and_gather_gloo():
     # snake dealing of sorted batches balances the shards' work
     fa, fb = lengths[np.array(a) % 1000].sum(), lengths[np.array(b) % 1000].sum()
     assert abs(fa - fb) / (fa + fb) < 0.1
+
+
+def _stream_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import threading
+    import torch.distributed as dist
+    r, _, w, group = rdist.setup("gloo")
+    lengths = np.random.default_rng(1).integers(47, 501, 700).astype(np.int32)
+    qsl = RNNTQSL([None] * len(lengths), lengths)
+    ids, idx = rdist.query_arrays(len(lengths), 2000)
+    mine = rdist.shard_query(qsl, ids, idx, 96, rank, world)
+    stream = rdist.ResponseStream(world, group)
+    # batches complete on two "engine" threads in any order, like the OfflineSUT's workers
+    halves = [mine[0::2], mine[1::2]]
+
+    def engine(part):
+        for b_ids, _ in part:
+            rows = [_tokens(int(i)) for i in b_ids]
+            stream.push(b_ids, np.array([len(t) for t in rows], np.int32),
+                        np.concatenate(rows + [np.zeros(0, np.int32)]).astype(np.int32))
+
+    ths = [threading.Thread(target=engine, args=(h,)) for h in halves]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    got = stream.finish()
+    out = None
+    if got is not None:
+        out = (got[0].tolist(), got[1].tolist(), got[2].tolist())
+    q.put((rank, out))
+    rdist.barrier(group)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_response_stream_gloo(world):
+    """dist.ResponseStream (bench.py): every rank's batches, completed on several threads, reach
+    rank 0 intact in the compact wire form (ids int32, lens int16, tokens uint8)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stream_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(outs[r] is None for r in range(1, world))
+    gids, glens, gtoks = outs[0]
+    assert sorted(gids) == list(range(2000))
+    off = 0
+    for i, L in zip(gids, glens):
+        np.testing.assert_array_equal(gtoks[off: off + L], _tokens(i))
+        off += L
+    assert off == len(gtoks)
+
+
+def test_pack_responses_roundtrip_and_range():
+    ids = np.array([0, 5, 2 ** 31 - 1], np.int64)
+    lens = np.array([0, 3, 7500], np.int32)
+    toks = np.arange(7503, dtype=np.int32) % 29
+    back = rdist.unpack_responses(rdist.pack_responses(ids, lens, toks), 3, len(toks))
+    for a, b in zip(back, (ids, lens, toks)):
+        np.testing.assert_array_equal(a, b)
+    with pytest.raises(ValueError):
+        rdist.pack_responses(np.array([2 ** 31]), np.array([1]), np.array([0]))
+    with pytest.raises(ValueError):
+        rdist.pack_responses(np.array([1]), np.array([1]), np.array([256]))
