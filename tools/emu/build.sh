@@ -1,0 +1,30 @@
+#!/bin/bash
+# Development: build the host emulation of the decode kernels (tools/emu/dec_emu.cpp) with
+# AddressSanitizer into build_dev/emu/.  The sources are copied with the few GPU-only constructs
+# (s_barrier asm, dynamic LDS, address-space typedefs) rewritten for the host.
+set -e
+ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
+SRC=$ROOT/rnnt-inference_amd/csrc
+OUT=$ROOT/build_dev/emu
+mkdir -p $OUT
+python3 - "$SRC" "$OUT" <<'PY'
+import re, sys
+src, out = sys.argv[1], sys.argv[2]
+def fix(text):
+    text = text.replace('asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory")', 'emu_sync()')
+    text = text.replace('asm volatile("s_waitcnt vmcnt(0)\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory")', 'emu_sync()')
+    text = text.replace('asm volatile("" : "+v"(c));', '')
+    text = re.sub(r'extern __shared__ (__attribute__\(\(aligned\(16\)\)\) )?(\w+) (\w+)\[\];',
+                  r'static \1\2 \3[1 << 17];', text)
+    text = re.sub(r'__attribute__\(\(address_space\(\d\)\)\) ', '', text)
+    if 'asm volatile' in text:
+        raise SystemExit('unhandled asm in ' + text[:40])
+    return text
+for name, dst in (("decoder.hip", "decoder_emu.hip.cpp"), ("rnnt_device.hpp", "rnnt_device.hpp"), ("decoder.hpp", "decoder.hpp")):
+    open(f"{out}/{dst}", "w").write(fix(open(f"{src}/{name}").read()))
+PY
+CXX=/opt/rocm/lib/llvm/bin/clang++
+$CXX -O1 -g -std=c++20 -ffp-contract=off -fsanitize=address -fno-omit-frame-pointer -pthread \
+  -DRNNT_DEC_CHECK -I$ROOT/tools/emu -I$OUT $ROOT/tools/emu/dec_emu.cpp $ROOT/oracle/rnnt_oracle.c -x none \
+  -o $OUT/dec_emu -lm
+echo "built $OUT/dec_emu"
