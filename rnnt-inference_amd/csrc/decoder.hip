@@ -44,7 +44,17 @@ __device__ __forceinline__ uint4 pack8(const float4 lo, const float4 hi) {
 }
 // emit-list entry: row | committed slot << 24 | label-table index << 25 (28 = SOS)
 __device__ __forceinline__ int emit_entry(int row, int slot, int label) { return row | (slot << 24) | (label << 25); }
-__device__ __forceinline__ int entry_row(int e) { return e & 0xffffff; }
+// The row goes through an opaque v_and: ROCm 7.2's AMDGPU backend miscompiles a 64-bit multiply
+// of (x & 0xffffff) by a constant that is not a power of two -- it matches a 24-bit multiply
+// (which ignores the high byte, so the mask is dropped as redundant) and then widens it to
+// v_mad_u64_u32, which multiplies all 32 bits: `base + (size_t)entry_row(e) * 1280` addressed
+// with the slot and label bits still in place (tools/probe/probe_mul24.hip; guarded by
+// tests/test_isa_lint.py).
+__device__ __forceinline__ int entry_row(int e) {
+  int r;
+  asm("v_and_b32 %0, 0xffffff, %1" : "=v"(r) : "v"(e));
+  return r;
+}
 __device__ __forceinline__ int entry_slot(int e) { return (e >> 24) & 1; }
 __device__ __forceinline__ int entry_label(int e) { return (e >> 25) & 31; }
 // list counters: DecState::count = {emit p0, live p0, emit p1, live p1} -- one parity's two

@@ -4,8 +4,8 @@
 # (s_barrier asm, dynamic LDS, address-space typedefs) rewritten for the host.
 set -e
 ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
-SRC=$ROOT/rnnt-inference_amd/csrc
-OUT=$ROOT/build_dev/emu
+SRC=${EMU_SRC:-$ROOT/rnnt-inference_amd/csrc}
+OUT=${EMU_OUT:-$ROOT/build_dev/emu}
 mkdir -p $OUT
 python3 - "$SRC" "$OUT" <<'PY'
 import re, sys
@@ -14,10 +14,11 @@ def fix(text):
     text = text.replace('asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory")', 'emu_sync()')
     text = text.replace('asm volatile("s_waitcnt vmcnt(0)\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory")', 'emu_sync()')
     text = text.replace('asm volatile("" : "+v"(c));', '')
+    text = text.replace('asm("v_and_b32 %0, 0xffffff, %1" : "=v"(r) : "v"(e));', 'r = e & 0xffffff;')
     text = re.sub(r'extern __shared__ (__attribute__\(\(aligned\(16\)\)\) )?(\w+) (\w+)\[\];',
                   r'static \1\2 \3[1 << 17];', text)
     text = re.sub(r'__attribute__\(\(address_space\(\d\)\)\) ', '', text)
-    if 'asm volatile' in text:
+    if 'asm volatile' in text or 'asm(' in text:
         raise SystemExit('unhandled asm in ' + text[:40])
     return text
 for name, dst in (("decoder.hip", "decoder_emu.hip.cpp"), ("rnnt_device.hpp", "rnnt_device.hpp"), ("decoder.hpp", "decoder.hpp")):

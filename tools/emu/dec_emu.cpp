@@ -1,7 +1,7 @@
 // dec_emu.cpp -- runs the engine's greedy decode (decoder.hip: launch_dec_xtab +
 // launch_greedy_decode, every step kernel) on the host emulation of the wave model
 // (emu_hip.hpp) and compares tokens with the oracle (oracle_greedy_decode, bf16 mode).
-// Built with AddressSanitizer by tools/emu/build.sh.  Usage: dec_emu [N rows] [Tp] [seed] [server]
+// Built with AddressSanitizer by tools/emu/build.sh.  Usage: dec_emu [N rows] [Tp] [seed] [server] [blank bias]
 // (server: two decode_stream-style calls over halves of the frames, slots kept between them).
 #include "emu_hip.hpp"
 #include "decoder_emu.hip.cpp"
@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
   std::vector<float> W1t = randv((size_t)J * H, 0.04f), W1p = randv((size_t)J * P, 0.08f);
   std::vector<float> bt = randv(J, 0.1f), bp = randv(J, 0.1f);
   std::vector<float> W2 = randv((size_t)NLAB * J, 0.15f), b2 = randv(NLAB, 0.3f);
-  b2[BLANK] += 1.5f;  // mostly blanks, some emissions (a few runs of several per frame)
+  b2[BLANK] += argc > 5 ? (float)atof(argv[5]) : 1.5f;  // blank bias: mostly blanks, some emissions
   // device layouts (engine.hip's packing: gate-interleaved rows 4u+g, [W_ih | W_hh] natural k)
   uint16_t* d_embed = dalloc<uint16_t>(28 * P);
   for (int i = 0; i < 28 * P; ++i) d_embed[i] = f2bf_bits(embed[i]);
