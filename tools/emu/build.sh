@@ -25,7 +25,13 @@ for name, dst in (("decoder.hip", "decoder_emu.hip.cpp"), ("rnnt_device.hpp", "r
     open(f"{out}/{dst}", "w").write(fix(open(f"{src}/{name}").read()))
 PY
 CXX=/opt/rocm/lib/llvm/bin/clang++
-$CXX -O1 -g -std=c++20 -ffp-contract=off -fsanitize=address -fno-omit-frame-pointer -pthread \
-  -DRNNT_DEC_CHECK -I$ROOT/tools/emu -I$OUT $ROOT/tools/emu/dec_emu.cpp $ROOT/oracle/rnnt_oracle.c -x none \
+# EMU_ASAN=0: an optimised build without AddressSanitizer (the CPU test's build)
+if [ "${EMU_ASAN:-1}" = 1 ]; then SAN="-O1 -fsanitize=address -fno-omit-frame-pointer"; else SAN="-O2"; fi
+# features of the decoder being emulated (the harness adapts to either step structure)
+FEAT=""
+grep -q "g_dec_err" $SRC/decoder.hip && FEAT="$FEAT -DEMU_HAS_DEC_CHECK"
+grep -q "float\* ah0;" $SRC/decoder.hpp && FEAT="$FEAT -DEMU_HAS_AH"
+$CXX $SAN -g -std=c++20 -ffp-contract=off -pthread $FEAT \
+  -DRNNT_DEC_CHECK -I$ROOT/tools/emu -I$OUT $ROOT/tools/emu/dec_emu.cpp $ROOT/oracle/rnnt_oracle.c \
   -o $OUT/dec_emu -lm
 echo "built $OUT/dec_emu"
