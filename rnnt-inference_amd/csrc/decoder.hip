@@ -19,8 +19,11 @@
 //   * prediction(pre_g, pre_hg, pre_cg) depends only on state that changes on an emit, so it
 //     (and the joint's prediction half G) is evaluated once per emit, not once per step;
 //   * layer 0's input half b_ih + emb[g].W_ih^T depends only on the label: a [29][1280] table
-//     computed once per engine with the same instruction sequence (launch_dec_xtab).
-// The step is latency-bound (four dependent launches), so each kernel keeps its chain of
+//     computed once per engine with the same instruction sequence (launch_dec_xtab);
+//   * the recurrent halves b_hh + h.W_hh^T of a prediction depend only on the committed state,
+//     i.e. on the previous candidate, so they are computed when that candidate is made (beside
+//     layer 1 and G); the joint then runs layer 0's cell itself at an emission.
+// The step is latency-bound (three dependent launches: layer 1, G, joint), so each kernel keeps its chain of
 // dependent memory round trips short: emit-list entries carry (row, slot, label), the list
 // entries of a workgroup's first tile are loaded beside the list length, the cell state is
 // fetched beside the input staging, and the joint walks a compact list of unfinished rows.
@@ -41,7 +44,17 @@ __device__ __forceinline__ uint4 pack8(const float4 lo, const float4 hi) {
 }
 // emit-list entry: row | committed slot << 24 | label-table index << 25 (28 = SOS)
 __device__ __forceinline__ int emit_entry(int row, int slot, int label) { return row | (slot << 24) | (label << 25); }
-__device__ __forceinline__ int entry_row(int e) { return e & 0xffffff; }
+// The row goes through an opaque v_and: ROCm 7.2's AMDGPU backend miscompiles a 64-bit multiply
+// of (x & 0xffffff) by a constant that is not a power of two -- it matches a 24-bit multiply
+// (which ignores the high byte, so the mask is dropped as redundant) and then widens it to
+// v_mad_u64_u32, which multiplies all 32 bits: `base + (size_t)entry_row(e) * 1280` addressed
+// with the slot and label bits still in place (tools/probe/probe_mul24.hip; guarded by
+// tests/test_isa_lint.py).
+__device__ __forceinline__ int entry_row(int e) {
+  int r;
+  asm("v_and_b32 %0, 0xffffff, %1" : "=v"(r) : "v"(e));
+  return r;
+}
 __device__ __forceinline__ int entry_slot(int e) { return (e >> 24) & 1; }
 __device__ __forceinline__ int entry_label(int e) { return (e >> 25) & 31; }
 // list counters: DecState::count = {emit p0, live p0, emit p1, live p1} -- one parity's two
@@ -76,6 +89,18 @@ __device__ unsigned int g_st_n;
 #define ST_MARK(v)
 #define ST_SET(v)
 #define ST_FLUSH(kid, a0, a1, a2, a3)
+#endif
+
+// development bounds checks (-DRNNT_DEC_CHECK, tools/build_variants.sh): a failed check sets its
+// bit in g_dec_err and the access is skipped; in the shipping build every check is `true`
+#ifdef RNNT_DEC_CHECK
+__device__ unsigned int g_dec_err;
+__device__ __forceinline__ bool dec_ok(bool c, int bit) {
+  if (!c) atomicOr(&g_dec_err, 1u << bit);
+  return c;
+}
+#else
+__device__ __forceinline__ constexpr bool dec_ok(bool, int) { return true; }
 #endif
 
 // Workgroup barrier over LDS only: waits for this wave's LDS operations, not for its global loads
@@ -340,11 +365,20 @@ __global__ void __launch_bounds__(256) dec_reset_res_kernel(int32_t* __restrict_
 
 // One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates =
 // (b_ih + x.W_ih^T) + (b_hh + h.W_hh^T); c fp32, h bf16.  A workgroup (4 waves) owns 4 gate
-// tiles, one per wave, whose W_hh (and, layer 1, W_ih) rows stay in registers for the launch
-// (10 x 16 B per chain per lane; layer 0's input half comes from the label table).  Every
-// launch reloads its weights, and one CU takes in only a few tens of GB/s, so the slice per
-// workgroup is kept small (20-40 KB: in-kernel stamps showed 160-320 KB slices costing 12-20 us
-// per launch).  Grid: x = 20 gate groups, y = row groups striding over the emit list's tiles.
+// tiles, one per wave, whose weight rows stay in registers for the launch (10 x 16 B per chain
+// per lane; layer 0's input half comes from the label table).  Every launch reloads its weights,
+// and one CU takes in only a few tens of GB/s, so the slice per workgroup is kept small (20-40
+// KB: in-kernel stamps showed 160-320 KB slices costing 12-20 us per launch).  Grid: x = 20 gate
+// groups, y = row groups striding over the emit list's tiles.
+//
+// The recurrent halves b_hh + h.W_hh^T depend only on the committed state, i.e. on the previous
+// candidate, so they are computed when that candidate is made, off the next emission's critical
+// path: every layer-1 launch also runs the W_hh0 chain over the new candidate's h0 (-> ah0) and
+// every G launch the W_hh1 chain over its h1 (-> ah1).  Layer 0 then runs only in a call's first
+// step (the joint runs the layer-0 cell of every later emission from the label table and ah0), and
+// layer 1 always takes its recurrent half from ah1 (a call's first step computes it from the
+// committed h1 first: dec_g_kernel<true>).  Each chain is the same instruction sequence wherever
+// it runs, so the results are bit-identical.
 constexpr int PRED_THREADS = 256;  // 4 waves, one gate tile each: 40 KB of weights per workgroup
 // rows per workgroup iteration of the prediction / G kernels: 32 (two MFMA row tiles per weight
 // fragment) with 24 / 48 row groups -- isolated greedy 69.5 -> 66.7 ms per query vs 16 rows and
@@ -361,8 +395,9 @@ constexpr int JOINT_GROUPS = 512;
 template <int LAYER, int NW>
 __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity) {
   constexpr int PRED_THREADS = NW * 64;
-  constexpr int NT = 1;                  // gate tiles per wave
-  constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
+  constexpr int NT = 1;                     // gate tiles per wave
+  constexpr bool H_CHAIN = LAYER == 0;  // this layer's recurrent chain runs here (layer 1: ah1)
+  constexpr int KX = P;                 // staged k: layer 0 h0 committed, layer 1 h0 of the candidate
   // bf16 pitch +32 B per row: every ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows c, 16-B
   // column q) lands on 16 distinct bank quads; the round-2 +16 B pitch put rows c and c+8 on the same
   // quads (2-way, 36-37 % of the LDS cycles of these kernels in the r02 PMC pass)
@@ -386,30 +421,34 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
   // the weight slice (10 / 20 x 16 B per lane) is issued after the first tile's input loads:
   // vmcnt retires in order, so loads issued first would hold up the staging that needs the inputs
-  uint4 wh[NT][P / 32], wx[NT][LAYER ? P / 32 : 1];
-  float4 bh[NT], bx[NT];
+  uint4 wh[NT][H_CHAIN ? P / 32 : 1], wx[NT][LAYER ? P / 32 : 1], w0[NT][LAYER ? P / 32 : 1];
+  float4 bh[NT], bx[NT], b0[NT];
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT)  // past the prefetched tiles (the slot's tile is done)
-      ents[tid] = rt * DEC_RT + tid < cnt ? list[rt * DEC_RT + tid] : -1;
+      ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 3) ? list[rt * DEC_RT + tid] : -1;
     lds_barrier();
     ST_MARK(st1);
-    // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and, layer 0, its
-    // label-table input halves, fetched beside the input staging
+    // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and its precomputed
+    // gate halves (layer 0: the label table's input half; layer 1: ah1), fetched
+    // beside the input staging
     float cp[DEC_SUB][NT];
     float4 xt[DEC_SUB][NT];
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
-      const int ec = ents[16 * st + c];
+      int ec = ents[16 * st + c];
+      if (ec >= 0 && !dec_ok(entry_row(ec) < a.Npad && entry_label(ec) <= 28, 0)) ec = -1;
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         cp[st][tt] = ec >= 0 ? hc_part(a.hc, entry_row(ec), entry_slot(ec), 2 + LAYER)[(t0 + tt) * 4 + q] : 0.0f;
         if (!LAYER)
           xt[st][tt] = *(const float4*)(a.w.xtab + (size_t)(ec >= 0 ? entry_label(ec) : 28) * PG4 + (t0 + tt) * 16 + 4 * q);
+        else
+          xt[st][tt] = *(const float4*)(a.ah1 + (size_t)(ec >= 0 ? entry_row(ec) : 0) * PG4 + (t0 + tt) * 16 + 4 * q);
       }
     }
-    // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1
-    // [h0 of the candidate slot | h1 committed]
+    // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1 h0 of the
+    // candidate slot
     // every load of the tile first (one memory round trip); entries past the list end read row
     // 0 (a safe cached address) and stage zeros
     constexpr int NX = DEC_RT * (KX / 8), NIT = (NX + PRED_THREADS - 1) / PRED_THREADS;
@@ -425,9 +464,8 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       const int i = tid + PRED_THREADS * u;
       if (NX % PRED_THREADS == 0 || i < NX) {
         const int k = (i % (KX / 8)) * 8, em = emv[u];
-        const int r = em >= 0 ? entry_row(em) : 0, smm = em >= 0 ? entry_slot(em) : 0;
-        const uint16_t* src = LAYER == 0 ? h_bf(a.hc, r, smm, 0) + k
-                                         : (k < P ? h_bf(a.hc, r, smm ^ 1, 0) + k : h_bf(a.hc, r, smm, 1) + k - P);
+        const int r = em >= 0 && dec_ok(entry_row(em) < a.Npad, 1) ? entry_row(em) : 0, smm = em >= 0 ? entry_slot(em) : 0;
+        const uint16_t* src = h_bf(a.hc, r, LAYER == 0 ? smm : smm ^ 1, 0) + k;
         xv[u] = *(const uint4*)src;
       }
     }
@@ -435,15 +473,22 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     if (it == 0) {
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
-        const uint16_t* wr = a.w.wp[LAYER] + (size_t)((t0 + tt) * 16 + c) * 640 + 8 * q;
+        const int gr = (t0 + tt) * 16 + c;
+        const uint16_t* wr = a.w.wp[LAYER] + (size_t)gr * 640 + 8 * q;
+        if (H_CHAIN) {
 #pragma unroll
-        for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
+          for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
+          bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+        }
         if (LAYER) {
 #pragma unroll
           for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
-          bx[tt] = *(const float4*)(a.w.bih_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+          bx[tt] = *(const float4*)(a.w.bih_p[1] + (t0 + tt) * 16 + 4 * q);
+          const uint16_t* w0r = a.w.wp[0] + (size_t)gr * 640 + P + 8 * q;  // W_hh0: the successor's ah0
+#pragma unroll
+          for (int b = 0; b < P / 32; ++b) w0[tt][b] = *(const uint4*)(w0r + 32 * b);
+          b0[tt] = *(const float4*)(a.w.bhh_p[0] + (t0 + tt) * 16 + 4 * q);
         }
-        bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
       }
     }
 #pragma unroll
@@ -456,32 +501,38 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     }
     lds_barrier();
     ST_MARK(st2);
-    // the chains of every sub-tile (h, and x on layer 1) advance together, one k block at a
-    // time, so each block's fragment reads overlap the previous block's MFMAs (sub-tiles past the
-    // list end run on the staged zeros; their results are not stored).  Each chain is still the
-    // contract's natural-k sequence from its bias.
+    // the chains of every sub-tile advance together, one k block at a time, so each block's
+    // fragment reads overlap the previous block's MFMAs (sub-tiles past the list end run on the
+    // staged zeros; their results are not stored).  Each chain is still the contract's natural-k
+    // sequence from its bias.
     static_assert(NT == 1, "one gate tile per wave");
     int ecs[DEC_SUB];
-    v4f ahs[DEC_SUB], axs[DEC_SUB];
+    v4f ahs[DEC_SUB], axs[DEC_SUB], a0s[DEC_SUB];
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       ecs[st] = ents[16 * st + c];
-      ahs[st] = v4f{bh[0].x, bh[0].y, bh[0].z, bh[0].w};
+      if (H_CHAIN) ahs[st] = v4f{bh[0].x, bh[0].y, bh[0].z, bh[0].w};
+      else ahs[st] = v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
       axs[st] = LAYER ? v4f{bx[0].x, bx[0].y, bx[0].z, bx[0].w} : v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
+      if (LAYER) a0s[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
     }
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) {
 #pragma unroll
       for (int st = 0; st < DEC_SUB; ++st) {
         const uint16_t* xr = &X[16 * st + c][8 * q];
-        ahs[st] = mfma_bf16(wh[0][b], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ahs[st]);
-        if (LAYER) axs[st] = mfma_bf16(wx[0][LAYER ? b : 0], *(const uint4*)(xr + 32 * b), axs[st]);
+        if (H_CHAIN) ahs[st] = mfma_bf16(wh[0][H_CHAIN ? b : 0], *(const uint4*)(xr + 32 * b), ahs[st]);
+        if (LAYER) {
+          const uint4 xf = *(const uint4*)(xr + 32 * b);
+          axs[st] = mfma_bf16(wx[0][LAYER ? b : 0], xf, axs[st]);
+          a0s[st] = mfma_bf16(w0[0][LAYER ? b : 0], xf, a0s[st]);
+        }
       }
     }
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ecs[st];
-      const int row = ec >= 0 ? entry_row(ec) : -1, sl = ec >= 0 ? entry_slot(ec) : 0;
+      const int row = ec >= 0 && dec_ok(entry_row(ec) < a.Npad, 2) ? entry_row(ec) : -1, sl = ec >= 0 ? entry_slot(ec) : 0;
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         const v4f ah = ahs[st], ax = axs[st];
@@ -493,6 +544,10 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
           const float hh = bf_round_ftz(og * det_tanh(cn));
           hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
           h_bf(a.hc, row, sl ^ 1, LAYER)[u] = (uint16_t)(__float_as_uint(hh) >> 16);  // hh is bf16-exact
+          if (LAYER) {
+            const v4f h0 = a0s[st];
+            *(float4*)(a.ah0 + (size_t)row * PG4 + (t0 + tt) * 16 + 4 * q) = float4{h0[0], h0[1], h0[2], h0[3]};
+          }
         }
       }
     }
@@ -501,12 +556,17 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   }
 }
 
-// G = b_p + g . W1p^T for the listed rows' new candidates.  Workgroups of 4 waves, one 16-column
-// tile (10 KB of W1p) per wave in registers: grid x = 8 column groups, y = row groups striding
-// over the emit list's tiles.  Also clears the next step's emit and live lists for the joint
-// that follows.
+// G = b_p + g . W1p^T for the listed rows' new candidates, and beside it their successors'
+// layer-1 recurrent half ah1 = b_hh1 + h1.W_hh1^T (same staged input, see dec_pred_kernel).
+// Workgroups of 4 waves, one 16-column tile (10 KB of W1p or W_hh1) per wave in registers: grid
+// x = 8 G column groups + 20 ah1 gate groups, y = row groups striding over the emit list's tiles.
+// Also clears the next step's emit and live lists for the joint that follows.  INIT (a call's
+// first step, before layer 1): only ah1, from the committed h1.
 constexpr int GXP = P + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
-constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each; grid x = 8 column groups
+constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each
+constexpr int G_GROUPS = J / (16 * (G_THREADS / 64));        // 8
+constexpr int AH1_GROUPS = PG4 / (16 * (G_THREADS / 64));    // 20
+template <bool INIT>
 __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
   constexpr int NK = G_THREADS / DEC_RT;  // row tiles whose list entries load up front
@@ -514,8 +574,9 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
-  const GridXY gxy = xcd_grid(J / (16 * (G_THREADS / 64)));
-  if (blockIdx.x == 0 && tid == 0) {
+  constexpr int G0 = INIT ? 0 : G_GROUPS;  // column groups before the ah1 groups
+  const GridXY gxy = xcd_grid(G0 + AH1_GROUPS);
+  if (!INIT && blockIdx.x == 0 && tid == 0) {
     s.count[EMIT_N(parity ^ 1)] = 0;
     s.count[LIVE_N(parity ^ 1)] = 0;
   }
@@ -526,12 +587,16 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
-  constexpr int NJ = 1;  // column tiles per wave
-  uint4 wv[NJ][P / 32];  // issued after the first tile's input loads (see dec_pred_kernel)
-  float4 b0[NJ];
+  // this wave's 16 output columns: a G column tile, or an ah1 gate tile (workgroup-uniform)
+  const bool is_g = gxy.x < G0;
+  const int jt = (is_g ? gxy.x : gxy.x - G0) * (G_THREADS / 64) + wave;
+  float* const out = is_g ? a.G : a.ah1;
+  const int ostride = is_g ? J : PG4;
+  uint4 wv[P / 32];  // issued after the first tile's input loads (see dec_pred_kernel)
+  float4 b0;
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
-    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt ? list[rt * DEC_RT + tid] : -1;
+    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? list[rt * DEC_RT + tid] : -1;
     lds_barrier();
     ST_MARK(st1);
     constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
@@ -547,19 +612,17 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       const int i = tid + G_THREADS * u;
       if (NX % G_THREADS == 0 || i < NX) {
         const int k = (i % (P / 8)) * 8, em = emv[u];
-        xv[u] = *(const uint4*)(h_bf(a.hc, em >= 0 ? entry_row(em) : 0, em >= 0 ? entry_slot(em) ^ 1 : 0, 1) + k);
+        const bool okr = em >= 0 && dec_ok(entry_row(em) < a.Npad, 4);
+        xv[u] = *(const uint4*)(h_bf(a.hc, okr ? entry_row(em) : 0, okr ? entry_slot(em) ^ (INIT ? 0 : 1) : 0, 1) + k);
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
     if (it == 0) {
+      const uint16_t* w0 = is_g ? a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q
+                                : a.w.wp[1] + (size_t)(jt * 16 + c) * 640 + P + 8 * q;
 #pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) {
-        const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
-        const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
-#pragma unroll
-        for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
-        b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
-      }
+      for (int b = 0; b < P / 32; ++b) wv[b] = *(const uint4*)(w0 + 32 * b);
+      b0 = *(const float4*)((is_g ? a.w.bp : a.w.bhh_p[1]) + jt * 16 + 4 * q);
     }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
@@ -572,22 +635,20 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     lds_barrier();
     ST_MARK(st2);
     // every sub-tile's chain advances one k block at a time (fragment reads overlap MFMAs)
-    static_assert(NJ == 1, "one column tile per wave");
     v4f accs[DEC_SUB];
 #pragma unroll
-    for (int st = 0; st < DEC_SUB; ++st) accs[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
+    for (int st = 0; st < DEC_SUB; ++st) accs[st] = v4f{b0.x, b0.y, b0.z, b0.w};
 #pragma unroll
     for (int b = 0; b < P / 32; ++b)
 #pragma unroll
       for (int st = 0; st < DEC_SUB; ++st)
-        accs[st] = mfma_bf16(wv[0][b], *(const uint4*)(&X[16 * st + c][8 * q] + 32 * b), accs[st]);
+        accs[st] = mfma_bf16(wv[b], *(const uint4*)(&X[16 * st + c][8 * q] + 32 * b), accs[st]);
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ents[16 * st + c];
       const v4f acc = accs[st];
-      const int jt = gxy.x * (G_THREADS / 64) + wave;
-      if (ec >= 0)
-        *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
+      if (ec >= 0 && dec_ok(entry_row(ec) < a.Npad && jt < (is_g ? J / 16 : PG4 / 16), 5))
+        *(float4*)(out + (size_t)entry_row(ec) * ostride + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
     }
     lds_barrier();
     ST_FLUSH(2, st0, st1, st2, 0ull);
@@ -610,6 +671,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ float Lp[4][JRT][NLAB_PAD + 1];
   __shared__ int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT];
   __shared__ int slot_[JRT], add_[JRT], flen_[JRT], idx_[JRT];
+  __shared__ int em_m[JRT], em_n;  // the tile's emitting rows (tile indices), compacted
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
@@ -628,8 +690,9 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   for (int rt = blockIdx.x; rt < ntiles; rt += gridDim.x) {
     if (tid < JRT) {
       const int i = rt * JRT + tid;
-      const int4 e = i < lcnt ? (rt == (int)blockIdx.x ? r_first : llist[i]) : int4{-1, 0, 0, 0};
-      const int r = e.x < 0 ? -1 : e.x & 0xffffff;
+      const int4 e = i < lcnt && dec_ok(i < a.Npad, 7) ? (rt == (int)blockIdx.x ? r_first : llist[i]) : int4{-1, 0, 0, 0};
+      int r = e.x < 0 ? -1 : entry_row(e.x);
+      if (r >= 0 && !dec_ok(r < a.Npad && (e.y & 0xffff) < ((e.y >> 16) & 0xffff), 8)) r = -1;
       rows[tid] = r;
       walking[tid] = r >= 0;
       emit_e[tid] = -1;
@@ -786,17 +849,61 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       const int r = lane < JRT ? rows[lane] : -1;
       const unsigned long long me = __ballot(e >= 0), mr = __ballot(r >= 0);
       unsigned long long base = 0;
+      if (lane == 0) dec_ok(false, 31);  // ran
       if (lane == 0 && (me | mr))
         base = atomicAdd((unsigned long long*)&s.count[EMIT_N(parity ^ 1)],
                          (unsigned long long)__popcll(me) | ((unsigned long long)__popcll(mr) << 32));
       base = __shfl(base, 0);
       const unsigned long long below = (1ull << lane) - 1;
-      if (e >= 0) s.list[(parity ^ 1) * a.Npad + (int)(base & 0xffffffffu) + __popcll(me & below)] = e;
-      if (r >= 0)
+      if (e >= 0 && dec_ok((int)(base & 0xffffffffu) + __popcll(me & below) < a.Npad, 9)) {
+        s.list[(parity ^ 1) * a.Npad + (int)(base & 0xffffffffu) + __popcll(me & below)] = e;
+        em_m[__popcll(me & below)] = lane;
+      }
+      if (r >= 0 && dec_ok((int)(base >> 32) + __popcll(mr & below) < a.Npad, 10))
         nlist[(int)(base >> 32) + __popcll(mr & below)] =
             live_entry(r, slot_[lane], add_[lane], tidx[lane], flen_[lane], idx_[lane]);
+      if (lane == 0) em_n = __popcll(me);
     }
-    lds_barrier();  // rows / walking / tidx / X are reused by the next row tile
+    lds_barrier();
+    // layer 0 of every emitting row's new candidate, here instead of in a launch of its own: its
+    // gates are the label table's input half plus ah0, the committed h0's recurrent half computed
+    // when that state was made (dec_pred_kernel), so the cell is all that is left -- the same
+    // cell as dec_pred_kernel's, written to the candidate slot for the next step's layer 1.
+    {
+      const int ne = em_n;
+      for (int ib = 0; ib < ne * P; ib += 4 * 256) {
+        float4 xa[4], ha[4];
+        float cv[4];
+        int rw[4], sl[4], uu[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {  // every load of the round first
+          const int i = ib + 256 * v + tid;
+          rw[v] = -1;
+          const int mi = i < ne * P ? em_m[i / P] : -1;
+          const int e = mi >= 0 && dec_ok(mi < JRT, 11) ? emit_e[mi] : -1;
+          if (i < ne * P && dec_ok(e >= 0 && entry_row(e) < a.Npad && entry_label(e) < 28, 12)) {
+            const int u = i % P, row = entry_row(e), nsl = entry_slot(e);
+            rw[v] = row;
+            sl[v] = nsl;
+            uu[v] = u;
+            xa[v] = *(const float4*)(a.w.xtab + (size_t)entry_label(e) * PG4 + 4 * u);
+            ha[v] = *(const float4*)(a.ah0 + (size_t)row * PG4 + 4 * u);
+            cv[v] = hc_part(a.hc, row, nsl, 2)[u];
+          }
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          if (rw[v] < 0) continue;
+          const float4 gs = float4{xa[v].x + ha[v].x, xa[v].y + ha[v].y, xa[v].z + ha[v].z, xa[v].w + ha[v].w};
+          const float ig = det_sigmoid(gs.x), fg = det_sigmoid(gs.y), gg = det_tanh(gs.z), og = det_sigmoid(gs.w);
+          const float cn = fg * cv[v] + ig * gg;
+          const float hh = bf_round_ftz(og * det_tanh(cn));
+          hc_part(a.hc, rw[v], sl[v] ^ 1, 2)[uu[v]] = cn;
+          h_bf(a.hc, rw[v], sl[v] ^ 1, 0)[uu[v]] = (uint16_t)(__float_as_uint(hh) >> 16);  // hh is bf16-exact
+        }
+      }
+    }
+    lds_barrier();  // rows / walking / tidx / X / em_m are reused by the next row tile
     ST_FLUSH(3, st0, st1, st2, 0ull);
   }
 }
@@ -818,7 +925,7 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   }
   // Steps are enqueued in chunks and the host reads the live count one chunk behind, so a decode
   // ends with the rest of the chunk holding its last step plus one more chunk of (cheap, but still
-  // ~20 us each: four dependent launches) empty steps.  Once few rows are left -- the long-tail
+  // ~15-20 us each: three dependent launches) empty steps.  Once few rows are left -- the long-tail
   // rows whose last emission ends the loop -- chunks shrink to 8 steps: the overshoot falls from
   // ~48 to ~12 steps while the host (~3.5 us per launch) still stays ahead of the GPU.
   constexpr int CHUNK = 32, TAIL_CHUNK = 8, TAIL_ROWS = 64;
@@ -836,12 +943,16 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_joint = ljt < JOINT_GROUPS ? ljt : JOINT_GROUPS;
     for (int i = 0; i < csz && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                         dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                         dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL(dec_g_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), rg_g)), dim3(G_THREADS), 0, st, a,
-                         p);
+      const dim3 pgrid(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred));
+      // three dependent launches per step; the call's first step (the emit list of every live row,
+      // from dec_init*) also runs ah1 of the committed states and layer 0 (see dec_pred_kernel)
+      if (step == 0) {
+        hipLaunchKernelGGL((dec_g_kernel<true>), dim3(xcd_grid_size(AH1_GROUPS, rg_g)), dim3(G_THREADS), 0, st, a, p);
+        hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
+      }
+      hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
+      hipLaunchKernelGGL((dec_g_kernel<false>), dim3(xcd_grid_size(G_GROUPS + AH1_GROUPS, rg_g)), dim3(G_THREADS), 0, st,
+                         a, p);
       hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
     }
     // poll the live-row count one chunk behind, so the host never drains the queue: the length of
@@ -888,6 +999,15 @@ int launch_dec_xtab(const DecWeights& w, float* xtab, hipStream_t st) {
 }
 
 }  // namespace rnnt
+
+#ifdef RNNT_DEC_CHECK
+extern "C" int rnnt_dev_read_dec_err(unsigned int* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_dec_err), sizeof(unsigned int)) != hipSuccess) return -1;
+  const unsigned int z = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_dec_err), &z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef RNNT_DEV_STAMPS
 // development: copy out (and reset) the step kernels' stamp records (6 x u64 each)

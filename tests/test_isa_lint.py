@@ -1,8 +1,11 @@
 """Compiler-bug lint over the HIP sources (no GPU): ROCm 7.2's AMDGPU backend drops an
 `and 0xffffff` (any mask of 17-24 bits) that feeds a 64-bit multiply by a non-power-of-two
 constant and then multiplies the unmasked word (tools/probe/probe_mul24.hip).  Every kernel
-source is compiled to LLVM IR and scanned for `mul i64 (zext (and x, M)), C` with such M, C;
-decoder.hip extracts list-entry rows through an opaque v_and for this reason."""
+source is compiled to LLVM IR and scanned for a `mul i64 V, C` (C not a power of two) whose
+operand V derives from such an `and` through zext / sext / shl / or / add / mul -- the direct form
+`mul i64 (zext (and x, M)), C` and the chain form `((size_t)(x & M) * 2 + s) * C` alike.  Round 3's
+main extracted rows with a plain mask and had 16 such multiplies (the chain form); decoder.hip
+now extracts every list-entry row through the opaque v_and of `entry_row`."""
 import glob
 import os
 import re
@@ -25,21 +28,56 @@ def masked_wide_multiplies(ir):
     return hits
 
 
+# integer operations a masked value may pass through on its way into the wide multiply (the
+# backend's 24-bit multiply matching looks through the same shifts / ors / adds / extensions:
+# ((size_t)(e & M) * 2 + slot) * 1280 is `mul i64 (or (shl (zext (and e, M)), 1), slot), 1280`)
+_PASS = {"zext", "sext", "shl", "or", "add", "mul", "trunc"}
+
+
+def _masked_source(name, defs, depth=0):
+    """The 17..24-bit `and` mask that `name` is derived from through _PASS ops, or None."""
+    d = defs.get(name)
+    if d is None or depth > 8:
+        return None
+    op, rest = d
+    if op == "and":
+        mk = re.search(r", (\d+)$", rest)
+        if mk and (1 << 16) < int(mk.group(1)) < (1 << 24):
+            return int(mk.group(1))
+        return None
+    if op not in _PASS:
+        return None
+    for operand in re.findall(r"(%[\w.]+)", rest):
+        m = _masked_source(operand, defs, depth + 1)
+        if m is not None:
+            return m
+    return None
+
+
 def _scan_function(ir):
     defs = {m.group(1): (m.group(2), m.group(4)) for m in
-            re.finditer(r"(%[\w.]+) = (\w+)((?: nuw| nsw| nneg| disjoint)*) (?:i32|i64) ([^\n]*)", ir)}
+            re.finditer(r"(%[\w.]+) = (\w+)((?: nuw| nsw| nneg| disjoint| exact)*) (?:i8|i16|i32|i64) ([^\n]*)", ir)}
     hits = []
     for m in re.finditer(r"(%[\w.]+) = mul(?: nuw| nsw)* i64 (%[\w.]+), (\d+)", ir):
         c = int(m.group(3))
         if c & (c - 1) == 0:
             continue
-        d = defs.get(m.group(2))
-        inner = re.match(r"(%[\w.]+) to", d[1]) if d and d[0] == "zext" else None
-        di = defs.get(inner.group(1)) if inner else None
-        mk = re.search(r", (\d+)$", di[1]) if di and di[0] == "and" else None
-        if mk and (1 << 16) < int(mk.group(1)) < (1 << 24):
+        if _masked_source(m.group(2), defs) is not None:
             hits.append(m.group(0))
     return hits
+
+
+def test_lint_sees_through_shl_or():
+    """The chain form (row * 2 + slot) * 1280 is flagged as well as the direct one."""
+    ir = ("\ndefine void @f(i32 %e, i64 %s) {\n"
+          "  %a = and i32 %e, 16777215\n"
+          "  %z = zext nneg i32 %a to i64\n"
+          "  %h = shl nuw nsw i64 %z, 1\n"
+          "  %o = or disjoint i64 %h, %s\n"
+          "  %m = mul nuw nsw i64 %o, 1280\n"
+          "  ret void\n}\n")
+    assert masked_wide_multiplies(ir) == ["%m = mul nuw nsw i64 %o, 1280"]
+    assert masked_wide_multiplies(ir.replace("16777215", "65535")) == []
 
 
 def _ir(src, out):
