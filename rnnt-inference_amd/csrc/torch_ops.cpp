@@ -76,18 +76,35 @@ void key_add(Key& k, const at::Tensor& t) {
   k.refs.push_back(t);
 }
 
+// Concurrency (the reference's SUT runs up to INTER=28 worker threads through these ops at once on
+// shared read-only weights, rnnt_model.hpp:45-46, torch_sut.cpp:143-149): every (device, calling
+// thread) has its own engine, so calls from different threads share no mutable state and take no
+// lock.  An engine's weights are unpacked and uploaded the first time that thread passes a weight
+// set (keyed as above); an engine orders its own calls across streams by its state event.
+// Per-call padded inputs are staged in scratch tensors owned by the engine, one set per stream
+// (a buffer reused on another stream could be overwritten while the first stream still reads it),
+// grown on demand and never reallocated per call; inputs already in the engine's padded shape are
+// passed through without a copy.  Engines are never destroyed from thread-local destructors (HIP
+// calls at thread / process exit are unsafe); intel_mlperf_mi355x_release_thread_engines() frees
+// the calling thread's engines explicitly.
+struct Scratch {
+  at::Tensor t[10];  // one slot per staged operand of each op (see the calls), so no op evicts another's
+};
 struct OpEngine {
   rnnt_engine* e = nullptr;
   int max_batch = 0, max_frames = 0;
   Key enc[5], pred, pred32, joint1, joint2;
+  std::map<void*, Scratch> scratch;  // keyed by stream
 };
-std::mutex g_mu;
-std::map<int, OpEngine> g_eng;
+thread_local std::map<int, OpEngine*> t_eng;
+thread_local int64_t t_loads = 0;  // weight-set (re)loads by this thread: intel_mlperf_mi355x_weight_loads()
 
-// The device's engine with room for n_pad rows and `frames` feature frames (recreated larger on
-// demand; its components then reload from the next call's weights).
+// This thread's engine on `dev` with room for n_pad rows and `frames` feature frames (recreated
+// larger on demand; its components then reload from the next call's weights).
 OpEngine& engine_for(int dev, int64_t n_pad, int64_t frames) {
-  OpEngine& oe = g_eng[dev];
+  OpEngine*& slot = t_eng[dev];
+  if (!slot) slot = new OpEngine{};
+  OpEngine& oe = *slot;
   if (oe.e && n_pad <= oe.max_batch && frames <= oe.max_frames) return oe;
   if (oe.e) rnnt_engine_destroy(oe.e);
   oe = OpEngine{};
@@ -102,6 +119,39 @@ OpEngine& engine_for(int dev, int64_t n_pad, int64_t frames) {
 }
 
 void* stream_of(const at::Tensor& t) { return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+// A [sizes] view of scratch buffer `i` of this engine on `stream`, zero-filled when (re)allocated.
+// Only the caller's region is written per call, so padding columns stay zero; padding rows may hold
+// an earlier call's rows, which is harmless: every op here computes rows independently and the
+// padding rows' outputs are discarded.
+at::Tensor scratch(OpEngine& oe, void* stream, int i, at::IntArrayRef sizes, const at::TensorOptions& opt) {
+  at::Tensor& s = oe.scratch[stream].t[i];
+  int64_t n = 1;
+  for (auto v : sizes) n *= v;
+  if (!s.defined() || s.numel() < n || s.scalar_type() != opt.dtype().toScalarType() || s.device() != opt.device())
+    s = at::zeros({n}, opt);
+  return s.narrow(0, 0, n).view(sizes);
+}
+
+// x as a contiguous [rows, cols] tensor of dtype st when it already is one (no copy), else undefined
+at::Tensor as_is(const at::Tensor& x, int64_t rows, int64_t cols, at::ScalarType st) {
+  if (x.scalar_type() == st && x.is_contiguous() && x.numel() == rows * cols && ((uintptr_t)x.data_ptr() & 15) == 0)
+    return x.view({rows, cols});
+  return at::Tensor();
+}
+
+// x ([A, N, C], or [N, C] when A == 1) as a contiguous [A, n_pad, C] tensor of dtype st: x itself
+// when it already is one, else scratch buffer `i` with x copied into its first N rows.
+at::Tensor staged(OpEngine& oe, void* stream, int i, const at::Tensor& x, int64_t A, int64_t N, int64_t n_pad, int64_t C,
+                  at::ScalarType st) {
+  if (N == n_pad) {
+    at::Tensor v = as_is(x, A * N, C, st);
+    if (v.defined()) return v.view({A, n_pad, C});
+  }
+  at::Tensor s = scratch(oe, stream, i, {A, n_pad, C}, x.options().dtype(st));
+  s.narrow(1, 0, N).copy_(x.reshape({A, N, C}));
+  return s;
+}
 
 template <class T>
 std::vector<T> host_vec(const at::Tensor& t, at::ScalarType st) {
@@ -173,11 +223,8 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
   TORCH_CHECK(skip_quant_y == (first + L == 5), "lstm_amx_int8: skip_quant_y is set exactly for post_rnn");
   const int64_t T = x.size(0), N = x.size(1), n_pad = round_up(N, 256);
   const int dev = x.device().index();
-  std::lock_guard<std::mutex> lock(g_mu);
   OpEngine& oe = engine_for(dev, n_pad, pre ? T : 2 * T);
-  const std::vector<float> rb = host_vec<float>(rb_scale, at::kFloat), ins = host_vec<float>(in_scale, at::kFloat),
-                           outs = host_vec<float>(out_scale, at::kFloat);
-  TORCH_CHECK((int)rb.size() >= L && (int)ins.size() >= L && (int)outs.size() >= L, "lstm_amx_int8: scale tensors");
+  std::vector<float> rb, ins, outs;  // read (a host copy) only when a layer (re)loads
   for (int i = 0; i < L; ++i) {
     const int l = first + i;
     const c10::List<at::Tensor> wl = weights.get(i);
@@ -188,6 +235,12 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
     key_add(k, in_scale);
     key_add(k, out_scale);
     if (k == oe.enc[l]) continue;
+    if (rb.empty()) {
+      rb = host_vec<float>(rb_scale, at::kFloat);
+      ins = host_vec<float>(in_scale, at::kFloat);
+      outs = host_vec<float>(out_scale, at::kFloat);
+      TORCH_CHECK((int)rb.size() >= L && (int)ins.size() >= L && (int)outs.size() >= L, "lstm_amx_int8: scale tensors");
+    }
     const int I = ENC_I[l];
     const std::vector<int8_t> wi = enc_weight(wl.get(0), I), wh = enc_weight(wl.get(1), H);
     std::vector<int8_t> w((size_t)4 * H * (I + H));
@@ -201,16 +254,17 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
     const float* bp = bq.data();
     check_rc(rnnt_engine_load_encoder_layers(oe.e, l, 1, &wp, &bp, &rb[i], &ins[i], &outs[i]), "lstm_amx_int8 load");
     oe.enc[l] = k;
+    ++t_loads;
   }
   const auto opt = x.options();
-  at::Tensor xin;
-  if (pre) {
-    xin = at::zeros({T, n_pad, 256}, opt.dtype(at::kFloat));
+  void* st = stream_of(x);
+  const int64_t C = pre ? 256 : 2 * H;
+  TORCH_CHECK(pre ? x.size(2) <= 256 : x.size(2) == 2 * H, "lstm_amx_int8: x [T, N, <=256] fp32 or [T, N, 2048] int8");
+  at::Tensor xin = x.size(2) == C ? as_is(x, T * n_pad, C, pre ? at::kFloat : at::kChar) : at::Tensor();
+  if (!xin.defined()) {
+    xin = scratch(oe, st, pre ? 0 : 9, {T, n_pad, C}, opt.dtype(pre ? at::kFloat : at::kChar));
     xin.narrow(1, 0, N).narrow(2, 0, x.size(2)).copy_(x);
-  } else {
-    TORCH_CHECK(x.size(2) == 2 * H, "lstm_amx_int8: post_rnn x int8 [T, N, 2048]");
-    xin = at::zeros({T, n_pad, 2 * H}, opt.dtype(at::kChar));
-    xin.narrow(1, 0, N).copy_(x);
+    if (x.size(2) < C) xin.narrow(2, x.size(2), C - x.size(2)).zero_();  // an earlier call may have been wider
   }
   at::Tensor h = at::zeros({L, n_pad, H}, opt.dtype(at::kChar));
   at::Tensor c = at::zeros({L, n_pad, H}, opt.dtype(at::kHalf));
@@ -220,7 +274,7 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
   }
   at::Tensor y = at::empty({T, n_pad, H}, opt.dtype(skip_quant_y ? at::kFloat : at::kChar));
   check_rc(rnnt_op_lstm_int8(oe.e, first, L, xin.data_ptr(), (int)T, (int)n_pad, (int8_t*)h.data_ptr(),
-                             (uint16_t*)c.data_ptr(), y.data_ptr(), stream_of(x)),
+                             (uint16_t*)c.data_ptr(), y.data_ptr(), st),
            "lstm_amx_int8");
   std::vector<at::Tensor> ho, co;
   for (int i = 0; i < L; ++i) {
@@ -235,15 +289,13 @@ at::Tensor stack_time(const at::Tensor& x, const at::Tensor& x_lens, int64_t fac
   TORCH_CHECK(factor == 2, "stack_time: factor 2");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kChar && x.dim() == 3, "stack_time: int8 [T, N, C] on the GPU");
   const int64_t T = x.size(0), N = x.size(1), C = x.size(2), n_pad = round_up(N, 16);
-  at::Tensor xin = at::zeros({T, n_pad, C}, x.options());
-  xin.narrow(1, 0, N).copy_(x);
-  at::Tensor lens = at::zeros({n_pad}, x.options().dtype(at::kInt));
-  lens.narrow(0, 0, N).copy_(x_lens);
-  at::Tensor y = at::empty({(T + 1) / 2, n_pad, 2 * C}, x.options());
-  std::lock_guard<std::mutex> lock(g_mu);
   OpEngine& oe = engine_for(x.device().index(), 256, 500);
+  void* st = stream_of(x);
+  const at::Tensor xin = staged(oe, st, 1, x, T, N, n_pad, C, at::kChar);
+  const at::Tensor lens = staged(oe, st, 2, x_lens.to(x.device(), at::kInt), 1, N, n_pad, 1, at::kInt);
+  at::Tensor y = at::empty({(T + 1) / 2, n_pad, 2 * C}, x.options());
   check_rc(rnnt_op_stack_time(oe.e, (const int8_t*)xin.data_ptr(), lens.data_ptr<int32_t>(), (int)T, (int)n_pad, (int)C,
-                              (int8_t*)y.data_ptr(), stream_of(x)),
+                              (int8_t*)y.data_ptr(), st),
            "stack_time");
   return N == n_pad ? y : y.narrow(1, 0, N).contiguous();
 }
@@ -258,7 +310,6 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
   TORCH_CHECK(weights.size() == 2 && hx.size() == 2 && cx.size() == 2, "lstm_amx_bf16: 2 layers");
   const at::Tensor x2 = x.reshape({-1, P});
   const int64_t N = x2.size(0), n_pad = round_up(N, 16);
-  std::lock_guard<std::mutex> lock(g_mu);
   OpEngine& oe = engine_for(x.device().index(), n_pad, 500);
   Key k;
   for (int l = 0; l < 2; ++l)
@@ -285,19 +336,21 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
     }
     check_rc(rnnt_engine_load_prediction(oe.e, nullptr, pwi, pwh, pbi, pbh), "lstm_amx_bf16 load");
     oe.pred = k;
+    ++t_loads;
   }
   const auto opt = x.options();
-  at::Tensor xb = at::zeros({n_pad, P}, opt.dtype(at::kBFloat16));
-  xb.narrow(0, 0, N).copy_(x2);
-  at::Tensor h = at::zeros({2, n_pad, P}, opt.dtype(at::kBFloat16));
-  at::Tensor c = at::zeros({2, n_pad, P}, opt.dtype(at::kFloat));
+  void* st = stream_of(x);
+  const at::Tensor xb = staged(oe, st, 3, x2, 1, N, n_pad, P, at::kBFloat16);
+  // the engine reads both layers' state as one [2, n_pad, P] block
+  at::Tensor h = scratch(oe, st, 4, {2, n_pad, P}, opt.dtype(at::kBFloat16));
+  at::Tensor c = scratch(oe, st, 5, {2, n_pad, P}, opt.dtype(at::kFloat));
   for (int l = 0; l < 2; ++l) {
-    h[l].narrow(0, 0, N).copy_(hx[l]);
-    c[l].narrow(0, 0, N).copy_(cx[l]);
+    h[l].narrow(0, 0, N).copy_(hx[l].reshape({N, P}));
+    c[l].narrow(0, 0, N).copy_(cx[l].reshape({N, P}));
   }
-  at::Tensor hy = at::empty_like(h), cy = at::empty_like(c);
+  at::Tensor hy = at::empty({2, n_pad, P}, opt.dtype(at::kBFloat16)), cy = at::empty({2, n_pad, P}, opt.dtype(at::kFloat));
   check_rc(rnnt_op_lstm_bf16(oe.e, (const uint16_t*)xb.data_ptr(), (const uint16_t*)h.data_ptr(), c.data_ptr<float>(),
-                             (uint16_t*)hy.data_ptr(), cy.data_ptr<float>(), (int)n_pad, stream_of(x)),
+                             (uint16_t*)hy.data_ptr(), cy.data_ptr<float>(), (int)n_pad, st),
            "lstm_amx_bf16");
   std::vector<at::Tensor> ho{hy[0].narrow(0, 0, N), hy[1].narrow(0, 0, N)};
   std::vector<at::Tensor> co{cy[0].narrow(0, 0, N), cy[1].narrow(0, 0, N)};
@@ -314,7 +367,6 @@ at::Tensor amx_linear_bf16_accum_relu(const at::Tensor& f, const at::Tensor& w1_
   const at::Tensor f2 = f.reshape({-1, H}), g2 = g.reshape({-1, P});
   const int64_t N = f2.size(0), n_pad = round_up(N, 16);
   TORCH_CHECK(g2.size(0) == N, "amx_linear_bf16_accum_relu: f / g rows");
-  std::lock_guard<std::mutex> lock(g_mu);
   OpEngine& oe = engine_for(f.device().index(), n_pad, 500);
   Key k;
   key_add(k, w1_trans);
@@ -327,14 +379,14 @@ at::Tensor amx_linear_bf16_accum_relu(const at::Tensor& f, const at::Tensor& w1_
     TORCH_CHECK((int)bp.size() == J, "amx_linear_bf16_accum_relu: bias [512]");
     check_rc(rnnt_engine_load_joint(oe.e, wt.data(), wp.data(), bt.data(), bp.data()), "amx_linear_bf16_accum_relu load");
     oe.joint1 = k;
+    ++t_loads;
   }
-  at::Tensor fp = at::zeros({n_pad, H}, f.options().dtype(at::kFloat));
-  fp.narrow(0, 0, N).copy_(f2);
-  at::Tensor gp = at::zeros({n_pad, P}, g.options().dtype(at::kBFloat16));
-  gp.narrow(0, 0, N).copy_(g2);
+  void* st = stream_of(f);
+  const at::Tensor fp = staged(oe, st, 6, f2, 1, N, n_pad, H, at::kFloat);
+  const at::Tensor gp = staged(oe, st, 7, g2, 1, N, n_pad, P, at::kBFloat16);
   at::Tensor y1 = at::empty({n_pad, J}, g.options().dtype(at::kBFloat16));
   check_rc(rnnt_op_joint_hidden(oe.e, fp.data_ptr<float>(), (const uint16_t*)gp.data_ptr(), (uint16_t*)y1.data_ptr(),
-                                (int)n_pad, stream_of(f)),
+                                (int)n_pad, st),
            "amx_linear_bf16_accum_relu");
   return y1.narrow(0, 0, N);
 }
@@ -342,7 +394,6 @@ at::Tensor amx_linear_bf16_accum_relu(const at::Tensor& f, const at::Tensor& w1_
 at::Tensor amx_linear_i16o32(const at::Tensor& y, const at::Tensor& w2, const at::Tensor& b2) {
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.size(1) == J, "amx_linear_i16o32: y bf16 [N, 512] on the GPU");
   const int64_t N = y.size(0), n_pad = round_up(N, 16);
-  std::lock_guard<std::mutex> lock(g_mu);
   OpEngine& oe = engine_for(y.device().index(), n_pad, 500);
   Key k;
   key_add(k, w2);
@@ -353,12 +404,12 @@ at::Tensor amx_linear_i16o32(const at::Tensor& y, const at::Tensor& w2, const at
     TORCH_CHECK(b.size() == NLAB || b.size() == 32, "amx_linear_i16o32: bias [29] or [32]");
     check_rc(rnnt_engine_load_joint_out(oe.e, w.data(), b.data()), "amx_linear_i16o32 load");
     oe.joint2 = k;
+    ++t_loads;
   }
-  at::Tensor yp = at::zeros({n_pad, J}, y.options().dtype(at::kBFloat16));
-  yp.narrow(0, 0, N).copy_(y);
+  void* st = stream_of(y);
+  const at::Tensor yp = staged(oe, st, 8, y, 1, N, n_pad, J, at::kBFloat16);
   at::Tensor logits = at::empty({n_pad, 32}, y.options().dtype(at::kFloat));
-  check_rc(rnnt_op_joint_logits(oe.e, (const uint16_t*)yp.data_ptr(), logits.data_ptr<float>(), (int)n_pad,
-                                stream_of(y)),
+  check_rc(rnnt_op_joint_logits(oe.e, (const uint16_t*)yp.data_ptr(), logits.data_ptr<float>(), (int)n_pad, st),
            "amx_linear_i16o32");
   return logits.narrow(0, 0, N);
 }
@@ -393,7 +444,6 @@ bool greedy_decode_update(const at::Tensor& symbols, const at::Tensor& symbols_a
     chg[l] = (const uint16_t*)hg[l].data_ptr();
     ccg[l] = cg[l].data_ptr<float>();
   }
-  std::lock_guard<std::mutex> lock(g_mu);
   OpEngine& oe = engine_for(symbols.device().index(), 256, 500);
   const int rc = rnnt_op_greedy_update(oe.e, symbols.data_ptr(), symbols.scalar_type() == at::kLong,
                                        symbols_added.data_ptr<int32_t>(), res.data_ptr<int32_t>(),
@@ -421,7 +471,6 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_f3
   TORCH_CHECK(weights.size() == 2 && hx.size() == 2 && cx.size() == 2, "lstm: the 2-layer prediction LSTM");
   const at::Tensor x2 = x.reshape({-1, P});
   const int64_t N = x2.size(0), n_pad = round_up(N, 64);
-  std::lock_guard<std::mutex> lock(g_mu);
   OpEngine& oe = engine_for(x.device().index(), n_pad, 500);
   Key k;
   for (int l = 0; l < 2; ++l)
@@ -440,6 +489,7 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_f3
     }
     check_rc(rnnt_engine_load_f32_prediction(oe.e, pw[0], pw[1], pw[2], pw[3]), "lstm load");
     oe.pred32 = k;
+    ++t_loads;
   }
   const auto opt = x.options().dtype(at::kFloat);
   at::Tensor xp = at::zeros({n_pad, P}, opt);
@@ -531,6 +581,17 @@ void boxed_not_served(const c10::OperatorHandle& op, torch::jit::Stack*) {
 }
 
 }  // namespace
+
+// Diagnostics of the engine cache (not part of the reference's operator surface): weight-set loads
+// performed by the calling thread, and release of the calling thread's engines.
+extern "C" int64_t intel_mlperf_mi355x_weight_loads(void) { return t_loads; }
+extern "C" void intel_mlperf_mi355x_release_thread_engines(void) {
+  for (auto& kv : t_eng) {
+    if (kv.second->e) rnnt_engine_destroy(kv.second->e);
+    delete kv.second;
+  }
+  t_eng.clear();
+}
 
 TORCH_LIBRARY(intel_mlperf, m) {
   m.def("lstm_amx_int8(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights, Tensor rb_scale, Tensor in_scale, "

@@ -43,6 +43,24 @@ def load_library(path=OPS_LIB):
     return torch.ops.intel_mlperf
 
 
+def op_weight_loads():
+    """Weight-set loads the operator library has done for the calling thread (each (device,
+    thread) has its own engine; a changed weight tensor reloads).  Diagnostics, not a reference op."""
+    import ctypes
+    load_library()
+    f = ctypes.CDLL(OPS_LIB).intel_mlperf_mi355x_weight_loads
+    f.restype = ctypes.c_int64
+    return int(f())
+
+
+def release_thread_engines():
+    """Free the calling thread's operator-library engines (device memory); the next op call on this
+    thread creates and loads a new one."""
+    import ctypes
+    load_library()
+    ctypes.CDLL(OPS_LIB).intel_mlperf_mi355x_release_thread_engines()
+
+
 def lstm_amx_int8(x, hx, cx, weights, rb_scale, in_scale, out_scale, skip_quant_y):
     """quant_lstm.py:92-101: one iLSTM stack (pre_rnn 2 layers on fp32 x, post_rnn 3 on int8)."""
     return load_library().lstm_amx_int8(x, hx, cx, weights, rb_scale, in_scale, out_scale, skip_quant_y)
