@@ -6,14 +6,15 @@ LibriSpeech-dev-clean-shaped QSL of 2513 synthetic utterances (mlperf.conf:13), 
 in HBM on every GPU.  One step = one Offline query of --query samples per GPU (default 24576 =
 *.Offline.min_query_count, mlperf.conf:63; LoadGen repeats the QSL), issued exactly as the SUT
 serves it, all inside the timed region:
-  * sort the query longest first (rnnt_qsl.cpp:104-133), split it into batches of --batch and
-    deal them to the ranks (one process per GPU; rnnt_amd.dist.shard_query);
+  * sort the query longest first (rnnt_qsl.cpp:104-133) and split it into batches of --batch;
+    with several ranks (one process per GPU) every rank claims the next batch from one shared
+    counter whenever its encoder is free (rnnt_amd.dist.BatchClaim; --deal static: snake deal);
   * per rank, rnnt_amd.sut.OfflineSUT: --inflight engines, one host thread + HIP stream each,
     pulling batches from a shared list; per batch AssembleSamples fused into the int8 encoder's
     quantize pass (gathered straight from the ragged QSL store), the wavefront-tick int8 encoder,
     bf16 prediction/joint + device-side greedy decode, and the D2H copy of the token rows
     (QuerySamplesComplete payloads);
-  * the responses of all ranks gathered to rank 0's host (rnnt_amd.dist.gather_responses).
+  * the responses of all ranks streamed to rank 0's host per completed batch (rnnt_amd.dist.ResponseStream).
 Weak scaling: the query grows with the GPU count (--query per GPU), one query served by all.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -39,7 +40,7 @@ import torch  # noqa: E402
 from rnnt_amd import dist, synthetic, weights  # noqa: E402
 from rnnt_amd.config import encoder_frames, encoder_ops  # noqa: E402
 from rnnt_amd.engine import Engine  # noqa: E402
-from rnnt_amd.sut import GpuQSL, GpuWavQSL, OfflineSUT  # noqa: E402
+from rnnt_amd.sut import GpuQSL, GpuWavQSL, OfflineSUT, make_batches  # noqa: E402
 
 METRIC = "MLPerf Offline utterances/sec at 1/2/4/8 MI355X; WER vs fp32 ref"
 INT8_DENSE_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 MFMA = 2x the ~2.5 PF dense bf16 rate
@@ -73,6 +74,9 @@ def parse():
                          "GPU featurizer (FilterbankFeatures.forward) inside the timed region")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "tools", "roofline_traffic.json"),
                     help="per-launch HBM bytes from a rocprofv3 --pmc pass (profiles/), if present")
+    ap.add_argument("--deal", choices=("dynamic", "static"), default="dynamic",
+                    help="several ranks: claim batches from one shared counter when the encoder is free (dynamic), or "
+                         "deal them in snake order up front (static)")
     ap.add_argument("--mock", action="store_true",
                     help="launcher / sharding check without a GPU: gloo ranks deal and gather a query of stand-in "
                          "responses (no engine, no HIP); the line it prints is not a measurement")
@@ -104,9 +108,19 @@ def mock_main(args):
     query = args.query * world
     ids, idx = dist.query_arrays(args.qsl, query)
 
+    qno = [0]
+
     def step():
-        mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world)
-        stream = dist.ResponseStream(world, group) if world > 1 else None
+        if args.deal == "static" or world == 1:
+            mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world)
+        else:
+            batches = make_batches(qsl, ids, idx, args.batch)
+            claim = dist.claim_for_query(qno[0], len(batches))
+            mine = []
+            while (i := claim()) is not None:
+                mine.append(batches[i])
+        stream = dist.ResponseStream(world, group, tag=qno[0]) if world > 1 else None
+        qno[0] += 1
         got = []
         for b_ids, _ in mine:  # stand-in responses, shipped batch by batch like the SUT's completions
             rl = (b_ids % 7).astype(np.int32)
@@ -199,6 +213,24 @@ def cpu_baseline(pm, qsl, batches, batch_engine, responses, n_sample, inflight):
                 engines=sorted({batch_engine[b] for b, _ in picks}))
 
 
+def host_cpu_info():
+    """CPU model, the cores this process may run on and how it is pinned (cpu_baseline metadata)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    return {"cpu_model": model, "affinity_cpus": len(aff), "machine_cpus": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "pinning": "none: OpenMP threads over the process's CPU affinity set (no numactl; the GPU box grants a "
+                       "share of the host's cores)"}
+
+
 def wer_vs_fp32(n=1024, seed=44):
     """BASELINE metric's second half ("WER vs fp32 ref"), measured on the well-conditioned
     planted model (rnnt_amd.planted: contractive encoder, confident joint -- the regime of a
@@ -275,18 +307,27 @@ def main():
     max_b = max([args.batch] + ([int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else []))
     engines = [Engine(pm, device=local, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
     sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
+    sut.warmup(iters=1, batch_size=args.batch)  # OfflineSUT::warmup (torch_sut.cpp:124-138), before any query
     sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None
 
+    qno = [0]
+
     def step():
-        """One Offline query: sort + batch + deal, this rank's share through the SUT, every batch's
-        responses streamed to rank 0 as it completes (dist.ResponseStream)."""
-        mine = dist.shard_query(qsl, ids, idx, args.batch, rank, world, sizes)
-        stream = dist.ResponseStream(world, ggroup) if world > 1 else None
+        """One Offline query: sort + batch, this rank's batches through the SUT (claimed from the
+        shared counter, or dealt), every batch's responses streamed to rank 0 as it completes
+        (dist.ResponseStream, tagged with the query number)."""
+        if world > 1 and args.deal == "dynamic":
+            batches = make_batches(qsl, ids, idx, args.batch, sizes)
+            claim = dist.claim_for_query(qno[0], len(batches))
+        else:
+            batches, claim = dist.shard_query(qsl, ids, idx, args.batch, rank, world, sizes), None
+        stream = dist.ResponseStream(world, ggroup, tag=qno[0]) if world > 1 else None
+        qno[0] += 1
         sut.on_batch = stream.push if stream else None
-        sut.issue_batches(mine)
+        sut.issue_batches(batches, claim=claim)
         local = sut.take_completed()
         got = stream.finish() if stream else local
-        return mine, got, int(local[1].sum())
+        return sut.ran_batches(batches), got, int(local[1].sum())
 
     for _ in range(args.warmup):
         step()
@@ -305,7 +346,7 @@ def main():
     elapsed_max = dist.reduce_max(elapsed)
     sts = [e.stats(reset=True) for e in engines]
     st = {k: sum(x[k] for x in sts) for k in sts[0]}
-    batch_engine = list(sut.batch_engine)
+    batch_engine = [e for e in sut.batch_engine if e is not None]  # aligned with `mine` (the batches this rank ran)
     # isolated pass (untimed): this rank's batches once more on one engine, back to back, so the
     # encoder's event time is not shared with an overlapping decode
     iso_sut = OfflineSUT([engines[0]], qsl)
@@ -371,8 +412,11 @@ def main():
                              else "log-mel features resident in HBM, gathered by the encoder's quantize pass"),
                    "encoder": "int8 (lstm_amx_int8)",
                    "decoder": "bf16 prediction/joint, fp32 accumulate, greedy (device loop)",
-                   "parallelism": f"dp{world}: one query sorted, batched and dealt to {world} process(es), one per "
-                                  f"GPU; responses gathered to rank 0's host (gloo) inside the timed region",
+                   "parallelism": f"dp{world}: one query sorted and batched; {world} process(es), one per GPU, "
+                                  + ("claim batches from one shared counter when their encoder is free" if world > 1 and
+                                     args.deal == "dynamic" else "batches dealt in snake order")
+                                  + "; responses streamed to rank 0's host (gloo) inside the timed region",
+                   "batches_run_rank0": len(mine),
                    "encoder_frames_per_query_rank0": enc_frames, "emitted_symbols_per_query": emitted},
         "roofline": roofline,
     }
@@ -382,7 +426,7 @@ def main():
         resp = responses_dict(*got)
         cb = cpu_baseline(pm, qsl, mine, batch_engine, resp, args.cpu_sample, args.inflight)
         out["cpu_baseline"] = {"value": round(cb["value"], 3), "unit": "utterances/s", "cores": cb["cores"],
-                               "kind": "port",
+                               "kind": "port", **host_cpu_info(),
                                "sample": f"{cb['n']} utterances ({cb['frames']} frames) of the timed query (batches "
                                          f"{cb['batches']}, longest to shortest rows), int8 encoder + greedy decode, "
                                          f"{cb['seconds']:.1f} s"}

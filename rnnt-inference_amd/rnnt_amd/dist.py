@@ -1,9 +1,13 @@
 """Multi-GPU serving of one Offline query: one process per GPU, host-side gather.
 
 SURVEY 8e / north_star: the query shards embarrassingly (utterances are independent).  Every
-rank sorts the same query (rnnt_qsl.cpp:104-133), ``shard_query`` deals its length-sorted
-batches to the ranks in snake order (every rank gets a similar mix of long and short
-utterances), each rank runs its share through its own OfflineSUT, and
+rank sorts the same query (rnnt_qsl.cpp:104-133) into the same length-sorted batches and pulls
+them from ONE shared claim counter (``BatchClaim``: ``TCPStore.add`` on the job's rendezvous
+store), the cross-process form of the reference's instances pulling the next slice from one
+mutex-guarded queue (torch_sut.cpp:167-182): a rank claims a batch only when its encoder is free
+(OfflineSUT's per-device encode gate), so longer batches go first and a slower GPU simply takes
+fewer of them.  ``shard_query`` (a static snake deal) is kept as the alternative
+(``bench.py --deal static``).  Each rank runs its batches through its own OfflineSUT, and
 ``ResponseStream`` (bench.py; ``gather_responses`` is the one-shot form) brings every rank's
 token rows to rank 0's host as its batches complete, where the one LoadGen instance would
 complete them (the reference's single QuerySamplesComplete point,
@@ -51,6 +55,31 @@ def shard_query(qsl, ids, idx, batch_size, rank=0, world=1, sizes=None):
         if r == rank:
             mine.append(b)
     return mine
+
+
+class BatchClaim:
+    """Shared claim counter over one query's batches: ``claim()`` -> the next batch index not yet
+    taken by any rank, or None when all are taken.  ``store.add`` is atomic on the rendezvous
+    store (one TCP round trip, ~0.1 ms, against tens of ms per batch encode); every query gets its
+    own key, so nothing needs resetting between queries."""
+
+    def __init__(self, store, key, n_batches):
+        self.store, self.key, self.n = store, key, int(n_batches)
+
+    def __call__(self):
+        i = int(self.store.add(self.key, 1)) - 1
+        return i if i < self.n else None
+
+
+def claim_for_query(qno, n_batches, store=None):
+    """The BatchClaim of query number `qno` (every rank must use the same numbering) on the
+    default process group's store (or `store`); None on a single process (nothing to share)."""
+    import torch.distributed as dist
+    if store is None:
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return None
+        store = dist.distributed_c10d._get_default_store()
+    return BatchClaim(store, f"rnnt_offline_claim/{int(qno)}", n_batches)
 
 
 def query_arrays(count, query):
@@ -126,11 +155,13 @@ class ResponseStream:
     GPUs finish.  At 8 ranks the one-shot int32 gather moved ~7 MB per rank after the query
     (≈45-55 ms over gloo on the host); this moves ~1.7 MB per rank, mostly during the query."""
 
-    def __init__(self, world, group=None):
+    def __init__(self, world, group=None, tag=0):
+        """tag: this stream's message tag (the query number): streams of back-to-back queries
+        never mix even when a fast rank's next query overtakes a slow rank's end marker."""
         import queue
         import threading
         import torch.distributed as dist
-        self.world, self.group = world, group
+        self.world, self.group, self.tag = world, group, int(tag) & 0x7FFFFFFF
         self.rank = dist.get_rank()
         self.errors = []
         self._got = []
@@ -155,12 +186,12 @@ class ResponseStream:
             while True:
                 item = self._q.get()
                 if item is None:
-                    dist.send(torch.tensor([-1, 0], dtype=torch.int64), dst=0, group=self.group)
+                    dist.send(torch.tensor([-1, 0], dtype=torch.int64), dst=0, group=self.group, tag=self.tag)
                     return
                 buf = pack_responses(*item)
                 n, m = len(item[0]), len(item[2])
-                dist.send(torch.tensor([n, m], dtype=torch.int64), dst=0, group=self.group)
-                dist.send(torch.frombuffer(bytearray(buf), dtype=torch.uint8), dst=0, group=self.group)
+                dist.send(torch.tensor([n, m], dtype=torch.int64), dst=0, group=self.group, tag=self.tag)
+                dist.send(torch.frombuffer(bytearray(buf), dtype=torch.uint8), dst=0, group=self.group, tag=self.tag)
         except Exception as ex:  # surfaced by finish()
             self.errors.append(ex)
 
@@ -168,16 +199,20 @@ class ResponseStream:
         import torch
         import torch.distributed as dist
         try:
-            open_ranks = self.world - 1
-            while open_ranks:
+            ended = set()  # end markers counted per source rank, never twice from one
+            while len(ended) < self.world - 1:
                 hdr = torch.zeros(2, dtype=torch.int64)
-                src = dist.recv(hdr, src=None, group=self.group)
+                src = dist.recv(hdr, src=None, group=self.group, tag=self.tag)
                 n, m = int(hdr[0]), int(hdr[1])
                 if n < 0:
-                    open_ranks -= 1
+                    if src in ended:
+                        raise RuntimeError(f"ResponseStream: second end marker from rank {src} (tag {self.tag})")
+                    ended.add(src)
                     continue
+                if src in ended:
+                    raise RuntimeError(f"ResponseStream: data from rank {src} after its end marker (tag {self.tag})")
                 buf = torch.empty(6 * n + m, dtype=torch.uint8)
-                dist.recv(buf, src=src, group=self.group)
+                dist.recv(buf, src=src, group=self.group, tag=self.tag)
                 self._got.append(unpack_responses(buf.numpy().tobytes(), n, m))
         except Exception as ex:
             self.errors.append(ex)
@@ -225,5 +260,5 @@ def reduce_sum(x, group=None):
     return float(t.item())
 
 
-__all__ = ["setup", "shard_query", "query_arrays", "QuerySample", "gather_responses", "ResponseStream", "pack_responses",
+__all__ = ["setup", "shard_query", "BatchClaim", "claim_for_query", "query_arrays", "QuerySample", "gather_responses", "ResponseStream", "pack_responses",
            "unpack_responses", "barrier", "reduce_max", "reduce_sum", "batch_bounds", "env_rank"]

@@ -13,9 +13,10 @@ offline, so the query / response types are plain Python):
     (QuerySamplesComplete, torch_sut.cpp:221-236) through one completion point.  Engines may sit on
     several GPUs of the process (one stream per engine on its own device; encoders on one device
     take turns, so each batch's latency-bound greedy decode overlaps the next batch's encoder).
-Multi-process (one process per GPU, bench.py / rnnt_amd.dist): every rank sorts the same query,
-``dist.shard_query`` deals the batches to ranks (snake order), each rank runs its share through
-its OfflineSUT, and the responses are gathered to rank 0's host (``dist.gather_responses``).
+Multi-process (one process per GPU, bench.py / rnnt_amd.dist): every rank sorts the same query
+into the same batches and claims them from one shared counter (``dist.BatchClaim``, passed to
+``OfflineSUT.issue_batches``) whenever its encoder is free, and the responses are streamed to rank
+0's host (``dist.ResponseStream``).
 """
 import collections
 import threading
@@ -128,6 +129,7 @@ class OfflineSUT:
         self.completed = []  # per batch: (sample ids int64 [n], lengths int32 [n], tokens int32 [sum])
         self._streams = {}
         self._enc_turns = {}  # device -> (Condition, deque of batch indices in encode order)
+        self._gates = {}  # device -> Lock held from a shared-list claim to the end of that batch's encode
         self.encode_order = []  # batch indices in the order their encodes ran (all devices)
         self._hold = None
 
@@ -140,38 +142,63 @@ class OfflineSUT:
         idx = np.fromiter((s.index for s in samples), np.int64, len(samples))
         self.issue_batches(make_batches(self.qsl_for(self.engine.device), ids, idx, self.batch_size, self.batch_sizes))
 
-    def issue_batches(self, batches):
+    def issue_batches(self, batches, claim=None):
         """Run pre-formed batches -- (sample ids, QSL indices) int64 array pairs, each
         length-sorted (make_batches) -- on the engines: one host thread per engine pulls the next
-        batch from the shared list.  self.batch_engine[i] records which engine ran batch i."""
-        import torch
+        batch from the shared list.  self.batch_engine[i] records which engine ran batch i (None:
+        another process ran it).
+
+        claim: None = this process runs every batch; or a callable returning the next batch index
+        of a list shared with other processes (dist.BatchClaim), None once all are taken.  An
+        engine thread then claims only when its device's encoder is free (it holds the device's
+        encode gate from the claim to the end of that batch's encode), so batches go, longest
+        first, to whichever GPU can start them soonest -- the reference's instances pulling from
+        one queue (torch_sut.cpp:167-182) across processes."""
         nxt = [0]
         take = threading.Lock()
         errors = []
         self.batch_engine = [None] * len(batches)
         self.encode_order = []
         k = self.early_decodes
-        hold = k is not None and k < len(batches) <= len(self.engines)
+        hold = claim is None and k is not None and k < len(batches) <= len(self.engines)
         self._hold = None
         if hold:  # the held batches wait until every batch of the query is encoded (or one encode failed)
             self._hold = dict(k=k, cv=threading.Condition(), done=0, failed=False, nb=len(batches))
         for eng in self.engines:
-            if id(eng) not in self._streams:
-                self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
+            self._stream_for(eng)
             self._enc_turns.setdefault(eng.device, (threading.Condition(), collections.deque()))
+            self._gates.setdefault(eng.device, threading.Lock())
 
         def worker(eng):
             try:
                 while True:
-                    with take:
-                        i = nxt[0]
-                        nxt[0] += 1
-                        if i < len(batches):  # encoders on one GPU run in batch order (longest first)
-                            self._enc_turns[eng.device][1].append(i)
-                    if i >= len(batches):
-                        return
+                    gate = None
+                    if claim is None:
+                        with take:
+                            i = nxt[0]
+                            nxt[0] += 1
+                            if i < len(batches):  # encoders on one GPU run in batch order (longest first)
+                                self._enc_turns[eng.device][1].append(i)
+                        if i >= len(batches):
+                            return
+                    else:
+                        gate = self._gates[eng.device]
+                        gate.acquire()  # released by _run_batch once this batch is encoded
+                        try:
+                            i = claim()
+                            if i is not None:
+                                if not 0 <= i < len(batches):
+                                    raise RuntimeError(f"OfflineSUT: claimed batch {i} of {len(batches)}")
+                                with take:
+                                    self._enc_turns[eng.device][1].append(i)
+                        except BaseException:
+                            gate.release()
+                            raise
+                        if i is None:
+                            gate.release()
+                            return
                     self.batch_engine[i] = self.engines.index(eng)
-                    self._run_batch(eng, *batches[i], bi=i)
+                    self._run_batch(eng, *batches[i], bi=i, gate=gate)
             except Exception as ex:  # surfaced below: never leave the query half-complete silently
                 errors.append(ex)
 
@@ -186,12 +213,71 @@ class OfflineSUT:
         if errors:
             raise errors[0]
 
-    def _run_batch(self, eng, ids, idx, bi=0):
+    def warmup(self, iters=1, batch_size=None, frames=R.MAX_FEA_LEN):
+        """OfflineSUT::warmup (torch_sut.cpp:124-138): before the first query, run `iters` batches of
+        dummy samples (QSL::GenerateDummySamples, rnnt_qsl.cpp:136-147: N(0,1) features of
+        MAX_FEA_LEN frames, every length MAX_FEA_LEN) through every engine -- encode + greedy decode
+        on the engine's own stream -- so first-call costs (code-object loads, lazy allocations,
+        the engine's workspace first touch) land here, not in the first query.  Nothing is
+        completed.  batch_size: rows per dummy batch (default: the SUT's batch size, at most the
+        engine's capacity).  -> seconds spent."""
+        import time
+        t0 = time.perf_counter()
+        for eng in self.engines:
+            n = max(1, min(int(batch_size or self.batch_size), int(eng.max_batch)))
+            n_pad = pad_batch(n)
+            dummy = DummyQSL(frames, seed=0)
+            st = self._stream_for(eng)
+            for _ in range(int(iters)):
+                with self._device_scope(eng, st):
+                    enc = self._encode(eng, st, None, np.zeros(n, np.int64), n, n_pad, qsl=dummy)
+                    self._decode(eng, st, enc)
+        return time.perf_counter() - t0
+
+    def ran_batches(self, batches):
+        """The batches of the last issue_batches call this process ran (all of them without a claim)."""
+        return [b for b, e in zip(batches, self.batch_engine) if e is not None]
+
+    # ---- device hooks (a host-only test stands in for these; tests/test_sut_dist.py)
+    def _stream_for(self, eng):
         import torch
-        st = self._streams[id(eng)]
+        if id(eng) not in self._streams:
+            self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
+        return self._streams[id(eng)]
+
+    def _device_scope(self, eng, st):
+        import contextlib
+        import torch
+        scope = contextlib.ExitStack()
+        scope.enter_context(torch.cuda.device(eng.device))
+        scope.enter_context(torch.cuda.stream(st))
+        return scope
+
+    def _encode(self, eng, st, ids, idx, n, n_pad, qsl=None):
+        """Enqueue and finish one batch's encode; -> the decode's output buffers."""
+        import torch
+        res = torch.empty((n, eng.max_res), dtype=torch.int32, device=st.device)
+        rl = torch.empty(n, dtype=torch.int32, device=st.device)
+        inp = (qsl or self.qsl_for(eng.device)).batch_inputs(idx, n_pad, torch.device("cuda", eng.device))
+        if "store" in inp:
+            eng.encode_gather(inp["store"], inp["offsets"], inp["lens"], inp["lens_host"], inp["T"], n, n_pad, stream=st)
+        else:
+            eng.encode(inp["x"], inp["lens"], inp["lens_host"], n=n, stream=st)
+        st.synchronize()
+        return res, rl
+
+    def _decode(self, eng, st, enc):
+        """The greedy decode of the encoded batch -> (lengths int32 [n] host, tokens [n, >=max len] host)."""
+        res, rl = enc
+        eng.decode(res, rl, stream=st)
+        rlh = rl.cpu().numpy()
+        return rlh, res[:, : max(1, int(rlh.max()))].cpu().numpy()
+
+    def _run_batch(self, eng, ids, idx, bi=0, gate=None):
+        st = self._stream_for(eng)
         n = len(ids)
         n_pad = pad_batch(n)
-        with torch.cuda.device(eng.device), torch.cuda.stream(st):
+        with self._device_scope(eng, st):
             # encoders on one GPU take turns in batch order (longest first): the longest batch's
             # decode overlaps the most encoding, and the last encode is the shortest batch's.  Every
             # step after the wait is under the finally, so a failing batch still hands the turn on.
@@ -201,20 +287,14 @@ class OfflineSUT:
                 self.encode_order.append(bi)
             encoded = False
             try:
-                res = torch.empty((n, eng.max_res), dtype=torch.int32, device=st.device)
-                rl = torch.empty(n, dtype=torch.int32, device=st.device)
-                inp = self.qsl_for(eng.device).batch_inputs(idx, n_pad, torch.device("cuda", eng.device))
-                if "store" in inp:
-                    eng.encode_gather(inp["store"], inp["offsets"], inp["lens"], inp["lens_host"], inp["T"], n, n_pad,
-                                      stream=st)
-                else:
-                    eng.encode(inp["x"], inp["lens"], inp["lens_host"], n=n, stream=st)
-                st.synchronize()
+                enc = self._encode(eng, st, ids, idx, n, n_pad)
                 encoded = True
             finally:
                 with cv:
                     turn.popleft()
                     cv.notify_all()
+                if gate is not None:  # the device's encoder is free: the next claim may go
+                    gate.release()
                 h = self._hold
                 if h is not None:  # counted even when the encode raised, so the held decodes never wait forever
                     with h["cv"]:
@@ -227,9 +307,7 @@ class OfflineSUT:
                     h["cv"].wait_for(lambda: h["done"] == h["nb"] or h["failed"])
                     if h["failed"]:
                         raise RuntimeError("OfflineSUT: an encode of this query failed; held decode abandoned")
-            eng.decode(res, rl, stream=st)
-            rlh = rl.cpu().numpy()
-            toks = res[:, : max(1, int(rlh.max()))].cpu().numpy()
+            rlh, toks = self._decode(eng, st, enc)
         self.query_samples_complete(ids, idx, toks, rlh)
 
     def query_samples_complete(self, ids, idx, toks, lens):
@@ -268,6 +346,25 @@ class OfflineSUT:
 
     def flush_queries(self):
         pass
+
+
+class DummyQSL:
+    """QSL::GenerateDummySamples (rnnt_qsl.cpp:136-147) for the SUT warmups: every requested sample
+    is N(0,1) features of `frames` frames over all PADDED_INPUT_SIZE channels, length `frames`,
+    generated on the target device (nothing staged from the host)."""
+
+    def __init__(self, frames=R.MAX_FEA_LEN, seed=0):
+        self.frames, self.seed = int(frames), int(seed)
+
+    def batch_inputs(self, indices, n_pad, device=None):
+        import torch
+        n = len(indices)
+        g = torch.Generator(device=device)
+        g.manual_seed(self.seed)
+        x = torch.randn((self.frames, n_pad, R.PADDED_INPUT_SIZE), device=device, generator=g)
+        lens = torch.zeros(n_pad, dtype=torch.int32, device=device)
+        lens[:n] = self.frames
+        return dict(x=x, lens=lens, lens_host=np.full(n, self.frames, np.int32), T=self.frames)
 
 
 class GpuQSL(_SortedQSL):
@@ -545,6 +642,52 @@ class ServerSUT:
         self._threads = []
         self.rounds = 0
         self.errors = []
+
+    def warmup(self, iters=1, frames=R.MAX_FEA_LEN):
+        """ServerSUT::warmup (torch_sut.cpp:328-352), before ``start``: the producers' part
+        (processor=true: featurize dummy audio) and the consumers' part (dummy samples of
+        MAX_FEA_LEN frames through the model) -- here every feed featurizes up to one producer batch
+        of its QSL's samples into its store (slots returned afterwards) and every engine runs `iters`
+        dummy samples in all its slots through the same split_len rounds its worker runs
+        (encode_stream + decode_stream, reset on the first chunk, h/c and greedy state carried over
+        the following chunks).  The slots' carried state is left dirty, which is harmless: a slot
+        is reset whenever it takes a sample.  -> seconds spent."""
+        import time
+        import torch
+        if self._threads:
+            raise RuntimeError("ServerSUT.warmup must run before start()")
+        t0 = time.perf_counter()
+        for feed in self.feeds:
+            k = max(1, min(feed.pro_batch, feed.store.free, len(feed.qsl.lengths)))
+            slots = feed.store.alloc(k)
+            try:
+                st = feed.make_stream()
+                feed.featurize(list(range(k)), slots, st)
+                st.synchronize()
+            finally:
+                feed.store.release(slots)
+        S, L = self.slots, self.split_len
+        for eng in self.engines:
+            dev = torch.device("cuda", eng.device)
+            with torch.cuda.device(eng.device):
+                st = self._new_stream(eng.device)
+                g = torch.Generator(device=dev)
+                g.manual_seed(0)
+                store = torch.randn((int(frames), R.trans_input_size), device=dev, generator=g)  # one dummy sample
+                res = torch.empty((S, eng.max_res), dtype=torch.int32, device=dev)
+                rl = torch.zeros(S, dtype=torch.int32, device=dev)
+                with torch.cuda.stream(st):
+                    for _ in range(int(iters)):
+                        for c0 in range(0, int(frames), L):
+                            cl = min(L, int(frames) - c0)
+                            lens_h = np.full(S, cl, np.int32)
+                            d_reset = torch.full((S,), 1 if c0 == 0 else 0, dtype=torch.int32, device=dev)
+                            d_lens = torch.from_numpy(lens_h).to(dev)
+                            d_off = torch.full((S,), c0, dtype=torch.int64, device=dev)
+                            eng.encode_stream(store, d_off, d_lens, lens_h, d_reset, cl, S, S, stream=st)
+                            eng.decode_stream(res, rl, d_reset, stream=st)
+                    st.synchronize()
+        return time.perf_counter() - t0
 
     def _assign_lanes(self, lanes):
         if lanes is not None:

@@ -28,6 +28,8 @@ def test_config4_offline_query(pm, oracle):
     engines = [Engine(pm, device=0, max_batch=batch, max_frames=500) for _ in range(3)]
     try:
         sut = OfflineSUT(engines, qsl, batch_size=batch)
+        sut.warmup(iters=1, batch_size=256)  # OfflineSUT::warmup (torch_sut.cpp:124-138): completes nothing
+        assert sut.take_completed()[0].size == 0
         ids, idx = dist.query_arrays(count, query)
         batches = make_batches(qsl, ids, idx, batch)
         assert len(batches) == 3
