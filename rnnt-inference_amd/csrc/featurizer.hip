@@ -38,7 +38,6 @@ namespace {
 
 constexpr int NT = 256;                                    // threads per (sub-)workgroup (4 waves)
 constexpr int FZ_NSUB = 3;                                 // fz_logmel: chunks (4-wave sub-groups) per workgroup
-constexpr int FZ_CU_LDS = 160 * 1024;                      // LDS per CU: one fz_logmel workgroup takes it all
 constexpr int SEGC = FZ_HOP * (FZ_CHUNK - 1) + FZ_WIN;     // 2720 samples per chunk
 constexpr int WOFF = (FZ_NFFT - FZ_WIN) / 2;               // 96: torch.stft centres the window in n_fft
 constexpr int SCR = 17 * 16;                               // 16 x 16 complex transpose, rows padded to 17
@@ -452,13 +451,17 @@ extern "C" void rnnt_featurizer_destroy(rnnt_featurizer* f) {
   delete f;
 }
 
-// fz_logmel_kernel owns a whole CU: the unused rest of the 160 KiB LDS is requested as dynamic LDS
+// fz_logmel_kernel owns a whole CU: the unused rest of the CU's LDS (read from the device: 160 KiB
+// on gfx950) is requested as dynamic LDS
 static int launch_logmel(const FzArgs& a, size_t chunks, hipStream_t st) {
   static std::atomic<uint64_t> attr{0};
   static const int pad = [] {  // thread-safe one-time init
     hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, (const void*)fz_logmel_kernel) != hipSuccess) return -1;
-    return std::max(FZ_CU_LDS - (int)fa.sharedSizeBytes, 0);
+    int dev = 0, cu_lds = 0;
+    if (hipFuncGetAttributes(&fa, (const void*)fz_logmel_kernel) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
+      return -1;
+    return std::max(cu_lds - (int)fa.sharedSizeBytes, 0);
   }();
   if (pad < 0 || set_smem_attr_once((const void*)fz_logmel_kernel, pad, attr)) return -1;
   hipLaunchKernelGGL(fz_logmel_kernel, dim3((unsigned)((chunks + FZ_NSUB - 1) / FZ_NSUB)), dim3(NT * FZ_NSUB), pad, st,
