@@ -914,6 +914,13 @@ __global__ void dec_finish_kernel(DecArgs a) {
 }
 
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st, const int32_t* reset) {
+  // every buffer the step kernels address (a missing one is a host error here, not a GPU fault)
+  const void* need[] = {a.F, a.f_lens, a.hc, a.G, a.ah0, a.ah1, a.res, a.res_len, a.w.xtab, a.w.wp[0], a.w.wp[1],
+                        a.w.bih_p[1], a.w.bhh_p[0], a.w.bhh_p[1], a.w.w1p, a.w.bp, a.w.w2, a.w.b2, a.s.time,
+                        a.s.added, a.s.idx, a.s.preg, a.s.slot, a.s.fin, a.s.list, a.s.live, a.s.count};
+  for (const void* p : need)
+    if (!p) return -1;
+  if (a.Npad % DEC_RT || a.N > a.Npad || a.Npad >= (1 << 24)) return -1;
   const int rt = a.Npad / DEC_RT;
   if (hipMemsetAsync(a.s.count, 0, 4 * sizeof(int32_t), st) != hipSuccess) return -1;
   if (reset) {
