@@ -30,6 +30,10 @@
 #include "rnnt_device.hpp"
 #include "decoder.hpp"
 
+#ifndef RNNT_DEC_EARLY_W
+#define RNNT_DEC_EARLY_W 0  // step kernels' weight slices issued behind the list loads (1) or the inputs (0)
+#endif
+
 namespace rnnt {
 
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
@@ -415,14 +419,38 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
   const int e0 = i0 < a.Npad ? list[i0] : -1;
   const int cnt = s.count[EMIT_N(parity)];
+  const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
+  // the weight slice (10 / 20 x 16 B per lane): by default issued after the first tile's input
+  // loads (vmcnt retires in order, so loads issued before the inputs would hold up the staging);
+  // RNNT_DEC_EARLY_W issues it right behind the list loads instead, so it lands while the entries
+  // and then the inputs make their round trips
+  uint4 wh[NT][H_CHAIN ? P / 32 : 1], wx[NT][LAYER ? P / 32 : 1], w0[NT][LAYER ? P / 32 : 1];
+  float4 bh[NT], bx[NT], b0[NT];
+  auto load_w = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+      const int gr = (t0 + tt) * 16 + c;
+      const uint16_t* wr = a.w.wp[LAYER] + (size_t)gr * 640 + 8 * q;
+      if (H_CHAIN) {
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
+        bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+      }
+      if (LAYER) {
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
+        bx[tt] = *(const float4*)(a.w.bih_p[1] + (t0 + tt) * 16 + 4 * q);
+        const uint16_t* w0r = a.w.wp[0] + (size_t)gr * 640 + P + 8 * q;  // W_hh0: the successor's ah0
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) w0[tt][b] = *(const uint4*)(w0r + 32 * b);
+        b0[tt] = *(const float4*)(a.w.bhh_p[0] + (t0 + tt) * 16 + 4 * q);
+      }
+    }
+  };
+  if (RNNT_DEC_EARLY_W) load_w();
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
-  const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
-  // the weight slice (10 / 20 x 16 B per lane) is issued after the first tile's input loads:
-  // vmcnt retires in order, so loads issued first would hold up the staging that needs the inputs
-  uint4 wh[NT][H_CHAIN ? P / 32 : 1], wx[NT][LAYER ? P / 32 : 1], w0[NT][LAYER ? P / 32 : 1];
-  float4 bh[NT], bx[NT], b0[NT];
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT)  // past the prefetched tiles (the slot's tile is done)
@@ -470,27 +498,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
-    if (it == 0) {
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        const int gr = (t0 + tt) * 16 + c;
-        const uint16_t* wr = a.w.wp[LAYER] + (size_t)gr * 640 + 8 * q;
-        if (H_CHAIN) {
-#pragma unroll
-          for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
-          bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
-        }
-        if (LAYER) {
-#pragma unroll
-          for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
-          bx[tt] = *(const float4*)(a.w.bih_p[1] + (t0 + tt) * 16 + 4 * q);
-          const uint16_t* w0r = a.w.wp[0] + (size_t)gr * 640 + P + 8 * q;  // W_hh0: the successor's ah0
-#pragma unroll
-          for (int b = 0; b < P / 32; ++b) w0[tt][b] = *(const uint4*)(w0r + 32 * b);
-          b0[tt] = *(const float4*)(a.w.bhh_p[0] + (t0 + tt) * 16 + 4 * q);
-        }
-      }
-    }
+    if (!RNNT_DEC_EARLY_W && it == 0) load_w();
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int i = tid + PRED_THREADS * u;
@@ -584,16 +592,24 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
   const int e0 = i0 < a.Npad ? list[i0] : -1;
   const int cnt = s.count[EMIT_N(parity)];
-  const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
-  if (gxy.y >= ntiles) return;
-  ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
   // this wave's 16 output columns: a G column tile, or an ah1 gate tile (workgroup-uniform)
   const bool is_g = gxy.x < G0;
   const int jt = (is_g ? gxy.x : gxy.x - G0) * (G_THREADS / 64) + wave;
   float* const out = is_g ? a.G : a.ah1;
   const int ostride = is_g ? J : PG4;
-  uint4 wv[P / 32];  // issued after the first tile's input loads (see dec_pred_kernel)
+  uint4 wv[P / 32];  // issued after the first tile's input loads, or early (see dec_pred_kernel)
   float4 b0;
+  auto load_w = [&]() __attribute__((always_inline)) {
+    const uint16_t* w0 = is_g ? a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q
+                              : a.w.wp[1] + (size_t)(jt * 16 + c) * 640 + P + 8 * q;
+#pragma unroll
+    for (int b = 0; b < P / 32; ++b) wv[b] = *(const uint4*)(w0 + 32 * b);
+    b0 = *(const float4*)((is_g ? a.w.bp : a.w.bhh_p[1]) + jt * 16 + 4 * q);
+  };
+  if (RNNT_DEC_EARLY_W) load_w();
+  const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
+  if (gxy.y >= ntiles) return;
+  ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? list[rt * DEC_RT + tid] : -1;
@@ -617,13 +633,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
-    if (it == 0) {
-      const uint16_t* w0 = is_g ? a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q
-                                : a.w.wp[1] + (size_t)(jt * 16 + c) * 640 + P + 8 * q;
-#pragma unroll
-      for (int b = 0; b < P / 32; ++b) wv[b] = *(const uint4*)(w0 + 32 * b);
-      b0 = *(const float4*)((is_g ? a.w.bp : a.w.bhh_p[1]) + jt * 16 + 4 * q);
-    }
+    if (!RNNT_DEC_EARLY_W && it == 0) load_w();
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int i = tid + G_THREADS * u;

@@ -360,6 +360,10 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       yb[i] = q8_biased(hh * outs);
     }
     const uint32_t hq = pack_q8(hb[0], hb[1], hb[2], hb[3]), yq = pack_q8(yb[0], yb[1], yb[2], yb[3]);
+#ifdef RNNT_ABL_NOIMG  // profiling ablation only (tools/enc_ablate.sh): results kept live, no LDS image stores
+    asm volatile("" ::"v"(hq), "v"(yq), "v"(cw[0]), "v"(cw[1]));
+    continue;
+#endif
     if (WMT == 4) {
       *(uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)) = uint2{cw[0], cw[1]};
       *(uint32_t*)(hs + r * HP + ul) = hq;

@@ -32,6 +32,6 @@ FEAT=""
 grep -q "g_dec_err" $SRC/decoder.hip && FEAT="$FEAT -DEMU_HAS_DEC_CHECK"
 grep -q "float\* ah0;" $SRC/decoder.hpp && FEAT="$FEAT -DEMU_HAS_AH"
 $CXX $SAN -g -std=c++20 -ffp-contract=off -pthread $FEAT \
-  -DRNNT_DEC_CHECK -I$ROOT/tools/emu -I$OUT $ROOT/tools/emu/dec_emu.cpp $ROOT/oracle/rnnt_oracle.c \
+  -DRNNT_DEC_CHECK ${EMU_CFLAGS} -I$ROOT/tools/emu -I$OUT $ROOT/tools/emu/dec_emu.cpp $ROOT/oracle/rnnt_oracle.c \
   -o $OUT/dec_emu -lm
 echo "built $OUT/dec_emu"
