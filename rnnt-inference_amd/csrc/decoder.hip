@@ -30,6 +30,9 @@
 #include "rnnt_device.hpp"
 #include "decoder.hpp"
 
+#ifndef DEC_TAIL3_ROWS
+#define DEC_TAIL3_ROWS 0  // default: four-launch steps throughout (three-launch steps measured slower)
+#endif
 #ifndef RNNT_DEC_EARLY_W
 #define RNNT_DEC_EARLY_W 0  // step kernels' weight slices issued behind the list loads (1) or the inputs (0)
 #endif
@@ -396,12 +399,17 @@ constexpr int G_ROW_GROUPS = 48;
 constexpr int JOINT_GROUPS = 512;
 
 // NW waves per workgroup (NW gate tiles; 4: 8-wave workgroups measured no faster)
-template <int LAYER, int NW>
+// HCH: this layer's recurrent chain b_hh + h.W_hh^T runs here over the committed h (always on
+// layer 0; on layer 1 in four-launch steps -- in three-launch steps it is ah1, precomputed).
+// AH0 (layer 1, three-launch steps): also the W_hh0 chain over the new candidate's h0 -> ah0.
+template <int LAYER, int NW, bool HCH, bool AH0>
 __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity) {
+  static_assert(LAYER == 1 || (HCH && !AH0), "layer 0 runs its own recurrent chain and no ah0");
   constexpr int PRED_THREADS = NW * 64;
-  constexpr int NT = 1;                     // gate tiles per wave
-  constexpr bool H_CHAIN = LAYER == 0;  // this layer's recurrent chain runs here (layer 1: ah1)
-  constexpr int KX = P;                 // staged k: layer 0 h0 committed, layer 1 h0 of the candidate
+  constexpr int NT = 1;                 // gate tiles per wave
+  constexpr bool H_CHAIN = HCH;
+  // staged k: layer 0 [h0 committed]; layer 1 [h0 of the candidate | h1 committed (HCH)]
+  constexpr int KX = (LAYER && HCH) ? 2 * P : P;
   // bf16 pitch +32 B per row: every ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows c, 16-B
   // column q) lands on 16 distinct bank quads; the round-2 +16 B pitch put rows c and c+8 on the same
   // quads (2-way, 36-37 % of the LDS cycles of these kernels in the r02 PMC pass)
@@ -424,7 +432,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   // loads (vmcnt retires in order, so loads issued before the inputs would hold up the staging);
   // RNNT_DEC_EARLY_W issues it right behind the list loads instead, so it lands while the entries
   // and then the inputs make their round trips
-  uint4 wh[NT][H_CHAIN ? P / 32 : 1], wx[NT][LAYER ? P / 32 : 1], w0[NT][LAYER ? P / 32 : 1];
+  uint4 wh[NT][H_CHAIN ? P / 32 : 1], wx[NT][LAYER ? P / 32 : 1], w0[NT][AH0 ? P / 32 : 1];
   float4 bh[NT], bx[NT], b0[NT];
   auto load_w = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -440,6 +448,8 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
 #pragma unroll
         for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
         bx[tt] = *(const float4*)(a.w.bih_p[1] + (t0 + tt) * 16 + 4 * q);
+      }
+      if (AH0) {
         const uint16_t* w0r = a.w.wp[0] + (size_t)gr * 640 + P + 8 * q;  // W_hh0: the successor's ah0
 #pragma unroll
         for (int b = 0; b < P / 32; ++b) w0[tt][b] = *(const uint4*)(w0r + 32 * b);
@@ -471,12 +481,12 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
         cp[st][tt] = ec >= 0 ? hc_part(a.hc, entry_row(ec), entry_slot(ec), 2 + LAYER)[(t0 + tt) * 4 + q] : 0.0f;
         if (!LAYER)
           xt[st][tt] = *(const float4*)(a.w.xtab + (size_t)(ec >= 0 ? entry_label(ec) : 28) * PG4 + (t0 + tt) * 16 + 4 * q);
-        else
+        else if (!HCH)
           xt[st][tt] = *(const float4*)(a.ah1 + (size_t)(ec >= 0 ? entry_row(ec) : 0) * PG4 + (t0 + tt) * 16 + 4 * q);
       }
     }
-    // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1 h0 of the
-    // candidate slot
+    // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1 [h0 of the
+    // candidate slot | h1 committed (HCH)]
     // every load of the tile first (one memory round trip); entries past the list end read row
     // 0 (a safe cached address) and stage zeros
     constexpr int NX = DEC_RT * (KX / 8), NIT = (NX + PRED_THREADS - 1) / PRED_THREADS;
@@ -493,7 +503,8 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       if (NX % PRED_THREADS == 0 || i < NX) {
         const int k = (i % (KX / 8)) * 8, em = emv[u];
         const int r = em >= 0 && dec_ok(entry_row(em) < a.Npad, 1) ? entry_row(em) : 0, smm = em >= 0 ? entry_slot(em) : 0;
-        const uint16_t* src = h_bf(a.hc, r, LAYER == 0 ? smm : smm ^ 1, 0) + k;
+        const uint16_t* src = LAYER == 0 ? h_bf(a.hc, r, smm, 0) + k
+                                         : (k < P ? h_bf(a.hc, r, smm ^ 1, 0) + k : h_bf(a.hc, r, smm, 1) + k - P);
         xv[u] = *(const uint4*)src;
       }
     }
@@ -522,18 +533,18 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       if (H_CHAIN) ahs[st] = v4f{bh[0].x, bh[0].y, bh[0].z, bh[0].w};
       else ahs[st] = v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
       axs[st] = LAYER ? v4f{bx[0].x, bx[0].y, bx[0].z, bx[0].w} : v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
-      if (LAYER) a0s[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
+      if (AH0) a0s[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
     }
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) {
 #pragma unroll
       for (int st = 0; st < DEC_SUB; ++st) {
         const uint16_t* xr = &X[16 * st + c][8 * q];
-        if (H_CHAIN) ahs[st] = mfma_bf16(wh[0][H_CHAIN ? b : 0], *(const uint4*)(xr + 32 * b), ahs[st]);
+        if (H_CHAIN) ahs[st] = mfma_bf16(wh[0][H_CHAIN ? b : 0], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ahs[st]);
         if (LAYER) {
           const uint4 xf = *(const uint4*)(xr + 32 * b);
           axs[st] = mfma_bf16(wx[0][LAYER ? b : 0], xf, axs[st]);
-          a0s[st] = mfma_bf16(w0[0][LAYER ? b : 0], xf, a0s[st]);
+          if (AH0) a0s[st] = mfma_bf16(w0[0][AH0 ? b : 0], xf, a0s[st]);
         }
       }
     }
@@ -552,7 +563,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
           const float hh = bf_round_ftz(og * det_tanh(cn));
           hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
           h_bf(a.hc, row, sl ^ 1, LAYER)[u] = (uint16_t)(__float_as_uint(hh) >> 16);  // hh is bf16-exact
-          if (LAYER) {
+          if (AH0) {
             const v4f h0 = a0s[st];
             *(float4*)(a.ah0 + (size_t)row * PG4 + (t0 + tt) * 16 + 4 * q) = float4{h0[0], h0[1], h0[2], h0[3]};
           }
@@ -564,17 +575,24 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   }
 }
 
-// G = b_p + g . W1p^T for the listed rows' new candidates, and beside it their successors'
-// layer-1 recurrent half ah1 = b_hh1 + h1.W_hh1^T (same staged input, see dec_pred_kernel).
-// Workgroups of 4 waves, one 16-column tile (10 KB of W1p or W_hh1) per wave in registers: grid
-// x = 8 G column groups + 20 ah1 gate groups, y = row groups striding over the emit list's tiles.
-// Also clears the next step's emit and live lists for the joint that follows.  INIT (a call's
-// first step, before layer 1): only ah1, from the committed h1.
+// G = b_p + g . W1p^T for the listed rows' new candidates (MODE G_ONLY: four-launch steps) and
+// beside it their successors' layer-1 recurrent half ah1 = b_hh1 + h1.W_hh1^T (MODE G_AH1:
+// three-launch steps; same staged input, see dec_pred_kernel).  MODE AH_LIVE (the step that
+// switches to three launches): no G, but ah0 = b_hh0 + h0.W_hh0^T and ah1 of the current
+// candidate of every row of the LIVE list -- candidates made in four-launch steps have none.
+// Workgroups of 4 waves, one 16-column tile (10 KB of W1p, W_hh0 or W_hh1) per wave in registers:
+// grid x = the column groups (8 G, 20 ah0, 20 ah1 as the mode has them), y = row groups striding
+// over the list's tiles.  The G modes also clear the next step's emit and live lists for the joint
+// that follows.
 constexpr int GXP = P + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
 constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each
 constexpr int G_GROUPS = J / (16 * (G_THREADS / 64));        // 8
 constexpr int AH1_GROUPS = PG4 / (16 * (G_THREADS / 64));    // 20
-template <bool INIT>
+enum { G_ONLY = 0, G_AH1 = 1, AH_LIVE = 2 };
+__host__ __device__ constexpr int g_cols(int mode) {
+  return mode == G_ONLY ? G_GROUPS : mode == G_AH1 ? G_GROUPS + AH1_GROUPS : 2 * AH1_GROUPS;
+}
+template <int MODE>
 __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
   constexpr int NK = G_THREADS / DEC_RT;  // row tiles whose list entries load up front
@@ -582,29 +600,35 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
-  constexpr int G0 = INIT ? 0 : G_GROUPS;  // column groups before the ah1 groups
-  const GridXY gxy = xcd_grid(G0 + AH1_GROUPS);
-  if (!INIT && blockIdx.x == 0 && tid == 0) {
+  constexpr int NG = MODE == AH_LIVE ? 0 : G_GROUPS;  // G column groups, then ah0 groups, then ah1 groups
+  constexpr int NA0 = MODE == AH_LIVE ? AH1_GROUPS : 0;
+  const GridXY gxy = xcd_grid(g_cols(MODE));
+  if (MODE != AH_LIVE && blockIdx.x == 0 && tid == 0) {
     s.count[EMIT_N(parity ^ 1)] = 0;
     s.count[LIVE_N(parity ^ 1)] = 0;
   }
-  const int* list = s.list + parity * a.Npad;
+  // entries: the emit list, or (AH_LIVE) the live list's first words, whose row / slot bits are
+  // laid out as an emit entry's
+  auto entry = [&](int i) __attribute__((always_inline)) -> int {
+    return MODE == AH_LIVE ? s.live[parity * a.Npad + i].x : s.list[parity * a.Npad + i];
+  };
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
-  const int e0 = i0 < a.Npad ? list[i0] : -1;
-  const int cnt = s.count[EMIT_N(parity)];
-  // this wave's 16 output columns: a G column tile, or an ah1 gate tile (workgroup-uniform)
-  const bool is_g = gxy.x < G0;
-  const int jt = (is_g ? gxy.x : gxy.x - G0) * (G_THREADS / 64) + wave;
-  float* const out = is_g ? a.G : a.ah1;
-  const int ostride = is_g ? J : PG4;
+  const int e0 = i0 < a.Npad ? entry(i0) : -1;
+  const int cnt = s.count[MODE == AH_LIVE ? LIVE_N(parity) : EMIT_N(parity)];
+  // this wave's 16 output columns: a G column tile, an ah0 or an ah1 gate tile (workgroup-uniform)
+  const int kind = gxy.x < NG ? 0 : gxy.x < NG + NA0 ? 1 : 2;  // 0: G, 1: ah0, 2: ah1
+  const int jt = (gxy.x - (kind == 0 ? 0 : kind == 1 ? NG : NG + NA0)) * (G_THREADS / 64) + wave;
+  float* const out = kind == 0 ? a.G : kind == 1 ? a.ah0 : a.ah1;
+  const int ostride = kind == 0 ? J : PG4;
+  const int hl = kind == 1 ? 0 : 1;  // staged layer: h0 for ah0, h1 otherwise
   uint4 wv[P / 32];  // issued after the first tile's input loads, or early (see dec_pred_kernel)
   float4 b0;
   auto load_w = [&]() __attribute__((always_inline)) {
-    const uint16_t* w0 = is_g ? a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q
-                              : a.w.wp[1] + (size_t)(jt * 16 + c) * 640 + P + 8 * q;
+    const uint16_t* w0 = kind == 0 ? a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q
+                                   : a.w.wp[hl] + (size_t)(jt * 16 + c) * 640 + P + 8 * q;
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) wv[b] = *(const uint4*)(w0 + 32 * b);
-    b0 = *(const float4*)((is_g ? a.w.bp : a.w.bhh_p[1]) + jt * 16 + 4 * q);
+    b0 = *(const float4*)((kind == 0 ? a.w.bp : a.w.bhh_p[hl]) + jt * 16 + 4 * q);
   };
   if (RNNT_DEC_EARLY_W) load_w();
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
@@ -612,7 +636,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
-    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? list[rt * DEC_RT + tid] : -1;
+    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? entry(rt * DEC_RT + tid) : -1;
     lds_barrier();
     ST_MARK(st1);
     constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
@@ -629,7 +653,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       if (NX % G_THREADS == 0 || i < NX) {
         const int k = (i % (P / 8)) * 8, em = emv[u];
         const bool okr = em >= 0 && dec_ok(entry_row(em) < a.Npad, 4);
-        xv[u] = *(const uint4*)(h_bf(a.hc, okr ? entry_row(em) : 0, okr ? entry_slot(em) ^ (INIT ? 0 : 1) : 0, 1) + k);
+        xv[u] = *(const uint4*)(h_bf(a.hc, okr ? entry_row(em) : 0, okr ? entry_slot(em) ^ 1 : 0, hl) + k);
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
@@ -657,7 +681,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ents[16 * st + c];
       const v4f acc = accs[st];
-      if (ec >= 0 && dec_ok(entry_row(ec) < a.Npad && jt < (is_g ? J / 16 : PG4 / 16), 5))
+      if (ec >= 0 && dec_ok(entry_row(ec) < a.Npad && jt < (kind == 0 ? J / 16 : PG4 / 16), 5))
         *(float4*)(out + (size_t)entry_row(ec) * ostride + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
     }
     lds_barrier();
@@ -676,6 +700,8 @@ constexpr int JOINT_ITERS = 2;  // 1 / 3 / 4 measured slower (DESIGN.md section 
 
 constexpr int YP = J + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
 constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 waves x 4 rows x 16 lanes onto it
+// L0CELL (three-launch steps): also layer 0 of every emitting row's new candidate (see below)
+template <bool L0CELL>
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[JRT][YP];
   __shared__ float Lp[4][JRT][NLAB_PAD + 1];
@@ -879,7 +905,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     // gates are the label table's input half plus ah0, the committed h0's recurrent half computed
     // when that state was made (dec_pred_kernel), so the cell is all that is left -- the same
     // cell as dec_pred_kernel's, written to the candidate slot for the next step's layer 1.
-    {
+    if (L0CELL) {
       const int ne = em_n;
       for (int ib = 0; ib < ne * P; ib += 4 * 256) {
         float4 xa[4], ha[4];
@@ -923,6 +949,20 @@ __global__ void dec_finish_kernel(DecArgs a) {
   if (row < a.N) a.res_len[row] = a.s.idx[row] + 1;
 }
 
+// Step structure by live rows: with many live rows the four-launch step (layer 0 -> layer 1 -> G
+// -> joint) is cheaper -- the three-launch step's precomputed recurrent halves cost 2 x 5 KB of
+// fp32 written and read back per emission, which the early steps' thousands of emissions pay in
+// bandwidth; with few, the three-launch step (layer 1 + ah0 -> G + ah1 -> joint + layer-0 cell)
+// saves a dependent launch.  Rows at or below which the three-launch step runs: RNNT_DEC_TAIL3_ROWS
+// (0: never, a large value: from the first step).
+static int dec_tail3_rows() {
+  static const int v = [] {
+    const char* e = getenv("RNNT_DEC_TAIL3_ROWS");
+    return e ? atoi(e) : DEC_TAIL3_ROWS;
+  }();
+  return v;
+}
+
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st, const int32_t* reset) {
   // every buffer the step kernels address (a missing one is a host error here, not a GPU fault)
   const void* need[] = {a.F, a.f_lens, a.hc, a.G, a.ah0, a.ah1, a.res, a.res_len, a.w.xtab, a.w.wp[0], a.w.wp[1],
@@ -949,6 +989,8 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   int step = 0, chunk = 0;
   int live_bound = a.N;  // unfinished rows at the end of the last chunk read back (an upper bound)
   bool done = false;
+  bool mode3 = false;    // the steps so far run three launches (see below)
+  const int tail3 = dec_tail3_rows();
   while (!done && step < a.max_iter) {
     const int csz = live_bound > TAIL_ROWS ? CHUNK : TAIL_CHUNK;
     // row-tile workgroups per launch: one resident round, and no more than the live rows need
@@ -958,19 +1000,38 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_g = lt1 < G_ROW_GROUPS ? lt1 : G_ROW_GROUPS;
     const int ljt = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
     const int rg_joint = ljt < JOINT_GROUPS ? ljt : JOINT_GROUPS;
+    // step structure of this chunk: four launches while many rows are live, three once at most
+    // tail3 rows are (the host's bound, one chunk behind); the switch is one way
+    const bool want3 = live_bound <= tail3;
     for (int i = 0; i < csz && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
       const dim3 pgrid(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred));
-      // three dependent launches per step; the call's first step (the emit list of every live row,
-      // from dec_init*) also runs ah1 of the committed states and layer 0 (see dec_pred_kernel)
-      if (step == 0) {
-        hipLaunchKernelGGL((dec_g_kernel<true>), dim3(xcd_grid_size(AH1_GROUPS, rg_g)), dim3(G_THREADS), 0, st, a, p);
-        hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
+      if (step == 0 || !mode3) {
+        // layer 0 runs as its own launch: a call's first step (every live row's first prediction,
+        // emit list from dec_init*) and every four-launch step.  On the step that switches to three
+        // launches, the candidates made by earlier four-launch steps get their ah0 / ah1 first.
+        if (want3 && step > 0) {
+          const int ljt = (live_bound + DEC_RT - 1) / DEC_RT > 0 ? (live_bound + DEC_RT - 1) / DEC_RT : 1;
+          const int rg_ah = ljt < G_ROW_GROUPS ? ljt : G_ROW_GROUPS;
+          hipLaunchKernelGGL((dec_g_kernel<AH_LIVE>), dim3(xcd_grid_size(g_cols(AH_LIVE), rg_ah)), dim3(G_THREADS), 0, st,
+                             a, p);
+        }
+        hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64, true, false>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
+        if (want3)
+          hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64, true, true>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
+        else
+          hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64, true, false>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
+        mode3 = want3;
+      } else {
+        hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64, false, true>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
       }
-      hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL((dec_g_kernel<false>), dim3(xcd_grid_size(G_GROUPS + AH1_GROUPS, rg_g)), dim3(G_THREADS), 0, st,
-                         a, p);
-      hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
+      if (mode3) {
+        hipLaunchKernelGGL((dec_g_kernel<G_AH1>), dim3(xcd_grid_size(g_cols(G_AH1), rg_g)), dim3(G_THREADS), 0, st, a, p);
+        hipLaunchKernelGGL(dec_joint_kernel<true>, dim3(rg_joint), dim3(256), 0, st, a, p);
+      } else {
+        hipLaunchKernelGGL((dec_g_kernel<G_ONLY>), dim3(xcd_grid_size(g_cols(G_ONLY), rg_g)), dim3(G_THREADS), 0, st, a, p);
+        hipLaunchKernelGGL(dec_joint_kernel<false>, dim3(rg_joint), dim3(256), 0, st, a, p);
+      }
     }
     // poll the live-row count one chunk behind, so the host never drains the queue: the length of
     // the live list the chunk's last joint wrote (parity step & 1; the next step's G kernel resets

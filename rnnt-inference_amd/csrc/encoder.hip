@@ -290,7 +290,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     // reading the buffer stage s+NBUF-1 refills
     wait_stage<C::PA + C::PB, NBUF>(nS - 1 - s);
     if (s + NBUF - 1 < nS) issueA(s + NBUF - 1);
+#ifndef RNNT_ABL_NOC  // profiling ablation only (tools/enc_ablate.sh): the cell state neither read nor written
     else if (s == nS - 1) issue_c();
+#endif
     const int8_t* st = smem + (s % NBUF) * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -403,7 +405,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   for (int it = 0; it < (BN * C::CPR + NWAVE * 64 - 1) / (NWAVE * 64); ++it) {  // c (and bf16 f): BN rows x CROW bytes
     const int idx = it * NWAVE * 64 + tid, r = idx / C::CPR, ch = idx % C::CPR;
     if ((BN * C::CPR) % (NWAVE * 64) != 0 && idx >= BN * C::CPR) break;
+#ifndef RNNT_ABL_NOC
     st16<WT>(a.c, ((size_t)(n0 + r) * H + um + ch * 8) * 2, *(const uint4*)(smem + cbuf + cimg_off<C::CROW>(r, ch * 16)));
+#endif
     if (a.mode == ENC_OUT_FINAL)  // read after the launch only: plain
       *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + cimg_off<C::CROW>(r, ch * 16));
   }

@@ -15,7 +15,7 @@ import sys
 def main():
     src = sys.argv[1]
     out = {}
-    for v in ("base", "notab", "noimg", "both"):
+    for v in ("base", "notab", "noimg", "both", "noc"):
         rec = {}
         try:
             rec["time"] = json.load(open(os.path.join(src, f"time_{v}.json")))
