@@ -19,23 +19,13 @@
 //   * prediction(pre_g, pre_hg, pre_cg) depends only on state that changes on an emit, so it
 //     (and the joint's prediction half G) is evaluated once per emit, not once per step;
 //   * layer 0's input half b_ih + emb[g].W_ih^T depends only on the label: a [29][1280] table
-//     computed once per engine with the same instruction sequence (launch_dec_xtab);
-//   * the recurrent halves b_hh + h.W_hh^T of a prediction depend only on the committed state,
-//     i.e. on the previous candidate, so they are computed when that candidate is made (beside
-//     layer 1 and G); the joint then runs layer 0's cell itself at an emission.
-// The step is latency-bound (three dependent launches: layer 1, G, joint), so each kernel keeps its chain of
+//     computed once per engine with the same instruction sequence (launch_dec_xtab).
+// The step is latency-bound (four dependent launches), so each kernel keeps its chain of
 // dependent memory round trips short: emit-list entries carry (row, slot, label), the list
 // entries of a workgroup's first tile are loaded beside the list length, the cell state is
 // fetched beside the input staging, and the joint walks a compact list of unfinished rows.
 #include "rnnt_device.hpp"
 #include "decoder.hpp"
-
-#ifndef DEC_TAIL3_ROWS
-#define DEC_TAIL3_ROWS 0  // default: four-launch steps throughout (three-launch steps measured slower)
-#endif
-#ifndef RNNT_DEC_EARLY_W
-#define RNNT_DEC_EARLY_W 0  // step kernels' weight slices issued behind the list loads (1) or the inputs (0)
-#endif
 
 namespace rnnt {
 
@@ -54,8 +44,8 @@ __device__ __forceinline__ int emit_entry(int row, int slot, int label) { return
 // The row goes through an opaque v_and: ROCm 7.2's AMDGPU backend miscompiles a 64-bit multiply
 // of (x & 0xffffff) by a constant that is not a power of two -- it matches a 24-bit multiply
 // (which ignores the high byte, so the mask is dropped as redundant) and then widens it to
-// v_mad_u64_u32, which multiplies all 32 bits: `base + (size_t)entry_row(e) * 1280` addressed
-// with the slot and label bits still in place (tools/probe/probe_mul24.hip; guarded by
+// v_mad_u64_u32, which multiplies all 32 bits: `base + (size_t)entry_row(e) * 1280` would be
+// addressed with the slot and label bits still in place (tools/probe/probe_mul24.hip; guarded by
 // tests/test_isa_lint.py).
 __device__ __forceinline__ int entry_row(int e) {
   int r;
@@ -98,8 +88,14 @@ __device__ unsigned int g_st_n;
 #define ST_FLUSH(kid, a0, a1, a2, a3)
 #endif
 
-// development bounds checks (-DRNNT_DEC_CHECK, tools/build_variants.sh): a failed check sets its
-// bit in g_dec_err and the access is skipped; in the shipping build every check is `true`
+// Workgroup barrier over LDS only: waits for this wave's LDS operations, not for its global loads
+// and stores (a __syncthreads fence waits for every outstanding memory operation: in the step
+// kernels that serialised the weight-slice loads behind the list / staging round trips and
+// drained each tile's global stores).  Uniform control flow only.
+// development bounds checks (-DRNNT_DEC_CHECK: the host emulation, tools/emu, and
+// tools/build_variants.sh): a failed check sets its bit in g_dec_err and the access is skipped.
+// In the shipping build every check is `true`, so a check may only ever wrap a bounds assertion,
+// never a condition the logic needs.
 #ifdef RNNT_DEC_CHECK
 __device__ unsigned int g_dec_err;
 __device__ __forceinline__ bool dec_ok(bool c, int bit) {
@@ -110,10 +106,6 @@ __device__ __forceinline__ bool dec_ok(bool c, int bit) {
 __device__ __forceinline__ constexpr bool dec_ok(bool, int) { return true; }
 #endif
 
-// Workgroup barrier over LDS only: waits for this wave's LDS operations, not for its global loads
-// and stores (a __syncthreads fence waits for every outstanding memory operation: in the step
-// kernels that serialised the weight-slice loads behind the list / staging round trips and
-// drained each tile's global stores).  Uniform control flow only.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // XCD-aware decomposition of a 1-D grid of 8 * X * Y8 workgroups into (column group x, row group
@@ -372,20 +364,11 @@ __global__ void __launch_bounds__(256) dec_reset_res_kernel(int32_t* __restrict_
 
 // One prediction LSTM layer for the listed rows (lstm_amx_bf16 cell): gates =
 // (b_ih + x.W_ih^T) + (b_hh + h.W_hh^T); c fp32, h bf16.  A workgroup (4 waves) owns 4 gate
-// tiles, one per wave, whose weight rows stay in registers for the launch (10 x 16 B per chain
-// per lane; layer 0's input half comes from the label table).  Every launch reloads its weights,
-// and one CU takes in only a few tens of GB/s, so the slice per workgroup is kept small (20-40
-// KB: in-kernel stamps showed 160-320 KB slices costing 12-20 us per launch).  Grid: x = 20 gate
-// groups, y = row groups striding over the emit list's tiles.
-//
-// The recurrent halves b_hh + h.W_hh^T depend only on the committed state, i.e. on the previous
-// candidate, so they are computed when that candidate is made, off the next emission's critical
-// path: every layer-1 launch also runs the W_hh0 chain over the new candidate's h0 (-> ah0) and
-// every G launch the W_hh1 chain over its h1 (-> ah1).  Layer 0 then runs only in a call's first
-// step (the joint runs the layer-0 cell of every later emission from the label table and ah0), and
-// layer 1 always takes its recurrent half from ah1 (a call's first step computes it from the
-// committed h1 first: dec_g_kernel<true>).  Each chain is the same instruction sequence wherever
-// it runs, so the results are bit-identical.
+// tiles, one per wave, whose W_hh (and, layer 1, W_ih) rows stay in registers for the launch
+// (10 x 16 B per chain per lane; layer 0's input half comes from the label table).  Every
+// launch reloads its weights, and one CU takes in only a few tens of GB/s, so the slice per
+// workgroup is kept small (20-40 KB: in-kernel stamps showed 160-320 KB slices costing 12-20 us
+// per launch).  Grid: x = 20 gate groups, y = row groups striding over the emit list's tiles.
 constexpr int PRED_THREADS = 256;  // 4 waves, one gate tile each: 40 KB of weights per workgroup
 // rows per workgroup iteration of the prediction / G kernels: 32 (two MFMA row tiles per weight
 // fragment) with 24 / 48 row groups -- isolated greedy 69.5 -> 66.7 ms per query vs 16 rows and
@@ -399,17 +382,11 @@ constexpr int G_ROW_GROUPS = 48;
 constexpr int JOINT_GROUPS = 512;
 
 // NW waves per workgroup (NW gate tiles; 4: 8-wave workgroups measured no faster)
-// HCH: this layer's recurrent chain b_hh + h.W_hh^T runs here over the committed h (always on
-// layer 0; on layer 1 in four-launch steps -- in three-launch steps it is ah1, precomputed).
-// AH0 (layer 1, three-launch steps): also the W_hh0 chain over the new candidate's h0 -> ah0.
-template <int LAYER, int NW, bool HCH, bool AH0>
+template <int LAYER, int NW>
 __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity) {
-  static_assert(LAYER == 1 || (HCH && !AH0), "layer 0 runs its own recurrent chain and no ah0");
   constexpr int PRED_THREADS = NW * 64;
-  constexpr int NT = 1;                 // gate tiles per wave
-  constexpr bool H_CHAIN = HCH;
-  // staged k: layer 0 [h0 committed]; layer 1 [h0 of the candidate | h1 committed (HCH)]
-  constexpr int KX = (LAYER && HCH) ? 2 * P : P;
+  constexpr int NT = 1;                  // gate tiles per wave
+  constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
   // bf16 pitch +32 B per row: every ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows c, 16-B
   // column q) lands on 16 distinct bank quads; the round-2 +16 B pitch put rows c and c+8 on the same
   // quads (2-way, 36-37 % of the LDS cycles of these kernels in the r02 PMC pass)
@@ -427,49 +404,22 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
   const int e0 = i0 < a.Npad ? list[i0] : -1;
   const int cnt = s.count[EMIT_N(parity)];
-  const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
-  // the weight slice (10 / 20 x 16 B per lane): by default issued after the first tile's input
-  // loads (vmcnt retires in order, so loads issued before the inputs would hold up the staging);
-  // RNNT_DEC_EARLY_W issues it right behind the list loads instead, so it lands while the entries
-  // and then the inputs make their round trips
-  uint4 wh[NT][H_CHAIN ? P / 32 : 1], wx[NT][LAYER ? P / 32 : 1], w0[NT][AH0 ? P / 32 : 1];
-  float4 bh[NT], bx[NT], b0[NT];
-  auto load_w = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) {
-      const int gr = (t0 + tt) * 16 + c;
-      const uint16_t* wr = a.w.wp[LAYER] + (size_t)gr * 640 + 8 * q;
-      if (H_CHAIN) {
-#pragma unroll
-        for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
-        bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
-      }
-      if (LAYER) {
-#pragma unroll
-        for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
-        bx[tt] = *(const float4*)(a.w.bih_p[1] + (t0 + tt) * 16 + 4 * q);
-      }
-      if (AH0) {
-        const uint16_t* w0r = a.w.wp[0] + (size_t)gr * 640 + P + 8 * q;  // W_hh0: the successor's ah0
-#pragma unroll
-        for (int b = 0; b < P / 32; ++b) w0[tt][b] = *(const uint4*)(w0r + 32 * b);
-        b0[tt] = *(const float4*)(a.w.bhh_p[0] + (t0 + tt) * 16 + 4 * q);
-      }
-    }
-  };
-  if (RNNT_DEC_EARLY_W) load_w();
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
+  const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
+  // the weight slice (10 / 20 x 16 B per lane) is issued after the first tile's input loads:
+  // vmcnt retires in order, so loads issued first would hold up the staging that needs the inputs
+  uint4 wh[NT][P / 32], wx[NT][LAYER ? P / 32 : 1];
+  float4 bh[NT], bx[NT];
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT)  // past the prefetched tiles (the slot's tile is done)
       ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 3) ? list[rt * DEC_RT + tid] : -1;
     lds_barrier();
     ST_MARK(st1);
-    // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and its precomputed
-    // gate halves (layer 0: the label table's input half; layer 1: ah1), fetched
-    // beside the input staging
+    // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and, layer 0, its
+    // label-table input halves, fetched beside the input staging
     float cp[DEC_SUB][NT];
     float4 xt[DEC_SUB][NT];
 #pragma unroll
@@ -481,12 +431,10 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
         cp[st][tt] = ec >= 0 ? hc_part(a.hc, entry_row(ec), entry_slot(ec), 2 + LAYER)[(t0 + tt) * 4 + q] : 0.0f;
         if (!LAYER)
           xt[st][tt] = *(const float4*)(a.w.xtab + (size_t)(ec >= 0 ? entry_label(ec) : 28) * PG4 + (t0 + tt) * 16 + 4 * q);
-        else if (!HCH)
-          xt[st][tt] = *(const float4*)(a.ah1 + (size_t)(ec >= 0 ? entry_row(ec) : 0) * PG4 + (t0 + tt) * 16 + 4 * q);
       }
     }
-    // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1 [h0 of the
-    // candidate slot | h1 committed (HCH)]
+    // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1
+    // [h0 of the candidate slot | h1 committed]
     // every load of the tile first (one memory round trip); entries past the list end read row
     // 0 (a safe cached address) and stage zeros
     constexpr int NX = DEC_RT * (KX / 8), NIT = (NX + PRED_THREADS - 1) / PRED_THREADS;
@@ -509,7 +457,20 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
-    if (!RNNT_DEC_EARLY_W && it == 0) load_w();
+    if (it == 0) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        const uint16_t* wr = a.w.wp[LAYER] + (size_t)((t0 + tt) * 16 + c) * 640 + 8 * q;
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
+        if (LAYER) {
+#pragma unroll
+          for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
+          bx[tt] = *(const float4*)(a.w.bih_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+        }
+        bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int i = tid + PRED_THREADS * u;
@@ -520,32 +481,26 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     }
     lds_barrier();
     ST_MARK(st2);
-    // the chains of every sub-tile advance together, one k block at a time, so each block's
-    // fragment reads overlap the previous block's MFMAs (sub-tiles past the list end run on the
-    // staged zeros; their results are not stored).  Each chain is still the contract's natural-k
-    // sequence from its bias.
+    // the chains of every sub-tile (h, and x on layer 1) advance together, one k block at a
+    // time, so each block's fragment reads overlap the previous block's MFMAs (sub-tiles past the
+    // list end run on the staged zeros; their results are not stored).  Each chain is still the
+    // contract's natural-k sequence from its bias.
     static_assert(NT == 1, "one gate tile per wave");
     int ecs[DEC_SUB];
-    v4f ahs[DEC_SUB], axs[DEC_SUB], a0s[DEC_SUB];
+    v4f ahs[DEC_SUB], axs[DEC_SUB];
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       ecs[st] = ents[16 * st + c];
-      if (H_CHAIN) ahs[st] = v4f{bh[0].x, bh[0].y, bh[0].z, bh[0].w};
-      else ahs[st] = v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
+      ahs[st] = v4f{bh[0].x, bh[0].y, bh[0].z, bh[0].w};
       axs[st] = LAYER ? v4f{bx[0].x, bx[0].y, bx[0].z, bx[0].w} : v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
-      if (AH0) a0s[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
     }
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) {
 #pragma unroll
       for (int st = 0; st < DEC_SUB; ++st) {
         const uint16_t* xr = &X[16 * st + c][8 * q];
-        if (H_CHAIN) ahs[st] = mfma_bf16(wh[0][H_CHAIN ? b : 0], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ahs[st]);
-        if (LAYER) {
-          const uint4 xf = *(const uint4*)(xr + 32 * b);
-          axs[st] = mfma_bf16(wx[0][LAYER ? b : 0], xf, axs[st]);
-          if (AH0) a0s[st] = mfma_bf16(w0[0][AH0 ? b : 0], xf, a0s[st]);
-        }
+        ahs[st] = mfma_bf16(wh[0][b], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ahs[st]);
+        if (LAYER) axs[st] = mfma_bf16(wx[0][LAYER ? b : 0], *(const uint4*)(xr + 32 * b), axs[st]);
       }
     }
 #pragma unroll
@@ -563,10 +518,6 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
           const float hh = bf_round_ftz(og * det_tanh(cn));
           hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
           h_bf(a.hc, row, sl ^ 1, LAYER)[u] = (uint16_t)(__float_as_uint(hh) >> 16);  // hh is bf16-exact
-          if (AH0) {
-            const v4f h0 = a0s[st];
-            *(float4*)(a.ah0 + (size_t)row * PG4 + (t0 + tt) * 16 + 4 * q) = float4{h0[0], h0[1], h0[2], h0[3]};
-          }
         }
       }
     }
@@ -575,24 +526,12 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   }
 }
 
-// G = b_p + g . W1p^T for the listed rows' new candidates (MODE G_ONLY: four-launch steps) and
-// beside it their successors' layer-1 recurrent half ah1 = b_hh1 + h1.W_hh1^T (MODE G_AH1:
-// three-launch steps; same staged input, see dec_pred_kernel).  MODE AH_LIVE (the step that
-// switches to three launches): no G, but ah0 = b_hh0 + h0.W_hh0^T and ah1 of the current
-// candidate of every row of the LIVE list -- candidates made in four-launch steps have none.
-// Workgroups of 4 waves, one 16-column tile (10 KB of W1p, W_hh0 or W_hh1) per wave in registers:
-// grid x = the column groups (8 G, 20 ah0, 20 ah1 as the mode has them), y = row groups striding
-// over the list's tiles.  The G modes also clear the next step's emit and live lists for the joint
+// G = b_p + g . W1p^T for the listed rows' new candidates.  Workgroups of 4 waves, one 16-column
+// tile (10 KB of W1p) per wave in registers: grid x = 8 column groups, y = row groups striding
+// over the emit list's tiles.  Also clears the next step's emit and live lists for the joint
 // that follows.
 constexpr int GXP = P + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
-constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each
-constexpr int G_GROUPS = J / (16 * (G_THREADS / 64));        // 8
-constexpr int AH1_GROUPS = PG4 / (16 * (G_THREADS / 64));    // 20
-enum { G_ONLY = 0, G_AH1 = 1, AH_LIVE = 2 };
-__host__ __device__ constexpr int g_cols(int mode) {
-  return mode == G_ONLY ? G_GROUPS : mode == G_AH1 ? G_GROUPS + AH1_GROUPS : 2 * AH1_GROUPS;
-}
-template <int MODE>
+constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each; grid x = 8 column groups
 __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
   constexpr int NK = G_THREADS / DEC_RT;  // row tiles whose list entries load up front
@@ -600,43 +539,24 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
-  constexpr int NG = MODE == AH_LIVE ? 0 : G_GROUPS;  // G column groups, then ah0 groups, then ah1 groups
-  constexpr int NA0 = MODE == AH_LIVE ? AH1_GROUPS : 0;
-  const GridXY gxy = xcd_grid(g_cols(MODE));
-  if (MODE != AH_LIVE && blockIdx.x == 0 && tid == 0) {
+  const GridXY gxy = xcd_grid(J / (16 * (G_THREADS / 64)));
+  if (blockIdx.x == 0 && tid == 0) {
     s.count[EMIT_N(parity ^ 1)] = 0;
     s.count[LIVE_N(parity ^ 1)] = 0;
   }
-  // entries: the emit list, or (AH_LIVE) the live list's first words, whose row / slot bits are
-  // laid out as an emit entry's
-  auto entry = [&](int i) __attribute__((always_inline)) -> int {
-    return MODE == AH_LIVE ? s.live[parity * a.Npad + i].x : s.list[parity * a.Npad + i];
-  };
+  const int* list = s.list + parity * a.Npad;
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
-  const int e0 = i0 < a.Npad ? entry(i0) : -1;
-  const int cnt = s.count[MODE == AH_LIVE ? LIVE_N(parity) : EMIT_N(parity)];
-  // this wave's 16 output columns: a G column tile, an ah0 or an ah1 gate tile (workgroup-uniform)
-  const int kind = gxy.x < NG ? 0 : gxy.x < NG + NA0 ? 1 : 2;  // 0: G, 1: ah0, 2: ah1
-  const int jt = (gxy.x - (kind == 0 ? 0 : kind == 1 ? NG : NG + NA0)) * (G_THREADS / 64) + wave;
-  float* const out = kind == 0 ? a.G : kind == 1 ? a.ah0 : a.ah1;
-  const int ostride = kind == 0 ? J : PG4;
-  const int hl = kind == 1 ? 0 : 1;  // staged layer: h0 for ah0, h1 otherwise
-  uint4 wv[P / 32];  // issued after the first tile's input loads, or early (see dec_pred_kernel)
-  float4 b0;
-  auto load_w = [&]() __attribute__((always_inline)) {
-    const uint16_t* w0 = kind == 0 ? a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q
-                                   : a.w.wp[hl] + (size_t)(jt * 16 + c) * 640 + P + 8 * q;
-#pragma unroll
-    for (int b = 0; b < P / 32; ++b) wv[b] = *(const uint4*)(w0 + 32 * b);
-    b0 = *(const float4*)((kind == 0 ? a.w.bp : a.w.bhh_p[hl]) + jt * 16 + 4 * q);
-  };
-  if (RNNT_DEC_EARLY_W) load_w();
+  const int e0 = i0 < a.Npad ? list[i0] : -1;
+  const int cnt = s.count[EMIT_N(parity)];
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
+  constexpr int NJ = 1;  // column tiles per wave
+  uint4 wv[NJ][P / 32];  // issued after the first tile's input loads (see dec_pred_kernel)
+  float4 b0[NJ];
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
-    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? entry(rt * DEC_RT + tid) : -1;
+    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? list[rt * DEC_RT + tid] : -1;
     lds_barrier();
     ST_MARK(st1);
     constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
@@ -653,11 +573,20 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       if (NX % G_THREADS == 0 || i < NX) {
         const int k = (i % (P / 8)) * 8, em = emv[u];
         const bool okr = em >= 0 && dec_ok(entry_row(em) < a.Npad, 4);
-        xv[u] = *(const uint4*)(h_bf(a.hc, okr ? entry_row(em) : 0, okr ? entry_slot(em) ^ 1 : 0, hl) + k);
+        xv[u] = *(const uint4*)(h_bf(a.hc, okr ? entry_row(em) : 0, okr ? entry_slot(em) ^ 1 : 0, 1) + k);
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
-    if (!RNNT_DEC_EARLY_W && it == 0) load_w();
+    if (it == 0) {
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
+        const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
+#pragma unroll
+        for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
+        b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
       const int i = tid + G_THREADS * u;
@@ -669,20 +598,22 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     lds_barrier();
     ST_MARK(st2);
     // every sub-tile's chain advances one k block at a time (fragment reads overlap MFMAs)
+    static_assert(NJ == 1, "one column tile per wave");
     v4f accs[DEC_SUB];
 #pragma unroll
-    for (int st = 0; st < DEC_SUB; ++st) accs[st] = v4f{b0.x, b0.y, b0.z, b0.w};
+    for (int st = 0; st < DEC_SUB; ++st) accs[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
 #pragma unroll
     for (int b = 0; b < P / 32; ++b)
 #pragma unroll
       for (int st = 0; st < DEC_SUB; ++st)
-        accs[st] = mfma_bf16(wv[b], *(const uint4*)(&X[16 * st + c][8 * q] + 32 * b), accs[st]);
+        accs[st] = mfma_bf16(wv[0][b], *(const uint4*)(&X[16 * st + c][8 * q] + 32 * b), accs[st]);
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ents[16 * st + c];
       const v4f acc = accs[st];
-      if (ec >= 0 && dec_ok(entry_row(ec) < a.Npad && jt < (kind == 0 ? J / 16 : PG4 / 16), 5))
-        *(float4*)(out + (size_t)entry_row(ec) * ostride + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
+      const int jt = gxy.x * (G_THREADS / 64) + wave;
+      if (ec >= 0 && dec_ok(entry_row(ec) < a.Npad, 5))
+        *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
     }
     lds_barrier();
     ST_FLUSH(2, st0, st1, st2, 0ull);
@@ -700,14 +631,11 @@ constexpr int JOINT_ITERS = 2;  // 1 / 3 / 4 measured slower (DESIGN.md section 
 
 constexpr int YP = J + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
 constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 waves x 4 rows x 16 lanes onto it
-// L0CELL (three-launch steps): also layer 0 of every emitting row's new candidate (see below)
-template <bool L0CELL>
 __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   __shared__ __attribute__((aligned(16))) uint16_t X[JRT][YP];
   __shared__ float Lp[4][JRT][NLAB_PAD + 1];
   __shared__ int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT];
   __shared__ int slot_[JRT], add_[JRT], flen_[JRT], idx_[JRT];
-  __shared__ int em_m[JRT], em_n;  // the tile's emitting rows (tile indices), compacted
   DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
@@ -885,61 +813,19 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
       const int r = lane < JRT ? rows[lane] : -1;
       const unsigned long long me = __ballot(e >= 0), mr = __ballot(r >= 0);
       unsigned long long base = 0;
-      if (lane == 0) dec_ok(false, 31);  // ran
       if (lane == 0 && (me | mr))
         base = atomicAdd((unsigned long long*)&s.count[EMIT_N(parity ^ 1)],
                          (unsigned long long)__popcll(me) | ((unsigned long long)__popcll(mr) << 32));
       base = __shfl(base, 0);
       const unsigned long long below = (1ull << lane) - 1;
-      if (e >= 0 && dec_ok((int)(base & 0xffffffffu) + __popcll(me & below) < a.Npad, 9)) {
+      if (lane == 0) dec_ok(false, 31);  // ran (the emulator's check that the joint executed)
+      if (e >= 0 && dec_ok((int)(base & 0xffffffffu) + __popcll(me & below) < a.Npad, 9))
         s.list[(parity ^ 1) * a.Npad + (int)(base & 0xffffffffu) + __popcll(me & below)] = e;
-        em_m[__popcll(me & below)] = lane;
-      }
       if (r >= 0 && dec_ok((int)(base >> 32) + __popcll(mr & below) < a.Npad, 10))
         nlist[(int)(base >> 32) + __popcll(mr & below)] =
             live_entry(r, slot_[lane], add_[lane], tidx[lane], flen_[lane], idx_[lane]);
-      if (lane == 0) em_n = __popcll(me);
     }
-    lds_barrier();
-    // layer 0 of every emitting row's new candidate, here instead of in a launch of its own: its
-    // gates are the label table's input half plus ah0, the committed h0's recurrent half computed
-    // when that state was made (dec_pred_kernel), so the cell is all that is left -- the same
-    // cell as dec_pred_kernel's, written to the candidate slot for the next step's layer 1.
-    if (L0CELL) {
-      const int ne = em_n;
-      for (int ib = 0; ib < ne * P; ib += 4 * 256) {
-        float4 xa[4], ha[4];
-        float cv[4];
-        int rw[4], sl[4], uu[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {  // every load of the round first
-          const int i = ib + 256 * v + tid;
-          rw[v] = -1;
-          const int mi = i < ne * P ? em_m[i / P] : -1;
-          const int e = mi >= 0 && dec_ok(mi < JRT, 11) ? emit_e[mi] : -1;
-          if (i < ne * P && dec_ok(e >= 0 && entry_row(e) < a.Npad && entry_label(e) < 28, 12)) {
-            const int u = i % P, row = entry_row(e), nsl = entry_slot(e);
-            rw[v] = row;
-            sl[v] = nsl;
-            uu[v] = u;
-            xa[v] = *(const float4*)(a.w.xtab + (size_t)entry_label(e) * PG4 + 4 * u);
-            ha[v] = *(const float4*)(a.ah0 + (size_t)row * PG4 + 4 * u);
-            cv[v] = hc_part(a.hc, row, nsl, 2)[u];
-          }
-        }
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          if (rw[v] < 0) continue;
-          const float4 gs = float4{xa[v].x + ha[v].x, xa[v].y + ha[v].y, xa[v].z + ha[v].z, xa[v].w + ha[v].w};
-          const float ig = det_sigmoid(gs.x), fg = det_sigmoid(gs.y), gg = det_tanh(gs.z), og = det_sigmoid(gs.w);
-          const float cn = fg * cv[v] + ig * gg;
-          const float hh = bf_round_ftz(og * det_tanh(cn));
-          hc_part(a.hc, rw[v], sl[v] ^ 1, 2)[uu[v]] = cn;
-          h_bf(a.hc, rw[v], sl[v] ^ 1, 0)[uu[v]] = (uint16_t)(__float_as_uint(hh) >> 16);  // hh is bf16-exact
-        }
-      }
-    }
-    lds_barrier();  // rows / walking / tidx / X / em_m are reused by the next row tile
+    lds_barrier();  // rows / walking / tidx / X are reused by the next row tile
     ST_FLUSH(3, st0, st1, st2, 0ull);
   }
 }
@@ -949,25 +835,11 @@ __global__ void dec_finish_kernel(DecArgs a) {
   if (row < a.N) a.res_len[row] = a.s.idx[row] + 1;
 }
 
-// Step structure by live rows: with many live rows the four-launch step (layer 0 -> layer 1 -> G
-// -> joint) is cheaper -- the three-launch step's precomputed recurrent halves cost 2 x 5 KB of
-// fp32 written and read back per emission, which the early steps' thousands of emissions pay in
-// bandwidth; with few, the three-launch step (layer 1 + ah0 -> G + ah1 -> joint + layer-0 cell)
-// saves a dependent launch.  Rows at or below which the three-launch step runs: RNNT_DEC_TAIL3_ROWS
-// (0: never, a large value: from the first step).
-static int dec_tail3_rows() {
-  static const int v = [] {
-    const char* e = getenv("RNNT_DEC_TAIL3_ROWS");
-    return e ? atoi(e) : DEC_TAIL3_ROWS;
-  }();
-  return v;
-}
-
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st, const int32_t* reset) {
   // every buffer the step kernels address (a missing one is a host error here, not a GPU fault)
-  const void* need[] = {a.F, a.f_lens, a.hc, a.G, a.ah0, a.ah1, a.res, a.res_len, a.w.xtab, a.w.wp[0], a.w.wp[1],
-                        a.w.bih_p[1], a.w.bhh_p[0], a.w.bhh_p[1], a.w.w1p, a.w.bp, a.w.w2, a.w.b2, a.s.time,
-                        a.s.added, a.s.idx, a.s.preg, a.s.slot, a.s.fin, a.s.list, a.s.live, a.s.count};
+  const void* need[] = {a.F, a.f_lens, a.hc, a.G, a.res, a.res_len, a.w.xtab, a.w.wp[0], a.w.wp[1], a.w.bih_p[1],
+                        a.w.bhh_p[0], a.w.bhh_p[1], a.w.w1p, a.w.bp, a.w.w2, a.w.b2, a.s.time, a.s.added, a.s.idx,
+                        a.s.preg, a.s.slot, a.s.fin, a.s.list, a.s.live, a.s.count};
   for (const void* p : need)
     if (!p) return -1;
   if (a.Npad % DEC_RT || a.N > a.Npad || a.Npad >= (1 << 24)) return -1;
@@ -982,15 +854,13 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   }
   // Steps are enqueued in chunks and the host reads the live count one chunk behind, so a decode
   // ends with the rest of the chunk holding its last step plus one more chunk of (cheap, but still
-  // ~15-20 us each: three dependent launches) empty steps.  Once few rows are left -- the long-tail
+  // ~20 us each: four dependent launches) empty steps.  Once few rows are left -- the long-tail
   // rows whose last emission ends the loop -- chunks shrink to 8 steps: the overshoot falls from
   // ~48 to ~12 steps while the host (~3.5 us per launch) still stays ahead of the GPU.
   constexpr int CHUNK = 32, TAIL_CHUNK = 8, TAIL_ROWS = 64;
   int step = 0, chunk = 0;
   int live_bound = a.N;  // unfinished rows at the end of the last chunk read back (an upper bound)
   bool done = false;
-  bool mode3 = false;    // the steps so far run three launches (see below)
-  const int tail3 = dec_tail3_rows();
   while (!done && step < a.max_iter) {
     const int csz = live_bound > TAIL_ROWS ? CHUNK : TAIL_CHUNK;
     // row-tile workgroups per launch: one resident round, and no more than the live rows need
@@ -1000,38 +870,15 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_g = lt1 < G_ROW_GROUPS ? lt1 : G_ROW_GROUPS;
     const int ljt = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
     const int rg_joint = ljt < JOINT_GROUPS ? ljt : JOINT_GROUPS;
-    // step structure of this chunk: four launches while many rows are live, three once at most
-    // tail3 rows are (the host's bound, one chunk behind); the switch is one way
-    const bool want3 = live_bound <= tail3;
     for (int i = 0; i < csz && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      const dim3 pgrid(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred));
-      if (step == 0 || !mode3) {
-        // layer 0 runs as its own launch: a call's first step (every live row's first prediction,
-        // emit list from dec_init*) and every four-launch step.  On the step that switches to three
-        // launches, the candidates made by earlier four-launch steps get their ah0 / ah1 first.
-        if (want3 && step > 0) {
-          const int ljt = (live_bound + DEC_RT - 1) / DEC_RT > 0 ? (live_bound + DEC_RT - 1) / DEC_RT : 1;
-          const int rg_ah = ljt < G_ROW_GROUPS ? ljt : G_ROW_GROUPS;
-          hipLaunchKernelGGL((dec_g_kernel<AH_LIVE>), dim3(xcd_grid_size(g_cols(AH_LIVE), rg_ah)), dim3(G_THREADS), 0, st,
-                             a, p);
-        }
-        hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64, true, false>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
-        if (want3)
-          hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64, true, true>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
-        else
-          hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64, true, false>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
-        mode3 = want3;
-      } else {
-        hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64, false, true>), pgrid, dim3(PRED_THREADS), 0, st, a, p);
-      }
-      if (mode3) {
-        hipLaunchKernelGGL((dec_g_kernel<G_AH1>), dim3(xcd_grid_size(g_cols(G_AH1), rg_g)), dim3(G_THREADS), 0, st, a, p);
-        hipLaunchKernelGGL(dec_joint_kernel<true>, dim3(rg_joint), dim3(256), 0, st, a, p);
-      } else {
-        hipLaunchKernelGGL((dec_g_kernel<G_ONLY>), dim3(xcd_grid_size(g_cols(G_ONLY), rg_g)), dim3(G_THREADS), 0, st, a, p);
-        hipLaunchKernelGGL(dec_joint_kernel<false>, dim3(rg_joint), dim3(256), 0, st, a, p);
-      }
+      hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                         dim3(PRED_THREADS), 0, st, a, p);
+      hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                         dim3(PRED_THREADS), 0, st, a, p);
+      hipLaunchKernelGGL(dec_g_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), rg_g)), dim3(G_THREADS), 0, st, a,
+                         p);
+      hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
     }
     // poll the live-row count one chunk behind, so the host never drains the queue: the length of
     // the live list the chunk's last joint wrote (parity step & 1; the next step's G kernel resets
@@ -1078,15 +925,6 @@ int launch_dec_xtab(const DecWeights& w, float* xtab, hipStream_t st) {
 
 }  // namespace rnnt
 
-#ifdef RNNT_DEC_CHECK
-extern "C" int rnnt_dev_read_dec_err(unsigned int* out) {
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_dec_err), sizeof(unsigned int)) != hipSuccess) return -1;
-  const unsigned int z = 0;
-  return hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_dec_err), &z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif
-
 #ifdef RNNT_DEV_STAMPS
 // development: copy out (and reset) the step kernels' stamp records (6 x u64 each)
 extern "C" int rnnt_dev_read_stamps(unsigned long long* out, int max_records) {
@@ -1098,5 +936,14 @@ extern "C" int rnnt_dev_read_stamps(unsigned long long* out, int max_records) {
   const unsigned int z = 0;
   if (hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_st_n), &z, sizeof(z)) != hipSuccess) return -1;
   return (int)n;
+}
+#endif
+
+#ifdef RNNT_DEC_CHECK
+extern "C" int rnnt_dev_read_dec_err(unsigned int* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_dec_err), sizeof(unsigned int)) != hipSuccess) return -1;
+  const unsigned int z = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_dec_err), &z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

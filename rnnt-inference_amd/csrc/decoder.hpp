@@ -35,12 +35,6 @@ struct DecArgs {
   const int32_t* f_lens;   // [Npad]
   float* hc;               // [Npad][2 slots][4][320] (h0, h1, c0, c1) prediction state
   float* G;                // [Npad][512] joint pred half of the current candidate
-  // recurrent halves b_hh + h.W_hh^T of the current candidate's h0 / h1 ([Npad][1280] fp32,
-  // gate-interleaved): the halves its successor's gates need once it is committed, computed off
-  // the step's critical path (ah0 in the layer-1 launch, ah1 in the G launch) so the joint can run
-  // layer 0's cell itself at an emission
-  float* ah0;
-  float* ah1;
   int32_t* res;            // [N][max_res]
   int32_t* res_len;        // [N]
   DecState s;

@@ -64,7 +64,6 @@ struct rnnt_engine {
   uint16_t* c[5] = {};
   uint16_t* fbf = nullptr;
   float *F = nullptr, *hc = nullptr, *G = nullptr;
-  float *ah0 = nullptr, *ah1 = nullptr;  // the decode's precomputed recurrent halves (DecArgs::ah0 / ah1)
   int32_t* flen = nullptr;
   DecState ds{};
   int32_t* host_flags = nullptr;
@@ -338,8 +337,6 @@ static int alloc_workspace(rnnt_engine* e) {
   r = r ? r : dev_alloc(e, &e->F, TPM * NP * J);
   r = r ? r : dev_alloc(e, &e->hc, NP * 2 * 4 * P);
   r = r ? r : dev_alloc(e, &e->G, NP * J);
-  r = r ? r : dev_alloc(e, &e->ah0, NP * PG4);
-  r = r ? r : dev_alloc(e, &e->ah1, NP * PG4);
   r = r ? r : dev_alloc(e, &e->flen, NP);
   int32_t** ints[] = {&e->ds.time, &e->ds.added, &e->ds.idx, &e->ds.preg, &e->ds.slot, &e->ds.fin};
   for (auto pp : ints) r = r ? r : dev_alloc(e, pp, NP);
@@ -918,8 +915,6 @@ static int decode_core(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
   a.f_lens = flen;
   a.hc = e->hc;
   a.G = e->G;
-  a.ah0 = e->ah0;
-  a.ah1 = e->ah1;
   a.res = res;
   a.res_len = res_len;
   a.N = n;

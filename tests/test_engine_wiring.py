@@ -2,8 +2,9 @@
 
 The step kernels read their buffers from DecArgs / DecWeights / DecState (csrc/decoder.hpp); the
 engine fills those structs (csrc/engine.hip).  A member the kernels use but the engine never sets
-stays null on the GPU and faults the card -- round 4's first GPU run of the three-launch decode
-did exactly that (DecArgs::ah0 / ah1 added to the kernels, never allocated by the engine), and the
+stays null on the GPU and faults the card -- round 4's first GPU run of the (since removed)
+three-launch decode did exactly that (DecArgs::ah0 / ah1 added to the kernels, never allocated by
+the engine), and the
 host emulation (tools/emu) could not see it because its harness allocates the structs itself.
 This test parses the structs and requires, for every pointer member, an assignment in the engine
 (DecArgs: `a.<m> =`; DecState: allocated through `&e->ds.<m>`; DecWeights: `dw.<m>` set).  The
@@ -36,7 +37,7 @@ def test_decode_structs_are_fully_wired_by_the_engine():
     eng = open(os.path.join(CSRC, "engine.hip")).read()
     args = _struct_pointers(hpp, "DecArgs")
     names = {n for n, _ in args}
-    assert {"F", "hc", "G", "ah0", "ah1", "res"} <= names, names
+    assert {"F", "hc", "G", "res", "res_len"} <= names, names
     missing = [n for n, _ in args if not re.search(r"\ba\.%s\s*=" % n, eng)]
     assert not missing, f"DecArgs members never set in engine.hip: {missing}"
     state = _struct_pointers(hpp, "DecState")
