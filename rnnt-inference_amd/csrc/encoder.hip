@@ -443,8 +443,18 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
 // activation tiles through its L2 (weights fetched from HBM/MALL 2x, activations 4x per tick,
 // instead of 1x / 8x).  Batch tiles of a job: its active 128-row tiles in the tile's rows.
 template <class C>
-__device__ __forceinline__ int job_tiles(const EncTickArgs& args, int j) {
+__host__ __device__ __forceinline__ int job_tiles(const EncTickArgs& args, int j) {
+  if (args.bmask[j]) return __builtin_popcountll(enc_tile_mask(args.bmask[j], C::BN));
   return C::BN == 256 ? (args.nbt[j] + 1) >> 1 : args.nbt[j];
+}
+// batch tile of compact index i (0 .. job_tiles - 1): the i-th active tile
+template <class C>
+__device__ __forceinline__ int job_tile(const EncTickArgs& args, int j, int i) {
+  uint64_t m = args.bmask[j];
+  if (!m) return i;
+  m = enc_tile_mask(m, C::BN);
+  for (; i > 0; --i) m &= m - 1;  // drop the i lowest set bits
+  return __builtin_ctzll(m);
 }
 // job tile k (0..) of XCD xcd -> (mt, nt); -1 past the XCD's last tile.  A job with ONE batch tile
 // (small batches: config 3, short Server rounds, the tail of a sorted batch) spreads its gate tiles
@@ -458,7 +468,7 @@ __device__ __forceinline__ int xcd_pick(const EncTickArgs& args, int xcd, int k,
       constexpr int G8 = C::NGT / 8;
       if (k < G8) {
         mt = xcd * G8 + k;
-        nt = 0;
+        nt = job_tile<C>(args, j, 0);
         return j;
       }
       k -= G8;
@@ -469,7 +479,7 @@ __device__ __forceinline__ int xcd_pick(const EncTickArgs& args, int xcd, int k,
     const int cnt = C::GPX * (b1 - b0);
     if (k < cnt) {
       mt = gsel * C::GPX + k % C::GPX;
-      nt = b0 + k / C::GPX;
+      nt = job_tile<C>(args, j, b0 + k / C::GPX);
       return j;
     }
     k -= cnt;
@@ -634,7 +644,7 @@ template <class C>
 static int tick_grid(const EncTickArgs& a) {  // workgroups: 8 XCDs x the batch-half-0 XCDs' (larger) share
   int per_xcd = 0;
   for (int j = 0; j < a.njobs; ++j) {
-    const int nbt = C::BN == 256 ? (a.nbt[j] + 1) / 2 : a.nbt[j];
+    const int nbt = job_tiles<C>(a, j);
     per_xcd += nbt == 1 ? C::NGT / 8 : C::GPX * ((nbt + 1) / 2);  // as xcd_pick
   }
   return 8 * per_xcd;
@@ -650,7 +660,7 @@ static int launch_tick(const EncTickArgs& a, int grid, hipStream_t st) {
 int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st, int forced) {
   // shapes the kernel's staging assumes (checked on the host: a mismatch would read out of bounds)
   for (int j = 0; j < a.njobs; ++j)
-    if (a.job[j].I % 128 != 0 || a.nbt[j] < 0) return -1;
+    if (a.job[j].I % 128 != 0 || a.nbt[j] < 0 || (a.bmask[j] && __builtin_popcountll(a.bmask[j]) != a.nbt[j])) return -1;
   const int gb = tick_grid<BigTile>(a), gs = tick_grid<SmallTile>(a), gm = tick_grid<MiniTile>(a);
   if (gb <= 0) return 0;
   int choice = forced == ENC_TILE_FLOW || forced == ENC_TILE_TICKS ? ENC_TILE_AUTO : forced;  // (flow: engine-level)

@@ -47,8 +47,20 @@ constexpr int ENC_MAX_JOBS = 5;
 struct EncTickArgs {
   EncStepArgs job[ENC_MAX_JOBS];
   int nbt[ENC_MAX_JOBS];  // active 128-row batch tiles per job (leading tiles holding a row still running)
+  // bmask[j] != 0: the job's active 128-row tiles are the set bits (any subset of the first 64
+  // tiles; nbt[j] = its popcount) instead of the leading nbt[j] -- the Server's unsorted slots,
+  // where a tile whose rows are all done in this chunk is skipped wherever it sits
+  uint64_t bmask[ENC_MAX_JOBS];
   int njobs;
 };
+// the job's active batch tiles of a BN-row tile shape (BN = 128 or 256) as a mask over those tiles
+__host__ __device__ inline uint64_t enc_tile_mask(uint64_t m128, int BN) {
+  if (BN == 128) return m128;
+  uint64_t m = 0;  // 256-row tile k = 128-row tiles 2k, 2k+1
+  for (int k = 0; k < 32; ++k)
+    if ((m128 >> (2 * k)) & 3ull) m |= 1ull << k;
+  return m;
+}
 
 int launch_quantize(const float* feat, int64_t n, float s, int8_t* out, hipStream_t st);
 // AssembleSamples + the layer-0 input quantizer in one pass: row i of the batch is the QSL sample

@@ -52,6 +52,7 @@ struct rnnt_engine {
   rnnt_opts opts{};
   int np_max = 0, tp_max = 0;
   int tile = ENC_TILE_AUTO;  // tick tile shape / flow (rnnt_engine_set_tile; RNNT_ENC_TILE at create)
+  bool stream_prefix = false;  // stream chunks skip only trailing done tiles (RNNT_STREAM_PREFIX=1: A/B)
   // packed weights
   int8_t* enc_w[5] = {};
   float* enc_bq[5] = {};
@@ -425,6 +426,10 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
     if (v < 0) r = fail(RNNT_EINVAL, std::string("RNNT_ENC_TILE=") + t + ": auto|ticks|flow|big|small|tiny|mini");
     e->tile = v < 0 ? ENC_TILE_AUTO : v;
   }
+  {
+    const char* sp = getenv("RNNT_STREAM_PREFIX");
+    e->stream_prefix = sp && atoi(sp) != 0;
+  }
   if (!r && model) r = pack_model(e, model);
   if (!r) r = alloc_workspace(e);
   if (r) {
@@ -595,17 +600,22 @@ static EncStepArgs make_job(rnnt_engine* e, int l, int t, int n_pad, const int8_
 struct TickBuilder {
   EncTickArgs args{};
   int n = 0;
-  void add(const EncStepArgs& a, int tiles) {
+  // tiles: the job's active 128-row batch tiles, the leading `tiles` ones, or (mask != 0) the set
+  // bits of mask
+  void add(const EncStepArgs& a, int tiles, uint64_t mask = 0) {
+    if (mask) tiles = __builtin_popcountll(mask);
     if (tiles <= 0) return;
     // keep jobs ordered by K descending (longest workgroups dispatched first)
     int p = n++;
     while (p > 0 && args.job[p - 1].I < a.I) {
       args.job[p] = args.job[p - 1];
       args.nbt[p] = args.nbt[p - 1];
+      args.bmask[p] = args.bmask[p - 1];
       --p;
     }
     args.job[p] = a;
     args.nbt[p] = tiles;
+    args.bmask[p] = mask;
   }
   int launch(rnnt_engine* e, hipStream_t st) {
     if (n == 0) return 0;
@@ -819,22 +829,34 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
   // their inputs exist.  Every job of a tick is independent (inputs come from earlier ticks).
   const int nt_all = n_pad / ENC_ROW_TILE;
   auto tiles = [&](int thr) { return tm.empty() ? nt_all : active_tiles(tm, thr); };
+  // stream chunks (unsorted slots): the tick skips every 128-row tile whose rows are all done at
+  // this frame, not only a trailing run of them (a mask over at most 64 tiles; the set of active
+  // tiles only shrinks with the frame, so a skipped tile's rows are finished for this call)
+  const bool use_mask = reset != nullptr && !tm.empty() && nt_all <= 64 && !e->stream_prefix;
+  auto tmask = [&](int thr) -> uint64_t {
+    uint64_t m = 0;
+    if (use_mask)
+      for (int i = 0; i < nt_all; ++i)
+        if (tm[i] > thr) m |= 1ull << i;
+    return m;
+  };
   const int n_ticks = flow_wanted(e, n_pad) ? 0 : std::max(T + 1, 2 * Tp + 4);
   if (!n_ticks && (r = run_flow(e, T, n_pad, lens, f_out, tiles, st))) return r;
   for (int tau = 0; tau < n_ticks; ++tau) {
     TickBuilder tb;
-    if (tau < T) tb.add(make_job(e, 0, tau, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, lens, T), tiles(2 * (tau / 2)));
+    if (tau < T)
+      tb.add(make_job(e, 0, tau, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, lens, T), tiles(2 * (tau / 2)), tmask(2 * (tau / 2)));
     if (tau >= 1 && tau - 1 < T) {
       const int t = tau - 1;
-      tb.add(make_job(e, 1, t, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, lens, T), tiles(2 * (t / 2)));
+      tb.add(make_job(e, 1, t, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, lens, T), tiles(2 * (t / 2)), tmask(2 * (t / 2)));
     }
     for (int l = 2; l < 5; ++l) {
       const int d = tau - (l + 1);  // = 2t'
       if (d >= 0 && (d & 1) == 0 && d / 2 < Tp) {
         const int tp = d / 2;
-        if (l == 2) tb.add(make_job(e, 2, tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, lens, T), tiles(2 * tp));
-        if (l == 3) tb.add(make_job(e, 3, tp, n_pad, e->yB, ENC_OUT_I8, e->yC, nullptr, lens, T), tiles(2 * tp));
-        if (l == 4) tb.add(make_job(e, 4, tp, n_pad, e->yC, ENC_OUT_FINAL, e->fbf, f_out, lens, T), tiles(2 * tp));
+        if (l == 2) tb.add(make_job(e, 2, tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, lens, T), tiles(2 * tp), tmask(2 * tp));
+        if (l == 3) tb.add(make_job(e, 3, tp, n_pad, e->yB, ENC_OUT_I8, e->yC, nullptr, lens, T), tiles(2 * tp), tmask(2 * tp));
+        if (l == 4) tb.add(make_job(e, 4, tp, n_pad, e->yC, ENC_OUT_FINAL, e->fbf, f_out, lens, T), tiles(2 * tp), tmask(2 * tp));
       }
     }
     if ((r = tb.launch(e, st))) return r;

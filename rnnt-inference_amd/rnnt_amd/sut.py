@@ -601,11 +601,21 @@ class ServerSUT:
     the engines of a lane take only their lane's samples.  Latency then includes featurization."""
 
     def __init__(self, engines, qsl=None, slots=2048, split_len=128, qos_len=None, on_complete=None, pipelined=False,
-                 feeds=None, lanes=None, engine_cu_mask=None):
+                 feeds=None, lanes=None, engine_cu_mask=None, refill="fcfs", refill_window=2048):
+        """refill: "fcfs" -- every free slot takes the oldest waiting sample (PipelineState::update);
+        "tile" -- slots are refilled a 128-row tile at a time, once the whole tile is free, with the
+        oldest waiting sample and the waiting ones (among the first ``refill_window``) closest to its
+        length, so a tile's rows run out together and the encoder skips the tile as soon as they do
+        (the tick kernel skips any done tile of a stream chunk, not only trailing ones)."""
         import threading
         from .engine import pad_batch
         if split_len <= 0 or split_len % 2:
             raise ValueError("split_len must be a positive even number of frames (StackTime pairs frames)")
+        if refill not in ("fcfs", "tile"):
+            raise ValueError("refill: 'fcfs' or 'tile'")
+        if refill == "tile" and pipelined:
+            raise ValueError("refill='tile' is implemented for the round form (pipelined=False)")
+        self.refill, self.refill_window = refill, int(refill_window)
         self.engines = list(engines) if isinstance(engines, (list, tuple)) else [engines]
         self.qsl, self.split_len, self.qos_len = qsl, int(split_len), qos_len
         self.slots = pad_batch(int(slots))
@@ -833,16 +843,47 @@ class ServerSUT:
             self._cv.notify_all()
 
     # consumer -----------------------------------------------------------------------------
+    def _grouped(self, n_items, k, length_of):
+        """Indices (into a waiting list of n_items) of up to k samples taken in groups of TILE: each
+        group is the oldest sample not yet taken and the ones closest to its length among the first
+        refill_window samples not yet taken, in arrival order within the group."""
+        w = min(n_items, self.refill_window + k)
+        if w == 0 or k <= 0:
+            return []
+        L = np.array([length_of(i) for i in range(w)], np.int64)
+        taken = np.zeros(w, bool)
+        out = []
+        while len(out) < k and not taken.all():
+            elig = np.flatnonzero(~taken)[: self.refill_window]  # the window slides past taken samples
+            head = int(elig[0])
+            d = np.abs(L[elig] - L[head]).astype(np.float64) + np.arange(len(elig)) * 1e-9  # ties: older first
+            m = min(self.TILE, k - len(out), len(elig))
+            pick = np.sort(elig[np.argpartition(d, m - 1)[:m]])
+            taken[pick] = True
+            out.extend(int(i) for i in pick)
+        return out
+
+    TILE = 128  # the tick kernel's batch-row tile (ENC_ROW_TILE)
+
     def _take(self, k, busy, lane=None):
         """Up to k samples for free slots, as (issue_time, QuerySample, first store row, frames,
         store slot or None); blocks only while this engine has no busy slot.  With feeds: the
-        lane's featurized samples.  None: stopped and nothing left for this engine."""
+        lane's featurized samples.  None: stopped and nothing left for this engine.  With
+        refill='tile' the samples come in groups of TILE similar lengths (``_grouped``)."""
         with self._cv:
             while True:
                 if lane is not None:
                     rd = self._ready[lane]
                     if rd and k > 0:
-                        out = [rd.popleft() for _ in range(min(k, len(rd)))]
+                        if self.refill == "tile":
+                            items = list(rd)
+                            idx = self._grouped(len(items), k, lambda i: items[i][3])
+                            keep = set(idx)
+                            out = [items[i] for i in idx]
+                            rd.clear()
+                            rd.extend(x for i, x in enumerate(items) if i not in keep)
+                        else:
+                            out = [rd.popleft() for _ in range(min(k, len(rd)))]
                         self._cv.notify_all()  # the producer may have room again
                         return out
                     if busy or k == 0:
@@ -852,8 +893,14 @@ class ServerSUT:
                 else:
                     src = self._source()
                     if src and k > 0:
-                        out = src[:k]
-                        del src[:k]
+                        if self.refill == "tile":
+                            idx = self._grouped(len(src), k, lambda i: self.lengths[src[i][1].index])
+                            keep = set(idx)
+                            out = [src[i] for i in idx]
+                            src[:] = [x for i, x in enumerate(src) if i not in keep]
+                        else:
+                            out = src[:k]
+                            del src[:k]
                         q = self._meta_qsl  # replicas share offsets / lengths
                         return [(t0, s, int(q.offsets[s.index]), int(q.lengths[s.index]), None) for t0, s in out]
                     if busy or k == 0:
@@ -888,7 +935,13 @@ class ServerSUT:
         try:
             while True:
                 free = [i for i in range(S) if sample[i] is None]
-                new = self._take(len(free), busy=len(free) < S, lane=lane)
+                if self.refill == "tile":  # whole free tiles, filled group by group
+                    TL = self.TILE
+                    ftiles = [t for t in range(S // TL) if all(sample[i] is None for i in range(t * TL, (t + 1) * TL))]
+                    new = self._take(len(ftiles) * TL, busy=len(free) < S, lane=lane)
+                    free = [t * TL + j for t in ftiles for j in range(TL)]
+                else:
+                    new = self._take(len(free), busy=len(free) < S, lane=lane)
                 if new is None:
                     return
                 rs = h_reset.numpy()
@@ -1038,7 +1091,13 @@ class ServerSUT:
         try:
             while True:
                 free = [i for i in range(S) if sample[i] is None]
-                new = self._take(len(free), busy=len(free) < S, lane=lane)
+                if self.refill == "tile":  # whole free tiles, filled group by group
+                    TL = self.TILE
+                    ftiles = [t for t in range(S // TL) if all(sample[i] is None for i in range(t * TL, (t + 1) * TL))]
+                    new = self._take(len(ftiles) * TL, busy=len(free) < S, lane=lane)
+                    free = [t * TL + j for t in ftiles for j in range(TL)]
+                else:
+                    new = self._take(len(free), busy=len(free) < S, lane=lane)
                 if new is None:
                     return
                 rs = h_reset.numpy()

@@ -153,3 +153,43 @@ def test_two_lane_routing(devices):
     by_lane = [sum(1 for v in served.values() if v[0] == f) for f in range(2)]
     assert sum(len(fd.log) for fd in feeds) == n
     assert min(by_lane) > n // 5, by_lane  # both lanes take work
+
+
+class _LenQSL:
+    def __init__(self, lengths):
+        self.lengths = np.asarray(lengths, np.int32)
+        self.offsets = np.concatenate([[0], np.cumsum(self.lengths)[:-1]]).astype(np.int64)
+
+
+def test_tile_refill_groups_similar_lengths():
+    """refill='tile' (DESIGN §5 Server): waiting samples are taken in groups of 128 -- the oldest
+    waiting one and those closest to its length among the first refill_window -- so a refilled
+    tile's rows run out together; every sample is taken exactly once, the oldest always first."""
+    rng = np.random.default_rng(7)
+    lengths = rng.integers(47, 501, 1000)
+    srv = ServerSUT(_engines([0], max_batch=512), _LenQSL(lengths), slots=512, refill="tile", refill_window=600)
+    srv.issue_query([QuerySample(id=i, index=i) for i in range(700)], now=0.0)
+    got = srv._take(300, busy=True)
+    assert len(got) == 300
+    ids = [s.id for _, s, _, _, _ in got]
+    assert len(set(ids)) == 300
+    groups = [ids[0:128], ids[128:256], ids[256:300]]
+    remaining = list(range(700))
+    for g in groups:
+        assert g[0] == min(remaining)  # the oldest waiting sample leads its group
+        x0 = lengths[g[0]]
+        window = remaining[:600]
+        worst_in = max(abs(lengths[i] - x0) for i in g)
+        outside = [abs(lengths[i] - x0) for i in window if i not in set(g)]
+        assert not outside or worst_in <= min(outside)  # nobody closer was left behind
+        assert g == sorted(g)  # arrival order inside the group
+        remaining = [i for i in remaining if i not in set(g)]
+    # the rest stays queued in arrival order
+    left = [s.id for _, s in srv._pending]
+    assert left == remaining
+    # rows of the whole-tile refill: an fcfs SUT takes the oldest in order
+    fc = ServerSUT(_engines([0], max_batch=512), _LenQSL(lengths), slots=512)
+    fc.issue_query([QuerySample(id=i, index=i) for i in range(10)], now=0.0)
+    assert [s.id for _, s, _, _, _ in fc._take(4, busy=True)] == [0, 1, 2, 3]
+    with pytest.raises(ValueError):
+        ServerSUT(_engines([0], max_batch=512), _LenQSL(lengths), slots=512, refill="tile", pipelined=True)

@@ -39,16 +39,20 @@ def _oracle_answers(oracle, pm, qsl, idx):
     return [ro[i, : rlo[i]] for i in range(len(idx))]
 
 
-@pytest.mark.parametrize("pl", [False, True], ids=["plain", "pipelined_calls"])
-def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl):
+@pytest.mark.parametrize("pl,slot_rows", [(False, (0, 1, 2)), (True, (0, 1, 2)), (False, (5, 300, 301))],
+                         ids=["plain", "pipelined_calls", "plain_tile_holes"])
+def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl, slot_rows):
     """Slots keep their LSTM / prediction state across chunks; a slot that finishes is refilled
     (reset) with the next utterance while the others continue.  pl: the same rounds through the
-    pipelined entry points (rnnt_engine_encode_stream_pl / decode_stream_pl) from one thread."""
+    pipelined entry points (rnnt_engine_encode_stream_pl / decode_stream_pl) from one thread.
+    slot_rows (5, 300, 301) of 512: busy rows in 128-row tiles 0 and 2 only, so every tick's
+    batch-tile mask has holes (tiles 1 and 3) and, once slot 5 idles, tile 0 drops out while tile 2
+    runs on."""
     lens = np.array([137, 64, 92, 161, 45, 130, 77, 104, 59], np.int32)  # odd lengths end in odd chunks
     x = synthetic.make_features(int(lens.max()), len(lens), seed=61, lens=lens)  # emits 251 symbols in all
     store = torch.from_numpy(np.concatenate([x[: lens[i], i, :240] for i in range(len(lens))])).cuda()
     qsl = GpuQSL(lens, seed=0, store=store)
-    S, L, nslot = 256, 16, 3
+    S, L, nslot = (256 if max(slot_rows) < 256 else 512), 16, len(slot_rows)
     eng = Engine(pm, device=0, max_batch=S, max_frames=200)
     try:
         res = torch.empty((S, eng.max_res), dtype=torch.int32, device="cuda")
@@ -60,9 +64,9 @@ def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl):
         slot = [None] * S
         pos, remain = np.zeros(S, np.int64), np.zeros(S, np.int32)
         got, rounds = {}, 0
-        while queue or any(s is not None for s in slot[:nslot]):
+        while queue or any(slot[i] is not None for i in slot_rows):
             reset = np.zeros(S, np.int32)
-            for i in range(nslot):
+            for i in slot_rows:
                 if slot[i] is None and queue:
                     slot[i] = queue.pop(0)
                     pos[i], remain[i], reset[i] = 0, lens[slot[i]], 1
@@ -96,8 +100,9 @@ def test_stream_chunks_with_refill_equal_whole_utterances(pm, oracle, pl):
         np.testing.assert_array_equal(got[q], want[q], err_msg=f"utterance {q} (len {lens[q]})")
 
 
-@pytest.mark.parametrize("pipelined", [False, True], ids=["rounds", "pipelined"])
-def test_config5_server_continuous_batching(pm, oracle, pipelined):
+@pytest.mark.parametrize("pipelined,refill", [(False, "fcfs"), (True, "fcfs"), (False, "tile")],
+                         ids=["rounds", "pipelined", "rounds_tile_refill"])
+def test_config5_server_continuous_batching(pm, oracle, pipelined, refill):
     count, n, qps = 2513, 1200, 3000.0
     lengths = synthetic.devclean_lengths(count, seed=4)
     qsl = GpuQSL(lengths, seed=4, device="cuda")
@@ -107,7 +112,9 @@ def test_config5_server_continuous_batching(pm, oracle, pipelined):
     arrivals = np.cumsum(rng.exponential(1.0 / qps, size=n))
     qos = 460  # frames (the reference's QOS=233500 wav samples = 14.6 s)
     try:
-        srv = ServerSUT(engines, qsl, slots=512, split_len=32, qos_len=qos, pipelined=pipelined)
+        # refill='tile': whole 128-row tiles refilled with similar lengths, so stream chunks skip done
+        # tiles wherever they sit (the tick kernel's batch-tile mask)
+        srv = ServerSUT(engines, qsl, slots=512, split_len=32, qos_len=qos, pipelined=pipelined, refill=refill)
         srv.warmup(iters=1)  # ServerSUT::warmup (torch_sut.cpp:328-352): dummy rounds leave no trace in the answers
         srv.start()
         t0 = time.perf_counter()

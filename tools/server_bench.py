@@ -39,7 +39,7 @@ def run_point(engines, qsl, qps, duration, max_batch, seed, args, feeds=None):
     else:
         sut = ServerSUT(engines, None if feeds else qsl, slots=max_batch, split_len=args.split_len, qos_len=args.qos_len,
                         pipelined=args.pipelined, feeds=feeds,
-                        engine_cu_mask=cu_mask_words(args.fz_cus) if feeds and args.fz_cus else None)
+                        engine_cu_mask=cu_mask_words(args.fz_cus) if feeds and args.fz_cus else None, refill=args.refill)
     sut.start()
     rng = np.random.default_rng(seed)
     n = max(1, int(qps * duration))
@@ -88,6 +88,9 @@ def main():
                          "(profiles/r02z_server_search_continuous*.json)")
     ap.add_argument("--pipelined", action="store_true",
                     help="continuous: each engine encodes round k+1 while it decodes round k")
+    ap.add_argument("--refill", choices=["fcfs", "tile"], default="fcfs",
+                    help="continuous: free slots take the oldest samples (fcfs), or whole free 128-row tiles take "
+                         "groups of similar lengths (tile)")
     ap.add_argument("--qsl", type=int, default=2513)
     ap.add_argument("--search", action="store_true", help="largest QPS with p99 <= 1000 ms")
     ap.add_argument("--seed", type=int, default=5)
