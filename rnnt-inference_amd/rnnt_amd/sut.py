@@ -850,7 +850,7 @@ class ServerSUT:
         w = min(n_items, self.refill_window + k)
         if w == 0 or k <= 0:
             return []
-        L = np.array([length_of(i) for i in range(w)], np.int64)
+        L = np.fromiter((length_of(i) for i in range(w)), np.int64, w)
         taken = np.zeros(w, bool)
         out = []
         while len(out) < k and not taken.all():
@@ -876,12 +876,12 @@ class ServerSUT:
                     rd = self._ready[lane]
                     if rd and k > 0:
                         if self.refill == "tile":
-                            items = list(rd)
+                            w = min(len(rd), self.refill_window + k)
+                            items = [rd.popleft() for _ in range(w)]  # only the window can be taken from
                             idx = self._grouped(len(items), k, lambda i: items[i][3])
                             keep = set(idx)
                             out = [items[i] for i in idx]
-                            rd.clear()
-                            rd.extend(x for i, x in enumerate(items) if i not in keep)
+                            rd.extendleft(reversed([x for i, x in enumerate(items) if i not in keep]))
                         else:
                             out = [rd.popleft() for _ in range(min(k, len(rd)))]
                         self._cv.notify_all()  # the producer may have room again
@@ -897,7 +897,8 @@ class ServerSUT:
                             idx = self._grouped(len(src), k, lambda i: self.lengths[src[i][1].index])
                             keep = set(idx)
                             out = [src[i] for i in idx]
-                            src[:] = [x for i, x in enumerate(src) if i not in keep]
+                            w = max(idx) + 1  # only the window can be taken from: rebuild just that prefix
+                            src[:w] = [x for i, x in enumerate(src[:w]) if i not in keep]
                         else:
                             out = src[:k]
                             del src[:k]
