@@ -93,6 +93,9 @@ def main():
                          "groups of similar lengths (tile)")
     ap.add_argument("--qsl", type=int, default=2513)
     ap.add_argument("--search", action="store_true", help="largest QPS with p99 <= 1000 ms")
+    ap.add_argument("--burst", type=int, default=0,
+                    help="capacity instead of latency: issue this many samples at once and report samples / s until "
+                         "the last completes (the saturated throughput, free of the Poisson points' queueing noise)")
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--wav", action="store_true",
                     help="continuous, audio input (the reference's processor=true Server): --feeds WAV feeds, each "
@@ -124,6 +127,30 @@ def main():
     rp = lambda q, d, s: run_point(engines, qsl, q, d, args.max_batch, s, args, feeds)  # noqa: E731
     rp(2000.0, 1.0, 1)  # warm-up
     points = []
+    if args.burst:
+        rng = np.random.default_rng(args.seed)
+        index = rng.integers(0, len(qsl.lengths), size=args.burst)
+        sut = ServerSUT(engines, None if feeds else qsl, slots=args.max_batch, split_len=args.split_len,
+                        qos_len=args.qos_len, pipelined=args.pipelined, feeds=feeds, refill=args.refill)
+        sut.start()
+        t0 = time.perf_counter()
+        sut.issue_query([QuerySample(id=k, index=int(index[k])) for k in range(args.burst)], now=t0)
+        sut.flush_queries()
+        deadline = t0 + 300.0
+        while len(sut.latency) < args.burst and time.perf_counter() < deadline and not sut.errors:
+            time.sleep(0.005)
+        span = time.perf_counter() - t0
+        sut.stop()
+        if sut.errors:
+            raise sut.errors[0]
+        frames = int(qsl.lengths[index].sum())
+        print(json.dumps({"scenario": "Server capacity (burst)", "refill": args.refill, "samples": args.burst,
+                          "seconds": round(span, 3), "samples_per_s": round(args.burst / span, 1),
+                          "frames_per_s": round(frames / span, 1), "rounds": sut.rounds,
+                          "stream_prefix": os.environ.get("RNNT_STREAM_PREFIX", "0")}), flush=True)
+        for e in engines:
+            e.close()
+        return
     if not args.search:
         points.append(rp(args.qps, args.duration, args.seed))
     else:
