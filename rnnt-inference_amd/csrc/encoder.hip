@@ -212,9 +212,18 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   const uint32_t oA0 = rlA * K + gA0, oA1 = rlA * K + gA1;
   const uint32_t oX0 = rlB * a.I + gB0, oX1 = rlB * a.I + gB1;
   const uint32_t oH0 = rlB * H + gB0, oH1 = rlB * H + gB1;
+#ifdef RNNT_ABL_W1  // profiling ablation only (tools/enc_ablate.sh): every gate tile reads tile 0's weights (L2-resident)
+  const int8_t* wbase = a.W;
+#else
   const int8_t* wbase = a.W + (size_t)m0 * K;
+#endif
+#ifdef RNNT_ABL_X1  // profiling ablation only: every batch tile reads tile 0's activations (L2-resident)
+  const int8_t* xbase = a.x;
+  const int8_t* hbase = a.h_in - a.I;
+#else
   const int8_t* xbase = a.x + (size_t)n0 * a.I;
   const int8_t* hbase = a.h_in + (size_t)n0 * H - a.I;  // k >= I indexes h at k - I
+#endif
   auto issueA = [&](int s) __attribute__((always_inline)) {
     const int k = s * 128;
     lds_char* st = lds + (s % NBUF) * STAGE + wave * (C::PA * 1024);
