@@ -362,10 +362,11 @@ def main():
     emitted = int(got[1].sum()) if got is not None else 0  # whole query (rank 0 holds the gathered responses)
     achieved = enc_ops * args.steps / (st["encode_ms"] * 1e-3) / 1e12 if st["encode_ms"] > 0 else 0.0
     achieved_iso = enc_ops / (iso["encode_ms"] * 1e-3) / 1e12 if iso["encode_ms"] > 0 else 0.0
-    traffic = None
+    traffic, traffic_src = None, None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("lstm_i8_step_bytes_per_launch")
+            tj = json.load(open(args.traffic_json))
+            traffic, traffic_src = tj.get("lstm_i8_step_bytes_per_launch"), tj.get("source")
         except Exception:
             traffic = None
     # decode work: D = (T' + U) * 4,682,752 bf16 ops per utterance (this rank's share)
@@ -379,6 +380,9 @@ def main():
         "bound": "mfma", "kernel": "lstm_i8_tick_kernel (int8 encoder, up to 5 layer-steps per launch)",
         "achieved": round(achieved, 2), "peak": INT8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
         "frac": round(achieved / INT8_DENSE_PEAK_TOPS, 4), "traffic": traffic,
+        "traffic_source": ("HBM bytes per tick launch, rocprofv3 PMC pass of this round's profile "
+                           "(tools/profile_round.sh; (2 FETCH_SIZE + WRITE_SIZE) x 1024): " + str(traffic_src))
+        if traffic is not None else None,
         "measured_on": "HIP events around every encode call on its own stream, timed region (encode overlaps "
                        "other batches' decode); rank 0's share of the query",
         "encode_ms_per_query": round(st["encode_ms"] / args.steps, 3),
