@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--deal", choices=("dynamic", "static"), default="dynamic",
                     help="several ranks: claim batches from one shared counter when the encoder is free (dynamic), or "
                          "deal them in snake order up front (static)")
+    ap.add_argument("--sut-warmup", type=int, default=1,
+                    help="OfflineSUT.warmup iterations on dummy samples before the warmup steps (0: none)")
+    ap.add_argument("--sut-warmup-frames", type=int, default=500, help="frames per dummy sample (MAX_FEA_LEN)")
     ap.add_argument("--mock", action="store_true",
                     help="launcher / sharding check without a GPU: gloo ranks deal and gather a query of stand-in "
                          "responses (no engine, no HIP); the line it prints is not a measurement")
@@ -307,7 +310,8 @@ def main():
     max_b = max([args.batch] + ([int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else []))
     engines = [Engine(pm, device=local, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
     sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
-    sut.warmup(iters=1, batch_size=args.batch)  # OfflineSUT::warmup (torch_sut.cpp:124-138), before any query
+    if args.sut_warmup:  # OfflineSUT::warmup (torch_sut.cpp:124-138), before any query
+        sut.warmup(iters=args.sut_warmup, batch_size=args.batch, frames=args.sut_warmup_frames)
     sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None
 
     qno = [0]

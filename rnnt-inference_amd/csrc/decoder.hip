@@ -24,6 +24,7 @@
 // dependent memory round trips short: emit-list entries carry (row, slot, label), the list
 // entries of a workgroup's first tile are loaded beside the list length, the cell state is
 // fetched beside the input staging, and the joint walks a compact list of unfinished rows.
+#include <cstdlib>
 #include "rnnt_device.hpp"
 #include "decoder.hpp"
 
@@ -857,7 +858,18 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   // ~20 us each: four dependent launches) empty steps.  Once few rows are left -- the long-tail
   // rows whose last emission ends the loop -- chunks shrink to 8 steps: the overshoot falls from
   // ~48 to ~12 steps while the host (~3.5 us per launch) still stays ahead of the GPU.
-  constexpr int CHUNK = 32, TAIL_CHUNK = 8, TAIL_ROWS = 64;
+  constexpr int CHUNK = 32, TAIL_ROWS = 64;
+  // development knobs (same-box A/B of the tail, tools/r04_dectail.sh): RNNT_DEC_TAIL_CHUNK steps
+  // per tail chunk (default 8), RNNT_DEC_SPIN=1 polls the previous chunk's event without yielding
+  static const int TAIL_CHUNK = [] {
+    const char* v = getenv("RNNT_DEC_TAIL_CHUNK");
+    const int c = v ? atoi(v) : 8;
+    return c >= 1 && c <= CHUNK ? c : 8;
+  }();
+  static const bool SPIN = [] {
+    const char* v = getenv("RNNT_DEC_SPIN");
+    return v && v[0] == '1';
+  }();
   int step = 0, chunk = 0;
   int live_bound = a.N;  // unfinished rows at the end of the last chunk read back (an upper bound)
   bool done = false;
@@ -888,7 +900,14 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
       return -1;
     if (hipEventRecord(evs[chunk & 1], st) != hipSuccess) return -1;
     if (chunk > 0) {
-      if (hipEventSynchronize(evs[(chunk - 1) & 1]) != hipSuccess) return -1;
+      if (SPIN) {
+        hipError_t q;
+        while ((q = hipEventQuery(evs[(chunk - 1) & 1])) == hipErrorNotReady) {
+        }
+        if (q != hipSuccess) return -1;
+      } else if (hipEventSynchronize(evs[(chunk - 1) & 1]) != hipSuccess) {
+        return -1;
+      }
       live_bound = host_flags[(chunk - 1) & 1];
       done = live_bound == 0;
     }

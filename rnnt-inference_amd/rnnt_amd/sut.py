@@ -223,6 +223,8 @@ class OfflineSUT:
         engine's capacity).  -> seconds spent."""
         import time
         t0 = time.perf_counter()
+        for eng in self.engines:  # every engine's stream exists before any work is queued (as in issue_batches)
+            self._stream_for(eng)
         for eng in self.engines:
             n = max(1, min(int(batch_size or self.batch_size), int(eng.max_batch)))
             n_pad = pad_batch(n)
@@ -232,6 +234,8 @@ class OfflineSUT:
                 with self._device_scope(eng, st):
                     enc = self._encode(eng, st, None, np.zeros(n, np.int64), n, n_pad, qsl=dummy)
                     self._decode(eng, st, enc)
+            del dummy, enc
+        _release_cached(self.engines)  # the dummy batches' inputs are transient: give their blocks back
         return time.perf_counter() - t0
 
     def ran_batches(self, batches):
@@ -346,6 +350,18 @@ class OfflineSUT:
 
     def flush_queries(self):
         pass
+
+
+def _release_cached(engines):
+    """Return the caching allocator's free blocks on the engines' devices (after a warmup's large
+    transient dummy inputs) once their streams are idle."""
+    import torch
+    if not torch.cuda.is_available():  # host-side tests stand in for the devices
+        return
+    for dev in sorted({e.device for e in engines}):
+        with torch.cuda.device(dev):
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
 
 
 class DummyQSL:
@@ -697,6 +713,8 @@ class ServerSUT:
                             eng.encode_stream(store, d_off, d_lens, lens_h, d_reset, cl, S, S, stream=st)
                             eng.decode_stream(res, rl, d_reset, stream=st)
                     st.synchronize()
+                del store, res, rl
+        _release_cached(self.engines)
         return time.perf_counter() - t0
 
     def _assign_lanes(self, lanes):
