@@ -77,8 +77,9 @@ def parse():
     ap.add_argument("--deal", choices=("dynamic", "static"), default="dynamic",
                     help="several ranks: claim batches from one shared counter when the encoder is free (dynamic), or "
                          "deal them in snake order up front (static)")
-    ap.add_argument("--sut-warmup", type=int, default=1,
-                    help="OfflineSUT.warmup iterations on dummy samples before the warmup steps (0: none)")
+    ap.add_argument("--sut-warmup", type=int, default=0,
+                    help="OfflineSUT.warmup iterations on dummy samples before the --warmup steps (default 0: the "
+                         "--warmup steps on real batches already take the first-call costs; DESIGN section 5)")
     ap.add_argument("--sut-warmup-frames", type=int, default=500, help="frames per dummy sample (MAX_FEA_LEN)")
     ap.add_argument("--mock", action="store_true",
                     help="launcher / sharding check without a GPU: gloo ranks deal and gather a query of stand-in "
