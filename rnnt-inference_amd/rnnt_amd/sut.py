@@ -366,8 +366,11 @@ def _release_cached(engines):
 
 class DummyQSL:
     """QSL::GenerateDummySamples (rnnt_qsl.cpp:136-147) for the SUT warmups: every requested sample
-    is N(0,1) features of `frames` frames over all PADDED_INPUT_SIZE channels, length `frames`,
-    generated on the target device (nothing staged from the host)."""
+    is the same `frames`-frame N(0,1) feature sample (240 channels, length `frames`), generated on
+    the target device and handed over in the gather form of GpuQSL (one sample in a store, every
+    row's offset 0) -- the engine's gather-quantize pass assembles the batch, so no dense
+    [frames, n_pad, 256] batch is materialised (a dense 4096 x 500-frame dummy
+    batch left later queries slower)."""
 
     def __init__(self, frames=R.MAX_FEA_LEN, seed=0):
         self.frames, self.seed = int(frames), int(seed)
@@ -377,10 +380,11 @@ class DummyQSL:
         n = len(indices)
         g = torch.Generator(device=device)
         g.manual_seed(self.seed)
-        x = torch.randn((self.frames, n_pad, R.PADDED_INPUT_SIZE), device=device, generator=g)
+        store = torch.randn((self.frames, R.trans_input_size), device=device, generator=g)
         lens = torch.zeros(n_pad, dtype=torch.int32, device=device)
         lens[:n] = self.frames
-        return dict(x=x, lens=lens, lens_host=np.full(n, self.frames, np.int32), T=self.frames)
+        return dict(store=store, offsets=torch.zeros(n, dtype=torch.int64, device=device), lens=lens,
+                    lens_host=np.full(n, self.frames, np.int32), T=self.frames)
 
 
 class GpuQSL(_SortedQSL):

@@ -25,8 +25,8 @@ class _HostSUT(OfflineSUT):
 
     def _encode(self, eng, st, ids, idx, n, n_pad, qsl=None):
         inp = (qsl or self.qsl_for(eng.device)).batch_inputs(idx, n_pad, "cpu")
-        eng.calls.append(("encode", n, n_pad, inp["T"], tuple(inp["x"].shape), inp["lens_host"].copy(),
-                          inp["lens"][n:].abs().sum().item()))
+        eng.calls.append(("encode", n, n_pad, inp["T"], tuple(inp["store"].shape), inp["lens_host"].copy(),
+                          inp["lens"][n:].abs().sum().item(), tuple(inp["offsets"].tolist())))
         return n
 
     def _decode(self, eng, st, n):
@@ -44,10 +44,11 @@ def test_offline_warmup_runs_every_engine_and_completes_nothing():
         enc = [c for c in e.calls if c[0] == "encode"]
         assert len(enc) == 2 and [c[0] for c in e.calls] == ["encode", "decode"] * 2
         for c in enc:
-            _, nn, n_pad, T, shape, lh, pad_lens = c
+            _, nn, n_pad, T, shape, lh, pad_lens, offs = c
             assert nn == n and n_pad % 256 == 0 and n_pad >= n
-            assert T == R.MAX_FEA_LEN and shape == (R.MAX_FEA_LEN, n_pad, R.PADDED_INPUT_SIZE)
-            assert np.all(lh == R.MAX_FEA_LEN) and pad_lens == 0
+            # gather form: one MAX_FEA_LEN-frame sample in the store, every row at offset 0
+            assert T == R.MAX_FEA_LEN and shape == (R.MAX_FEA_LEN, R.trans_input_size)
+            assert np.all(lh == R.MAX_FEA_LEN) and pad_lens == 0 and offs == (0,) * n
     assert sut.take_completed()[0].size == 0 and not sut.responses
 
 
@@ -55,7 +56,8 @@ def test_dummy_samples_are_seeded_normal_features():
     d = DummyQSL(frames=40, seed=3)
     a = d.batch_inputs(np.zeros(5, np.int64), 256, "cpu")
     b = d.batch_inputs(np.zeros(5, np.int64), 256, "cpu")
-    assert a["x"].shape == (40, 256, 256) and a["T"] == 40
-    assert bool((a["x"] == b["x"]).all())  # deterministic
-    assert abs(float(a["x"].std()) - 1.0) < 0.02
+    assert a["store"].shape == (40, R.trans_input_size) and a["T"] == 40
+    assert a["offsets"].tolist() == [0] * 5 and a["lens"][:5].tolist() == [40] * 5 and int(a["lens"][5:].sum()) == 0
+    assert bool((a["store"] == b["store"]).all())  # deterministic
+    assert abs(float(a["store"].std()) - 1.0) < 0.05
     assert a["lens"][:5].tolist() == [40] * 5 and int(a["lens"][5:].abs().sum()) == 0
