@@ -856,15 +856,17 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   // Steps are enqueued in chunks and the host reads the live count one chunk behind, so a decode
   // ends with the rest of the chunk holding its last step plus one more chunk of (cheap, but still
   // ~20 us each: four dependent launches) empty steps.  Once few rows are left -- the long-tail
-  // rows whose last emission ends the loop -- chunks shrink to 8 steps: the overshoot falls from
-  // ~48 to ~12 steps while the host (~3.5 us per launch) still stays ahead of the GPU.
+  // rows whose last emission ends the loop -- chunks shrink (TAIL_CHUNK): less overshoot while the
+  // host (~3.5 us per launch) still stays ahead of the GPU.
   constexpr int CHUNK = 32, TAIL_ROWS = 64;
-  // development knobs (same-box A/B of the tail, tools/r04_dectail.sh): RNNT_DEC_TAIL_CHUNK steps
-  // per tail chunk (default 8), RNNT_DEC_SPIN=1 polls the previous chunk's event without yielding
+  // Tail chunks of 16 steps: isolated decode of the bench query 93.6 / 94.0 ms vs 94.6 / 94.9 with 8,
+  // 95.3-96.0 with 4 (tools/r04_dectail.sh, same box, alternating; fewer polls outweigh the longer
+  // overshoot).  Development knobs for that A/B: RNNT_DEC_TAIL_CHUNK steps per tail chunk,
+  // RNNT_DEC_SPIN=1 polls the previous chunk's event without yielding (no gain measured).
   static const int TAIL_CHUNK = [] {
     const char* v = getenv("RNNT_DEC_TAIL_CHUNK");
-    const int c = v ? atoi(v) : 8;
-    return c >= 1 && c <= CHUNK ? c : 8;
+    const int c = v ? atoi(v) : 16;
+    return c >= 1 && c <= CHUNK ? c : 16;
   }();
   static const bool SPIN = [] {
     const char* v = getenv("RNNT_DEC_SPIN");

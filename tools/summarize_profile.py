@@ -47,6 +47,37 @@ def main():
                   open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "roofline_traffic.json"), "w"), indent=1)
     for k, d in summary.items():
         print(k, {c: round(v, 3) for c, v in d.items() if c in ("dispatches", "hbm_bytes_per_launch", "mfma_busy_frac", "SQ_INSTS_VALU", "SQ_INSTS_MFMA")})
+    per_query(src, stats[0] if stats else None, prefix)
+
+
+def per_query(src, stats_csv, prefix):
+    """Encoder kernel-time fraction per query from the traced bench run: the bench line (printed to
+    trace.log) gives the int8 ops of one query (roofline.achieved x encode_ms_per_query) and the
+    step count; the traced run holds warmup + timed + one isolated query (bench.py), so the tick
+    kernels' total time / that many queries is the kernel time per query."""
+    try:
+        line = [x for x in open(os.path.join(src, "trace.log")) if x.startswith('{"metric"')][-1]
+        b = json.loads(line)
+    except (OSError, IndexError, ValueError):
+        return
+    r = b["roofline"]
+    ops = r["achieved"] * 1e12 * r["encode_ms_per_query"] * 1e-3
+    queries = b["steps"] + b["warmup"] + 1
+    tick_ns = 0.0
+    if stats_csv:
+        for row in csv.DictReader(open(stats_csv)):
+            if "lstm_i8_tick_kernel" in row["Name"]:
+                tick_ns += float(row["TotalDurationNs"])
+    if not tick_ns:
+        return
+    t = tick_ns * 1e-9 / queries
+    out = {"queries_in_trace": queries, "note": "bench.py --warmup W --steps K traced: W + K queries + 1 isolated pass",
+           "int8_ops_per_query": ops, "tick_kernel_ms_per_query": round(t * 1e3, 3),
+           "tick_launches_per_query": r.get("tick_launches_per_query"),
+           "encoder_kernel_time_frac": round(ops / t / 5.0e15, 4), "peak_tops": 5000.0,
+           "bench_value": b["value"], "bench_roofline_frac_event_time": r["frac"]}
+    json.dump(out, open(prefix + "_per_query.json", "w"), indent=1)
+    print("per query:", out)
 
 
 if __name__ == "__main__":
