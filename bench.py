@@ -81,6 +81,11 @@ def parse():
                     help="OfflineSUT.warmup iterations on dummy samples before the --warmup steps (default 0: the "
                          "--warmup steps on real batches already take the first-call costs; DESIGN section 5)")
     ap.add_argument("--sut-warmup-frames", type=int, default=500, help="frames per dummy sample (MAX_FEA_LEN)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="multi-rank rehearsal on a 1-GPU box: every rank on cuda:0, control plane on gloo (RCCL refuses "
+                         "two ranks on one device); the line checks the multi-process path, it is not a measurement")
+    ap.add_argument("--dump-responses", default=None,
+                    help="rank 0 writes the last timed query's gathered responses (ids, lens, toks) to this .npz")
     ap.add_argument("--mock", action="store_true",
                     help="launcher / sharding check without a GPU: gloo ranks deal and gather a query of stand-in "
                          "responses (no engine, no HIP); the line it prints is not a measurement")
@@ -301,15 +306,16 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the torchrun world has {world} rank(s)")
     if args.mock:
         return mock_main(args)
-    torch.cuda.set_device(local)
-    rank, local, world, ggroup = dist.setup("nccl")
-    device = f"cuda:{local}"
+    dev = 0 if args.share_device else local
+    torch.cuda.set_device(dev)
+    rank, local, world, ggroup = dist.setup("gloo" if args.share_device else "nccl")
+    device = f"cuda:{dev}"
     pm, _ = weights.build_model()
     qsl = build_qsl(args.qsl, seed=4, device=device, wav=args.wav)
     query = args.query * world
     ids, idx = dist.query_arrays(args.qsl, query)
     max_b = max([args.batch] + ([int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else []))
-    engines = [Engine(pm, device=local, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
+    engines = [Engine(pm, device=dev, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
     sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
     if args.sut_warmup:  # OfflineSUT::warmup (torch_sut.cpp:124-138), before any query
         sut.warmup(iters=args.sut_warmup, batch_size=args.batch, frames=args.sut_warmup_frames)
@@ -431,6 +437,11 @@ def main():
     }
     if rank == 0 and got is not None:
         assert len(got[0]) == query and len(np.unique(got[0])) == query, "gathered responses do not cover the query"
+        if args.dump_responses:
+            np.savez_compressed(args.dump_responses, ids=got[0], lens=got[1], toks=got[2])
+    if args.share_device:
+        out["rehearsal"] = (f"{world} ranks share cuda:0 (gloo control plane): multi-process path check, not a "
+                            "measurement")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.wav:
         resp = responses_dict(*got)
         cb = cpu_baseline(pm, qsl, mine, batch_engine, resp, args.cpu_sample, args.inflight)
