@@ -153,6 +153,8 @@ def mock_main(args):
     elapsed = dist.reduce_max(time.perf_counter() - t0, group)
     if rank == 0:
         assert len(got[0]) == query and len(np.unique(got[0])) == query, "gathered responses do not cover the query"
+        if args.dump_responses:
+            np.savez_compressed(args.dump_responses, ids=got[0], lens=got[1], toks=got[2])
         print(json.dumps({"metric": METRIC, "value": None, "unit": "utterances/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                           "data": "mock: no engine, stand-in responses (launcher / sharding check, not a measurement)",

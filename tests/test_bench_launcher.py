@@ -35,3 +35,32 @@ def test_world_disagreeing_with_gpus_fails():
     out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--mock", "--steps", "1", "--warmup", "0"],
                          capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode != 0 and "--gpus 2" in out.stderr
+
+
+def test_dumped_responses_equal_across_rank_counts(tmp_path):
+    """--dump-responses + tools/compare_responses.py (the GPU rehearsal's check,
+    tools/r04_multirank.sh) on the mock path: the query served by 2 ranks with dynamic claims and by
+    3 ranks with the static deal gathers the same rows as 1 rank; a changed row is reported."""
+    import numpy as np
+
+    def run(ranks, query, name, *extra):
+        p = str(tmp_path / f"{name}.npz")
+        out = subprocess.run([sys.executable, BENCH, "--gpus", str(ranks), "--mock", "--steps", "1", "--warmup", "0",
+                              "--query", str(query), "--batch", "256", "--dump-responses", p, *extra],
+                             capture_output=True, text=True, timeout=300, env=_env())
+        assert out.returncode == 0, out.stderr[-2000:]
+        return p
+
+    one = run(1, 1536, "one")
+    cmp = os.path.join(REPO, "tools", "compare_responses.py")
+    for p in (run(2, 768, "dyn2"), run(3, 512, "static3", "--deal", "static")):
+        out = subprocess.run([sys.executable, cmp, p, one], capture_output=True, text=True, timeout=60)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert json.loads(out.stdout)["identical"]
+    z = dict(np.load(one))
+    z["toks"] = z["toks"].copy()
+    z["toks"][0] ^= 1
+    bad = str(tmp_path / "bad.npz")
+    np.savez(bad, **z)
+    out = subprocess.run([sys.executable, cmp, bad, one], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 1 and json.loads(out.stdout)["mismatched_rows"] == 1
