@@ -345,47 +345,9 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   lds_char* hs = lds + cbuf + BN * C::CROW;
   lds_char* ys = lds + ((nS - 1) % NBUF) * STAGE;
   constexpr int HP = C::HP;
-#ifdef RNNT_EPI_PHASED
-  // development variant: every cell's state first (c_prev reads, all gate-table gathers, c, the
-  // tanh gathers, h), then the image stores -- no table gather waits behind an earlier column's
-  // stores or opaque copies
-  float cA[WNT][WMT], hA[WNT][WMT];
-  {
-    float cinA[WNT][WMT];
-#pragma unroll
-    for (int j = 0; j < WNT; ++j) {
-      const int r = nb + 16 * j - n0;
-      float* cin = cinA[j];
-      if (WMT == 4) {
-        const uint2 cv = *(const uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
-        cin[0] = h2f((uint16_t)(cv.x & 0xffff)); cin[1 % WMT] = h2f((uint16_t)(cv.x >> 16));
-        cin[2 % WMT] = h2f((uint16_t)(cv.y & 0xffff)); cin[3 % WMT] = h2f((uint16_t)(cv.y >> 16));
-      } else if (WMT == 1) {
-        cin[0] = h2f(*(const uint16_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)));
-      } else {
-        const uint32_t cv = *(const uint32_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
-        cin[0] = h2f((uint16_t)(cv & 0xffff)); cin[1 % WMT] = h2f((uint16_t)(cv >> 16));
-      }
-    }
-    float4 gA[WNT][WMT];
-#pragma unroll
-    for (int j = 0; j < WNT; ++j)
-#pragma unroll
-      for (int i = 0; i < WMT; ++i) gA[j][i] = enc_gates(tab, acc[i][j], bq[i], As, Ag);
-#pragma unroll
-    for (int j = 0; j < WNT; ++j)
-#pragma unroll
-      for (int i = 0; i < WMT; ++i) cA[j][i] = enc_c(gA[j][i], cinA[j][i]);
-#pragma unroll
-    for (int j = 0; j < WNT; ++j)
-#pragma unroll
-      for (int i = 0; i < WMT; ++i) hA[j][i] = enc_h(tab, gA[j][i].w, cA[j][i]);
-  }
-#endif
 #pragma unroll
   for (int j = 0; j < WNT; ++j) {
     const int n = nb + 16 * j, r = n - n0;
-#ifndef RNNT_EPI_PHASED
     float cin[WMT];
     if (WMT == 4) {
       const uint2 cv = *(const uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
@@ -397,17 +359,12 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       const uint32_t cv = *(const uint32_t*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2));
       cin[0] = h2f((uint16_t)(cv & 0xffff)); cin[1 % WMT] = h2f((uint16_t)(cv >> 16));
     }
-#endif
     uint32_t cw[2] = {0u, 0u}, hb[4] = {0u, 0u, 0u, 0u}, yb[4] = {0u, 0u, 0u, 0u};
     float hv[WMT];
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
-#ifdef RNNT_EPI_PHASED
-      const float cn = cA[j][i], hh = hA[j][i];
-#else
       float cn, hh;
       enc_cell(tab, acc[i][j], bq[i], As, Ag, cin[i], cn, hh);
-#endif
       cw[i >> 1] |= (uint32_t)f2h(cn) << (16 * (i & 1));
       hv[i] = hh;
       hb[i] = q8_biased(hh * ins);

@@ -115,31 +115,10 @@ __device__ __forceinline__ void enc_cell(const float2* __restrict__ tab, const v
   // opaque here: otherwise the backend folds fma + the later f32->f16 store conversion into
   // v_fma_mixlo_f16 (one rounding straight to f16), which is not the contract's fp32 c
   // rounded to fp16
-#ifdef RNNT_EPI_NV  // development variant: the opaque copy without side effects (no scheduling barrier)
-  asm("" : "+v"(c));
-#else
   asm volatile("" : "+v"(c));
-#endif
   const float tc = __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf(c, 128.0f, 1024.0f)), -1.0f);
   c_out = c;
   h_out = og * tc;
-}
-// enc_cell in three parts, same operations in the same order: the four gate activations
-// (i, f, 2 sigma(2x) - 1, o), the new cell state, and h = o tanh(c)
-__device__ __forceinline__ float4 enc_gates(const float2* __restrict__ tab, const v4i acc, const float4 B, float As,
-                                            float Ag) {
-  return float4{act_sig_t(tab, __builtin_fmaf((float)acc[0], As, B.x)),
-                act_sig_t(tab, __builtin_fmaf((float)acc[1], As, B.y)),
-                __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf((float)acc[2], Ag, B.z)), -1.0f),
-                act_sig_t(tab, __builtin_fmaf((float)acc[3], As, B.w))};
-}
-__device__ __forceinline__ float enc_c(const float4 g, float c_prev) {
-  float c = __builtin_fmaf(g.y, c_prev, g.x * g.z);
-  asm volatile("" : "+v"(c));  // as in enc_cell: no fused fma -> f16 conversion
-  return c;
-}
-__device__ __forceinline__ float enc_h(const float2* __restrict__ tab, float og, float c) {
-  return og * __builtin_fmaf(2.0f, act_sig_t(tab, __builtin_fmaf(c, 128.0f, 1024.0f)), -1.0f);
 }
 // q8(v) (= clamp(rint(v), -128, 127), RNE) in the int8 byte of the result: v + 1.5 * 2^23
 // rounds to the integer grid exactly as rint does (|v| < 2^22; larger values clamp anyway), the
