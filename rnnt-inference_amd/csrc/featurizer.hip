@@ -37,7 +37,10 @@ namespace rnnt {
 namespace {
 
 constexpr int NT = 256;                                    // threads per (sub-)workgroup (4 waves)
-constexpr int FZ_NSUB = 3;                                 // fz_logmel: chunks (4-wave sub-groups) per workgroup
+#ifndef RNNT_FZ_NSUB  // development override (tools/r04_fzdiag.sh variants): 3 = the round-3 workgroup
+#define RNNT_FZ_NSUB 1
+#endif
+constexpr int FZ_NSUB = RNNT_FZ_NSUB;                      // fz_logmel: chunks (4-wave sub-groups) per workgroup
 constexpr int SEGC = FZ_HOP * (FZ_CHUNK - 1) + FZ_WIN;     // 2720 samples per chunk
 constexpr int WOFF = (FZ_NFFT - FZ_WIN) / 2;               // 96: torch.stft centres the window in n_fft
 constexpr int SCR = 17 * 16;                               // 16 x 16 complex transpose, rows padded to 17
@@ -135,12 +138,12 @@ __global__ __launch_bounds__(1024) void fz_plan_kernel(FzArgs a) {
   }
 }
 
-// A workgroup = FZ_NSUB chunks, one 4-wave sub-group (NT threads) each, and it owns its CU: its
-// static LDS plus an unused dynamic remainder fill the 160 KiB (launch_logmel), so no workgroup of
-// another kernel is ever resident beside it.  Measured (tools/diag_fz_concurrency.py, DESIGN.md
-// 4b): with the decode step kernels resident on the same CU, the FFT of the frames held by lanes
-// 48-63 of a logmel wave came out wrong in ~13 % of the batches (no other co-runner, incl.
-// synthetic MFMA / LDS / VALU / load kernels, did it); with the CU to itself, 0 in 40k batches.
+// A workgroup = FZ_NSUB chunks, one 4-wave sub-group (NT threads) each; other kernels' workgroups
+// may share its CU.  This file is compiled WITHOUT packed FP32 VALU (-fno-slp-vectorize, Makefile;
+// tests/test_isa_lint.py checks the ISA): with v_pk_add/mul/fma_f32 in the FFT, the results of
+// lanes 48-63 of a logmel wave came out wrong in ~8-13 % of the batches whenever decode step
+// kernels shared the CU (the corrupted frames follow those lanes when the frame-to-lane map is
+// reversed); built without them, 0 in ~100k batches, and no slower.
 __global__ __launch_bounds__(NT * FZ_NSUB, 1) void fz_logmel_kernel(FzArgs a) {
   const int sub = threadIdx.x / NT;
   const int gj = blockIdx.x * FZ_NSUB + sub;  // this sub-group's plan entry
@@ -190,9 +193,14 @@ __global__ __launch_bounds__(NT * FZ_NSUB, 1) void fz_logmel_kernel(FzArgs a) {
   }
   __syncthreads();
 
-  float2* sc = scr[wave][slot];
+#ifdef RNNT_FZ_SLOTREV  // development variant (DESIGN 4b diagnosis): lanes 48-63 take frame slot 0, lanes 0-15 slot 3
+  const int fslot = 3 - slot;
+#else
+  const int fslot = slot;
+#endif
+  float2* sc = scr[wave][fslot];
   if (active) {
-    const int fl = 4 * wave + slot;  // frame in the chunk
+    const int fl = 4 * wave + fslot;  // frame in the chunk
     const float* sf = seg + FZ_HOP * fl - WOFF;
     float2 v[16];
 #pragma unroll
@@ -451,21 +459,8 @@ extern "C" void rnnt_featurizer_destroy(rnnt_featurizer* f) {
   delete f;
 }
 
-// fz_logmel_kernel owns a whole CU: the unused rest of the CU's LDS (read from the device: 160 KiB
-// on gfx950) is requested as dynamic LDS
 static int launch_logmel(const FzArgs& a, size_t chunks, hipStream_t st) {
-  static std::atomic<uint64_t> attr{0};
-  static const int pad = [] {  // thread-safe one-time init
-    hipFuncAttributes fa{};
-    int dev = 0, cu_lds = 0;
-    if (hipFuncGetAttributes(&fa, (const void*)fz_logmel_kernel) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cu_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
-      return -1;
-    return std::max(cu_lds - (int)fa.sharedSizeBytes, 0);
-  }();
-  if (pad < 0 || set_smem_attr_once((const void*)fz_logmel_kernel, pad, attr)) return -1;
-  hipLaunchKernelGGL(fz_logmel_kernel, dim3((unsigned)((chunks + FZ_NSUB - 1) / FZ_NSUB)), dim3(NT * FZ_NSUB), pad, st,
-                     a);
+  hipLaunchKernelGGL(fz_logmel_kernel, dim3((unsigned)((chunks + FZ_NSUB - 1) / FZ_NSUB)), dim3(NT * FZ_NSUB), 0, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

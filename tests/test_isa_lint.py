@@ -106,3 +106,24 @@ def test_no_masked_wide_multiply_in_kernels():
     bad = {os.path.basename(s): masked_wide_multiplies(ir) for s, ir in irs}
     bad = {k: v for k, v in bad.items() if v}
     assert not bad, f"masked 24-bit values in 64-bit multiplies (miscompiled by ROCm 7.2): {bad}"
+
+
+def test_featurizer_has_no_packed_fp32():
+    """featurizer.hip is built with -fno-slp-vectorize (Makefile): packed FP32 VALU
+    (v_pk_add / mul / fma_f32) in fz_logmel's FFT gave wrong results in lanes 48-63 of a wave while
+    decode step kernels shared the CU (tools/r04_fzdiag.sh, the corrupted frames move
+    with those lanes; without packed FP32 0 of ~100k batches).  The gfx950 ISA of the file, built
+    with the Makefile's flags, must not contain them."""
+    if not shutil.which(HIPCC) and not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    assert re.search(r"^featurizer\.o: FLAGS \+= -fno-slp-vectorize", mk, re.M), "Makefile lost the featurizer flag"
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "fz.s")
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-w",
+                        "-fno-slp-vectorize", "--cuda-device-only", "-S", "featurizer.hip", "-o", out],
+                       check=True, cwd=CSRC, capture_output=True)
+        isa = open(out).read()
+    assert "fz_logmel_kernel" in isa
+    hits = re.findall(r"^\s*(v_pk_(?:add|mul|fma)_f32)\b", isa, re.M)
+    assert not hits, f"packed FP32 in featurizer.hip's ISA: {sorted(set(hits))}"

@@ -12,7 +12,7 @@ build() {
   local objs=""
   for src in engine encoder encoder_f32 decoder decoder_f32 decoder_ops featurizer processor_ops; do
     local extra=""
-    [ $src = encoder ] && extra="-fno-slp-vectorize"
+    [ $src = encoder -o $src = featurizer ] && extra="-fno-slp-vectorize"
     $HIPCC $extra "$@" -c $src.hip -o $OUTD/${src}_$name.o &
     objs="$objs $OUTD/${src}_$name.o"
   done
