@@ -86,10 +86,24 @@ def parse():
                          "two ranks on one device); the line checks the multi-process path, it is not a measurement")
     ap.add_argument("--dump-responses", default=None,
                     help="rank 0 writes the last timed query's gathered responses (ids, lens, toks) to this .npz")
+    ap.add_argument("--control-backend", choices=("gloo", "nccl"), default="gloo",
+                    help="torch.distributed backend of the control plane (barriers, max-over-ranks timing, batch "
+                         "claims) for --gpus N: the data path has no collective (DESIGN section 6), and gloo is the "
+                         "backend the multi-rank hardware rehearsal (--share-device) ran; nccl (RCCL) is opt-in")
     ap.add_argument("--mock", action="store_true",
                     help="launcher / sharding check without a GPU: gloo ranks deal and gather a query of stand-in "
                          "responses (no engine, no HIP); the line it prints is not a measurement")
     return ap.parse_args()
+
+
+def control_backend(args):
+    """Backend of the multi-rank control plane: gloo unless --control-backend nccl (RCCL refuses two
+    ranks on one device, so --share-device is always gloo).  Utterances are independent, so no
+    device-side collective is on the data path; barriers and the max-over-ranks timing
+    are host scalars."""
+    if args.share_device or args.mock:
+        return "gloo"
+    return args.control_backend
 
 
 def launch_ranks(args):
@@ -110,7 +124,7 @@ def launch_ranks(args):
 def mock_main(args):
     """CPU rehearsal of the multi-rank step (--mock): the same shard / gather / barrier / max-over-ranks
     timing as main() over gloo, with stand-in token rows instead of the engine."""
-    rank, _, world, group = dist.setup("gloo")
+    rank, _, world, group = dist.setup(control_backend(args))
     lens = synthetic.devclean_lengths(args.qsl, seed=4)
     from rnnt_amd.sut import RNNTQSL
     qsl = RNNTQSL([None] * len(lens), lens)
@@ -158,6 +172,7 @@ def mock_main(args):
         print(json.dumps({"metric": METRIC, "value": None, "unit": "utterances/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                           "data": "mock: no engine, stand-in responses (launcher / sharding check, not a measurement)",
+                          "control_plane": dist.backend_name(),
                           "config": {"query_samples": query, "gathered": int(len(got[0]))}}), flush=True)
     if world > 1:
         import torch.distributed as tdist
@@ -209,37 +224,98 @@ def cpu_baseline(pm, qsl, batches, batch_engine, responses, n_sample, inflight):
     for i, q in enumerate(qidx):
         o = int(qsl.offsets[q])
         x[: sl[i], i, :240] = qsl.feats[o: o + int(sl[i])].cpu().numpy()
-    oracle.lib()
-    t0 = time.perf_counter()
-    f = oracle.encoder_i8(pm, x, sl)
-    res, rl, _ = oracle.greedy_decode(pm, f, (sl + 1) // 2, max_res=(500 // 2) * 30)
-    dt = time.perf_counter() - t0
+    import ctypes
+    lib = oracle.lib()
+    cpus, meta = host_cpu_budget()
+    arr = (ctypes.c_int * len(cpus))(*cpus)
+    lib.oracle_pin_threads.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    pinned = lib.oracle_pin_threads(len(cpus), arr)
+    lib.oracle_bind_master(cpus[0])
+    try:
+        t0 = time.perf_counter()
+        f = oracle.encoder_i8(pm, x, sl)
+        res, rl, _ = oracle.greedy_decode(pm, f, (sl + 1) // 2, max_res=(500 // 2) * 30)
+        dt = time.perf_counter() - t0
+    finally:
+        lib.oracle_bind_master(-1)
+    meta["threads_pinned"] = int(pinned)
     mism = 0
     for i, s in enumerate(sid):
         row = responses.get(int(s))
         if row is None or len(row) != int(rl[i]) or not np.array_equal(row, res[i, : rl[i]]):
             mism += 1
-    return dict(value=n / dt, seconds=dt, n=n, cores=oracle.lib().oracle_num_threads(), frames=int(sl.sum()),
+    return dict(value=n / dt, seconds=dt, n=n, cores=lib.oracle_num_threads(), frames=int(sl.sum()),
                 mismatches=mism, batches=sorted({b for b, _ in picks}),
-                engines=sorted({batch_engine[b] for b, _ in picks}))
+                engines=sorted({batch_engine[b] for b, _ in picks}), host=meta)
 
 
-def host_cpu_info():
-    """CPU model, the cores this process may run on and how it is pinned (cpu_baseline metadata)."""
-    model = None
+def _read(path):
     try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    model = line.split(":", 1)[1].strip()
-                    break
+        with open(path) as f:
+            return f.read().strip()
     except OSError:
-        pass
-    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
-    return {"cpu_model": model, "affinity_cpus": len(aff), "machine_cpus": os.cpu_count(),
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "pinning": "none: OpenMP threads over the process's CPU affinity set (no numactl; the GPU box grants a "
-                       "share of the host's cores)"}
+        return None
+
+
+def cgroup_cpu_quota():
+    """The cgroup CPU bandwidth limit of this process in CPUs (quota / period), or None when
+    unlimited / unreadable.  cgroup v2 (`cpu.max`) and v1 (`cpu.cfs_quota_us` / `cpu.cfs_period_us`),
+    at the namespace root and at the process's own cgroup path."""
+    paths = []
+    for line in (_read("/proc/self/cgroup") or "").splitlines():
+        parts = line.split(":", 2)
+        if len(parts) == 3:
+            ctl, rel = parts[1], parts[2]
+            if ctl == "":
+                paths.append(("v2", "/sys/fs/cgroup" + rel))
+            elif "cpu" in ctl.split(","):
+                for mnt in ("/sys/fs/cgroup/cpu", "/sys/fs/cgroup/cpu,cpuacct"):
+                    paths.append(("v1", mnt + rel))
+    paths += [("v2", "/sys/fs/cgroup"), ("v1", "/sys/fs/cgroup/cpu"), ("v1", "/sys/fs/cgroup/cpu,cpuacct")]
+    for kind, d in paths:
+        if kind == "v2":
+            v = _read(os.path.join(d, "cpu.max"))
+            if v:
+                q, _, per = v.partition(" ")
+                if q == "max":
+                    return None
+                return int(q) / int(per or 100000)
+        else:
+            q, per = _read(os.path.join(d, "cpu.cfs_quota_us")), _read(os.path.join(d, "cpu.cfs_period_us"))
+            if q is not None and per is not None:
+                return None if int(q) < 0 else int(q) / int(per)
+    return None
+
+
+def host_cpu_budget():
+    """The host CPUs this process can actually use: its affinity set, capped by the cgroup quota
+    (a GPU box grants a share of a many-core host: affinity may list every CPU while the quota
+    allows 16).  -> (cpus to pin one OpenMP thread each to, metadata).  CPUs are taken one per
+    physical core first (SMT siblings last), in affinity order."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    quota = cgroup_cpu_quota()
+    n = len(aff) if quota is None else max(1, min(len(aff), int(quota)))
+    env_threads = os.environ.get("OMP_NUM_THREADS")
+    seen, first, second = set(), [], []
+    for c in aff:
+        key = (_read(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"),
+               _read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id"))
+        (second if key in seen and key != (None, None) else first).append(c)
+        seen.add(key)
+    cpus = (first + second)[:n]
+    meta = {"affinity_cpus": len(aff), "machine_cpus": os.cpu_count(),
+            "cgroup_cpu_quota": round(quota, 3) if quota is not None else None,
+            "omp_num_threads_env": env_threads, "threads": n,
+            "pinning": f"one OpenMP thread per CPU (sched_setaffinity), CPUs {cpus[0]}..{cpus[-1]}" if len(cpus) > 1
+                       else f"one thread on CPU {cpus[0]}"}
+    return cpus, meta
+
+
+def host_cpu_model():
+    for line in (_read("/proc/cpuinfo") or "").splitlines():
+        if line.startswith("model name"):
+            return line.split(":", 1)[1].strip()
+    return None
 
 
 def wer_vs_fp32(n=1024, seed=44):
@@ -310,7 +386,7 @@ def main():
         return mock_main(args)
     dev = 0 if args.share_device else local
     torch.cuda.set_device(dev)
-    rank, local, world, ggroup = dist.setup("gloo" if args.share_device else "nccl")
+    rank, local, world, ggroup = dist.setup(control_backend(args))
     device = f"cuda:{dev}"
     pm, _ = weights.build_model()
     qsl = build_qsl(args.qsl, seed=4, device=device, wav=args.wav)
@@ -436,6 +512,7 @@ def main():
                    "batches_run_rank0": len(mine),
                    "encoder_frames_per_query_rank0": enc_frames, "emitted_symbols_per_query": emitted},
         "roofline": roofline,
+        "control_plane": dist.backend_name(),
     }
     if rank == 0 and got is not None:
         assert len(got[0]) == query and len(np.unique(got[0])) == query, "gathered responses do not cover the query"
@@ -448,7 +525,7 @@ def main():
         resp = responses_dict(*got)
         cb = cpu_baseline(pm, qsl, mine, batch_engine, resp, args.cpu_sample, args.inflight)
         out["cpu_baseline"] = {"value": round(cb["value"], 3), "unit": "utterances/s", "cores": cb["cores"],
-                               "kind": "port", **host_cpu_info(),
+                               "kind": "port", "cpu_model": host_cpu_model(), **cb["host"],
                                "sample": f"{cb['n']} utterances ({cb['frames']} frames) of the timed query (batches "
                                          f"{cb['batches']}, longest to shortest rows), int8 encoder + greedy decode, "
                                          f"{cb['seconds']:.1f} s"}

@@ -322,6 +322,10 @@ typedef struct {
 int rnnt_featurizer_create(const rnnt_featurizer_config* cfg, const float* window, const float* fb, int device,
                            rnnt_featurizer** out);
 void rnnt_featurizer_destroy(rnnt_featurizer* f);
+/* Dynamic LDS each fz_logmel workgroup requests so that it owns its CU (environment RNNT_FZ_OWN_CU=1 at
+ * create; 0 = off, the default).  A fallback guard beside the shipped one (no packed FP32 in any
+ * kernel); no reference counterpart. */
+size_t rnnt_featurizer_own_cu_lds(const rnnt_featurizer* f);
 /* Feature frames of a wav_len-sample utterance: ceil((1 + floor(wav_len/hop)) / 3), 0 for 0. */
 int64_t rnnt_featurizer_frames(int64_t wav_len);
 /* wav device fp32: row n's samples at wav + offsets[n] (offsets device int64 [n]) or, with

@@ -106,6 +106,8 @@ void oracle_prediction(int N, const int32_t* pre_g, const float* h, const float*
                        float* h_out, float* c_out);
 
 int oracle_num_threads(void);
+int oracle_pin_threads(int n, const int* cpus);
+int oracle_bind_master(int cpu);
 
 #ifdef __cplusplus
 }

@@ -346,6 +346,7 @@ struct rnnt_featurizer {
   std::vector<void*> allocs;
   int2* plan = nullptr;
   size_t plan_cap = 0;  // chunks
+  size_t own_cu_lds = 0;  // RNNT_FZ_OWN_CU=1: dynamic LDS that leaves no room for another workgroup on the CU
 };
 
 static int fz_fail(int code, const std::string& m) { return rnnt_internal_fail(code, m); }
@@ -370,6 +371,8 @@ extern "C" int64_t rnnt_featurizer_frames(int64_t wav_len) {
   if (wav_len <= 0) return 0;
   return (1 + wav_len / FZ_HOP + FZ_SPLICE - 1) / FZ_SPLICE;
 }
+
+static size_t own_cu_lds_bytes(int device);
 
 extern "C" int rnnt_featurizer_create(const rnnt_featurizer_config* cfg, const float* window, const float* fb,
                                       int device, rnnt_featurizer** out) {
@@ -447,6 +450,7 @@ extern "C" int rnnt_featurizer_create(const rnnt_featurizer_config* cfg, const f
   f->k.dither_sq = cfg->dither * cfg->dither;
   f->k.log_guard = cfg->log_guard;
   f->k.eps = cfg->norm_eps;
+  f->own_cu_lds = own_cu_lds_bytes(device);
   *out = f;
   return 0;
 }
@@ -459,10 +463,34 @@ extern "C" void rnnt_featurizer_destroy(rnnt_featurizer* f) {
   delete f;
 }
 
-static int launch_logmel(const FzArgs& a, size_t chunks, hipStream_t st) {
-  hipLaunchKernelGGL(fz_logmel_kernel, dim3((unsigned)((chunks + FZ_NSUB - 1) / FZ_NSUB)), dim3(NT * FZ_NSUB), 0, st, a);
+// RNNT_FZ_OWN_CU=1 (read at rnnt_featurizer_create): each fz_logmel workgroup requests the rest of its CU's
+// LDS as unused dynamic LDS, so no other kernel's workgroup shares the CU -- the round-3 guard against the
+// lanes-48-63 corruption beside decode workgroups, kept as a runtime switch behind the
+// shipped guard (no packed FP32 in any kernel).  Costs occupancy: one 4-wave chunk per CU.
+static size_t own_cu_lds_bytes(int device) {
+  const char* v = getenv("RNNT_FZ_OWN_CU");
+  if (!v || atoi(v) == 0) return 0;
+  int per_cu = 0;
+  if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess)
+    return 0;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fz_logmel_kernel)) != hipSuccess) return 0;
+  // more than half of what is left: a second workgroup of any kernel cannot fit beside it
+  const size_t left = (size_t)per_cu > fa.sharedSizeBytes ? (size_t)per_cu - fa.sharedSizeBytes : 0;
+  if (left == 0) return 0;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(fz_logmel_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)left) != hipSuccess)
+    return 0;
+  return left;
+}
+
+static int launch_logmel(const FzArgs& a, size_t chunks, size_t dyn_lds, hipStream_t st) {
+  hipLaunchKernelGGL(fz_logmel_kernel, dim3((unsigned)((chunks + FZ_NSUB - 1) / FZ_NSUB)), dim3(NT * FZ_NSUB),
+                     dyn_lds, st, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+extern "C" size_t rnnt_featurizer_own_cu_lds(const rnnt_featurizer* f) { return f ? f->own_cu_lds : 0; }
 
 // row_off == nullptr: padded [T_out][n_pad][256] output; else ragged rows (n_pad == n)
 static int featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* offsets, int64_t stride,
@@ -505,7 +533,7 @@ static int featurizer_run(rnnt_featurizer* f, const float* wav, const int64_t* o
   a.n_chunks = (int)chunks;
   if (chunks > 0) {
     hipLaunchKernelGGL(fz_plan_kernel, dim3(1), dim3(1024), 0, st, a);
-    if (launch_logmel(a, chunks, st)) return fz_fail(RNNT_EDEVICE, "fz_logmel launch failed");
+    if (launch_logmel(a, chunks, f->own_cu_lds, st)) return fz_fail(RNNT_EDEVICE, "fz_logmel launch failed");
   }
   if (n_pad > 0) hipLaunchKernelGGL(fz_norm_kernel, dim3(n_pad), dim3(NT), 0, st, a);
   FZCHK(hipGetLastError());

@@ -39,6 +39,9 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -77,16 +80,19 @@ void key_add(Key& k, const at::Tensor& t) {
 }
 
 // Concurrency (the reference's SUT runs up to INTER=28 worker threads through these ops at once on
-// shared read-only weights, rnnt_model.hpp:45-46, torch_sut.cpp:143-149): every (device, calling
-// thread) has its own engine, so calls from different threads share no mutable state and take no
-// lock.  An engine's weights are unpacked and uploaded the first time that thread passes a weight
-// set (keyed as above); an engine orders its own calls across streams by its state event.
-// Per-call padded inputs are staged in scratch tensors owned by the engine, one set per stream
-// (a buffer reused on another stream could be overwritten while the first stream still reads it),
-// grown on demand and never reallocated per call; inputs already in the engine's padded shape are
-// passed through without a copy.  Engines are never destroyed from thread-local destructors (HIP
-// calls at thread / process exit are unsafe); intel_mlperf_mi355x_release_thread_engines() frees
-// the calling thread's engines explicitly.
+// shared read-only weights, rnnt_model.hpp:45-46, torch_sut.cpp:143-149): every call leases an engine
+// from its device's pool for the duration of the call (Lease below), so concurrent calls share no
+// mutable state; the pool grows to the peak number of concurrent callers and no further, whatever
+// threads come and go (an engine is never owned by a thread, so nothing leaks when a thread exits).
+// A thread gets back the engine it used last when that one is idle, so a steady set of threads keeps
+// one engine each and no weights reload.  An engine's weights are unpacked and uploaded the first
+// time it sees a weight set (keyed as above).  Per-call padded inputs are staged in the engine's
+// scratch tensors (grown on demand, never reallocated per call; inputs already in the engine's
+// padded shape pass through without a copy); a call on another stream than the engine's previous
+// call first makes its stream wait for the end of that call (an event recorded at lease return), so
+// a staging copy never overwrites a buffer an earlier call's kernels still read.  Engines are
+// destroyed only by intel_mlperf_mi355x_release_engines() (idle engines; HIP calls at static
+// destruction are unsafe).
 struct Scratch {
   at::Tensor t[10];  // one slot per staged operand of each op (see the calls), so no op evicts another's
 };
@@ -94,29 +100,87 @@ struct OpEngine {
   rnnt_engine* e = nullptr;
   int max_batch = 0, max_frames = 0;
   Key enc[5], pred, pred32, joint1, joint2;
-  std::map<void*, Scratch> scratch;  // keyed by stream
+  Scratch scratch;
+  hipEvent_t done = nullptr;     // recorded on the last call's stream at lease return
+  void* last_stream = nullptr;
 };
-thread_local std::map<int, OpEngine*> t_eng;
+struct DevicePool {
+  std::mutex mu;
+  std::vector<OpEngine*> all, idle;
+};
+constexpr int MAX_DEV = 64;
+DevicePool g_pool[MAX_DEV];
+thread_local OpEngine* t_hint[MAX_DEV] = {};  // not owned: the engine this thread leased last per device
 thread_local int64_t t_loads = 0;  // weight-set (re)loads by this thread: intel_mlperf_mi355x_weight_loads()
 
-// This thread's engine on `dev` with room for n_pad rows and `frames` feature frames (recreated
-// larger on demand; its components then reload from the next call's weights).
-OpEngine& engine_for(int dev, int64_t n_pad, int64_t frames) {
-  OpEngine*& slot = t_eng[dev];
-  if (!slot) slot = new OpEngine{};
-  OpEngine& oe = *slot;
-  if (oe.e && n_pad <= oe.max_batch && frames <= oe.max_frames) return oe;
-  if (oe.e) rnnt_engine_destroy(oe.e);
-  oe = OpEngine{};
-  rnnt_opts o{};
-  o.max_batch = (int)std::max<int64_t>(round_up(n_pad, 256), 256);
-  o.max_frames = (int)std::max<int64_t>(frames, 500);
-  o.max_res = (o.max_frames / 2) * 30;
-  check_rc(rnnt_engine_create(nullptr, dev, &o, &oe.e), "engine create");
-  oe.max_batch = o.max_batch;
-  oe.max_frames = o.max_frames;
-  return oe;
+void destroy_engine(OpEngine* oe) {
+  if (oe->e) rnnt_engine_destroy(oe->e);
+  if (oe->done) (void)hipEventDestroy(oe->done);
+  delete oe;
 }
+
+// An engine of `dev` with room for n_pad rows and `frames` feature frames, exclusively the caller's
+// until the lease ends (recreated larger on demand; its components then reload from the next weights).
+class Lease {
+ public:
+  Lease(int dev, int64_t n_pad, int64_t frames, void* stream) : dev_(dev), stream_(stream) {
+    TORCH_CHECK(dev >= 0 && dev < MAX_DEV, "intel_mlperf: device index ", dev);
+    DevicePool& pool = g_pool[dev];
+    {
+      std::lock_guard<std::mutex> g(pool.mu);
+      auto it = std::find(pool.idle.begin(), pool.idle.end(), t_hint[dev]);
+      if (it == pool.idle.end() && !pool.idle.empty()) it = pool.idle.end() - 1;
+      if (it != pool.idle.end()) {
+        oe_ = *it;
+        pool.idle.erase(it);
+      } else {
+        oe_ = new OpEngine{};
+        pool.all.push_back(oe_);
+      }
+    }
+    t_hint[dev] = oe_;
+    try {
+      if (!oe_->e || n_pad > oe_->max_batch || frames > oe_->max_frames) {
+        // the old scratch goes back to torch's allocator: no earlier call may still read it
+        if (oe_->done && oe_->last_stream) (void)hipEventSynchronize(oe_->done);
+        if (oe_->e) rnnt_engine_destroy(oe_->e);
+        hipEvent_t ev = oe_->done;
+        *oe_ = OpEngine{};
+        oe_->done = ev;
+        rnnt_opts o{};
+        o.max_batch = (int)std::max<int64_t>(round_up(n_pad, 256), 256);
+        o.max_frames = (int)std::max<int64_t>(frames, 500);
+        o.max_res = (o.max_frames / 2) * 30;
+        check_rc(rnnt_engine_create(nullptr, dev, &o, &oe_->e), "engine create");
+        oe_->max_batch = o.max_batch;
+        oe_->max_frames = o.max_frames;
+      }
+      if (!oe_->done) TORCH_CHECK(hipEventCreateWithFlags(&oe_->done, hipEventDisableTiming) == hipSuccess, "event create");
+      if (oe_->last_stream && oe_->last_stream != stream_)
+        TORCH_CHECK(hipStreamWaitEvent((hipStream_t)stream_, oe_->done, 0) == hipSuccess, "stream wait");
+    } catch (...) {
+      give_back();
+      throw;
+    }
+  }
+  ~Lease() { give_back(); }
+  OpEngine& operator*() { return *oe_; }
+  Lease(const Lease&) = delete;
+  Lease& operator=(const Lease&) = delete;
+
+ private:
+  void give_back() {
+    if (!oe_) return;
+    if (oe_->done && hipEventRecord(oe_->done, (hipStream_t)stream_) == hipSuccess) oe_->last_stream = stream_;
+    DevicePool& pool = g_pool[dev_];
+    std::lock_guard<std::mutex> g(pool.mu);
+    pool.idle.push_back(oe_);
+    oe_ = nullptr;
+  }
+  int dev_;
+  void* stream_;
+  OpEngine* oe_ = nullptr;
+};
 
 void* stream_of(const at::Tensor& t) { return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
@@ -125,11 +189,16 @@ void* stream_of(const at::Tensor& t) { return (void*)c10::hip::getCurrentHIPStre
 // an earlier call's rows, which is harmless: every op here computes rows independently and the
 // padding rows' outputs are discarded.
 at::Tensor scratch(OpEngine& oe, void* stream, int i, at::IntArrayRef sizes, const at::TensorOptions& opt) {
-  at::Tensor& s = oe.scratch[stream].t[i];
+  (void)stream;  // one set per engine: the lease orders a new stream behind the engine's previous call
+  at::Tensor& s = oe.scratch.t[i];
   int64_t n = 1;
   for (auto v : sizes) n *= v;
-  if (!s.defined() || s.numel() < n || s.scalar_type() != opt.dtype().toScalarType() || s.device() != opt.device())
+  if (!s.defined() || s.numel() < n || s.scalar_type() != opt.dtype().toScalarType() || s.device() != opt.device()) {
+    // the old buffer goes back to torch's allocator (free for reuse on the stream it was allocated on):
+    // the engine's earlier calls, on whatever streams, must be done with it first
+    if (s.defined() && oe.done && oe.last_stream) (void)hipEventSynchronize(oe.done);
     s = at::zeros({n}, opt);
+  }
   return s.narrow(0, 0, n).view(sizes);
 }
 
@@ -223,7 +292,8 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
   TORCH_CHECK(skip_quant_y == (first + L == 5), "lstm_amx_int8: skip_quant_y is set exactly for post_rnn");
   const int64_t T = x.size(0), N = x.size(1), n_pad = round_up(N, 256);
   const int dev = x.device().index();
-  OpEngine& oe = engine_for(dev, n_pad, pre ? T : 2 * T);
+  Lease lease(dev, n_pad, pre ? T : 2 * T, stream_of(x));
+  OpEngine& oe = *lease;
   std::vector<float> rb, ins, outs;  // read (a host copy) only when a layer (re)loads
   for (int i = 0; i < L; ++i) {
     const int l = first + i;
@@ -289,7 +359,8 @@ at::Tensor stack_time(const at::Tensor& x, const at::Tensor& x_lens, int64_t fac
   TORCH_CHECK(factor == 2, "stack_time: factor 2");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kChar && x.dim() == 3, "stack_time: int8 [T, N, C] on the GPU");
   const int64_t T = x.size(0), N = x.size(1), C = x.size(2), n_pad = round_up(N, 16);
-  OpEngine& oe = engine_for(x.device().index(), 256, 500);
+  Lease lease(x.device().index(), 256, 500, stream_of(x));
+  OpEngine& oe = *lease;
   void* st = stream_of(x);
   const at::Tensor xin = staged(oe, st, 1, x, T, N, n_pad, C, at::kChar);
   const at::Tensor lens = staged(oe, st, 2, x_lens.to(x.device(), at::kInt), 1, N, n_pad, 1, at::kInt);
@@ -310,7 +381,8 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_am
   TORCH_CHECK(weights.size() == 2 && hx.size() == 2 && cx.size() == 2, "lstm_amx_bf16: 2 layers");
   const at::Tensor x2 = x.reshape({-1, P});
   const int64_t N = x2.size(0), n_pad = round_up(N, 16);
-  OpEngine& oe = engine_for(x.device().index(), n_pad, 500);
+  Lease lease(x.device().index(), n_pad, 500, stream_of(x));
+  OpEngine& oe = *lease;
   Key k;
   for (int l = 0; l < 2; ++l)
     for (int j = 0; j < 4; ++j) key_add(k, weights.get(l).get(j));
@@ -367,7 +439,8 @@ at::Tensor amx_linear_bf16_accum_relu(const at::Tensor& f, const at::Tensor& w1_
   const at::Tensor f2 = f.reshape({-1, H}), g2 = g.reshape({-1, P});
   const int64_t N = f2.size(0), n_pad = round_up(N, 16);
   TORCH_CHECK(g2.size(0) == N, "amx_linear_bf16_accum_relu: f / g rows");
-  OpEngine& oe = engine_for(f.device().index(), n_pad, 500);
+  Lease lease(f.device().index(), n_pad, 500, stream_of(f));
+  OpEngine& oe = *lease;
   Key k;
   key_add(k, w1_trans);
   key_add(k, w1_pred);
@@ -394,7 +467,8 @@ at::Tensor amx_linear_bf16_accum_relu(const at::Tensor& f, const at::Tensor& w1_
 at::Tensor amx_linear_i16o32(const at::Tensor& y, const at::Tensor& w2, const at::Tensor& b2) {
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.size(1) == J, "amx_linear_i16o32: y bf16 [N, 512] on the GPU");
   const int64_t N = y.size(0), n_pad = round_up(N, 16);
-  OpEngine& oe = engine_for(y.device().index(), n_pad, 500);
+  Lease lease(y.device().index(), n_pad, 500, stream_of(y));
+  OpEngine& oe = *lease;
   Key k;
   key_add(k, w2);
   key_add(k, b2);
@@ -444,7 +518,8 @@ bool greedy_decode_update(const at::Tensor& symbols, const at::Tensor& symbols_a
     chg[l] = (const uint16_t*)hg[l].data_ptr();
     ccg[l] = cg[l].data_ptr<float>();
   }
-  OpEngine& oe = engine_for(symbols.device().index(), 256, 500);
+  Lease lease(symbols.device().index(), 256, 500, stream_of(symbols));
+  OpEngine& oe = *lease;
   const int rc = rnnt_op_greedy_update(oe.e, symbols.data_ptr(), symbols.scalar_type() == at::kLong,
                                        symbols_added.data_ptr<int32_t>(), res.data_ptr<int32_t>(),
                                        res_idx.data_ptr<int32_t>(), f.data_ptr<float>(), (int)f.size(1),
@@ -471,7 +546,8 @@ std::tuple<at::Tensor, std::vector<at::Tensor>, std::vector<at::Tensor>> lstm_f3
   TORCH_CHECK(weights.size() == 2 && hx.size() == 2 && cx.size() == 2, "lstm: the 2-layer prediction LSTM");
   const at::Tensor x2 = x.reshape({-1, P});
   const int64_t N = x2.size(0), n_pad = round_up(N, 64);
-  OpEngine& oe = engine_for(x.device().index(), n_pad, 500);
+  Lease lease(x.device().index(), n_pad, 500, stream_of(x));
+  OpEngine& oe = *lease;
   Key k;
   for (int l = 0; l < 2; ++l)
     for (int j = 0; j < 4; ++j) key_add(k, weights.get(l).get(j));
@@ -582,16 +658,36 @@ void boxed_not_served(const c10::OperatorHandle& op, torch::jit::Stack*) {
 
 }  // namespace
 
-// Diagnostics of the engine cache (not part of the reference's operator surface): weight-set loads
-// performed by the calling thread, and release of the calling thread's engines.
+// Diagnostics of the engine pool (not part of the reference's operator surface): weight-set loads
+// performed by the calling thread, the engines a device's pool holds, and release of the idle ones.
 extern "C" int64_t intel_mlperf_mi355x_weight_loads(void) { return t_loads; }
-extern "C" void intel_mlperf_mi355x_release_thread_engines(void) {
-  for (auto& kv : t_eng) {
-    if (kv.second->e) rnnt_engine_destroy(kv.second->e);
-    delete kv.second;
-  }
-  t_eng.clear();
+extern "C" int intel_mlperf_mi355x_engine_count(int dev) {
+  if (dev < 0 || dev >= MAX_DEV) return -1;
+  std::lock_guard<std::mutex> g(g_pool[dev].mu);
+  return (int)g_pool[dev].all.size();
 }
+// Destroys every idle engine of every device (engines leased by a running call stay); -> engines freed.
+extern "C" int intel_mlperf_mi355x_release_engines(void) {
+  int freed = 0;
+  for (int d = 0; d < MAX_DEV; ++d) {
+    DevicePool& pool = g_pool[d];
+    std::vector<OpEngine*> idle;
+    {
+      std::lock_guard<std::mutex> g(pool.mu);
+      idle.swap(pool.idle);
+      for (OpEngine* oe : idle) pool.all.erase(std::find(pool.all.begin(), pool.all.end(), oe));
+    }
+    for (OpEngine* oe : idle) {
+      if (oe->done) (void)hipEventSynchronize(oe->done);
+      destroy_engine(oe);
+      ++freed;
+    }
+  }
+  for (auto& h : t_hint) h = nullptr;
+  return freed;
+}
+// round-4 name, kept for callers of the thread-owned engines: releases the idle pool engines
+extern "C" void intel_mlperf_mi355x_release_thread_engines(void) { (void)intel_mlperf_mi355x_release_engines(); }
 
 TORCH_LIBRARY(intel_mlperf, m) {
   m.def("lstm_amx_int8(Tensor x, Tensor[] hx, Tensor[] cx, Tensor[][] weights, Tensor rb_scale, Tensor in_scale, "

@@ -57,6 +57,7 @@ _SIGS = {
                                          C.POINTER(C.c_void_p)]),
     "rnnt_featurizer_destroy": (None, [C.c_void_p]),
     "rnnt_featurizer_frames": (C.c_int64, [C.c_int64]),
+    "rnnt_featurizer_own_cu_lds": (C.c_size_t, [C.c_void_p]),
     "rnnt_featurizer_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "rnnt_featurizer_run_rows": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,

@@ -12,8 +12,9 @@ fewer of them.  ``shard_query`` (a static snake deal) is kept as the alternative
 token rows to rank 0's host as its batches complete, where the one LoadGen instance would
 complete them (the reference's single QuerySamplesComplete point,
 torch_sut.cpp:221-236).  The gather runs over a gloo (host) group -- the responses are host
-data after the per-batch D2H copy, so no device-side collective is involved (RCCL stays for the
-control plane: barriers and timing reductions).
+data after the per-batch D2H copy, so no device-side collective is involved.  The control plane
+(barriers, timing reductions, claims) is gloo as well by default (bench.py --control-backend;
+RCCL is opt-in: nothing on the data path needs a device collective).
 """
 import os
 
@@ -231,6 +232,14 @@ class ResponseStream:
         return tuple(np.concatenate([g[k] for g in self._got]) for k in range(3))
 
 
+def backend_name():
+    """The default group's backend ("gloo" / "nccl"), or None on a single process."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return str(dist.get_backend())
+    return None
+
+
 def barrier(group=None):
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
@@ -261,4 +270,4 @@ def reduce_sum(x, group=None):
 
 
 __all__ = ["setup", "shard_query", "BatchClaim", "claim_for_query", "query_arrays", "QuerySample", "gather_responses", "ResponseStream", "pack_responses",
-           "unpack_responses", "barrier", "reduce_max", "reduce_sum", "batch_bounds", "env_rank"]
+           "unpack_responses", "backend_name", "barrier", "reduce_max", "reduce_sum", "batch_bounds", "env_rank"]

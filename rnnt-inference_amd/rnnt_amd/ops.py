@@ -44,8 +44,9 @@ def load_library(path=OPS_LIB):
 
 
 def op_weight_loads():
-    """Weight-set loads the operator library has done for the calling thread (each (device,
-    thread) has its own engine; a changed weight tensor reloads).  Diagnostics, not a reference op."""
+    """Weight-set loads the operator library has done for the calling thread (an engine loads a
+    weight set the first time it sees it; a changed weight tensor reloads).  Diagnostics, not a
+    reference op."""
     import ctypes
     load_library()
     f = ctypes.CDLL(OPS_LIB).intel_mlperf_mi355x_weight_loads
@@ -53,12 +54,30 @@ def op_weight_loads():
     return int(f())
 
 
-def release_thread_engines():
-    """Free the calling thread's operator-library engines (device memory); the next op call on this
-    thread creates and loads a new one."""
+def op_engine_count(device=0):
+    """Engines in the operator library's pool of `device`: the peak number of concurrent op calls
+    seen there (calls lease an engine each; threads own none)."""
     import ctypes
     load_library()
-    ctypes.CDLL(OPS_LIB).intel_mlperf_mi355x_release_thread_engines()
+    f = ctypes.CDLL(OPS_LIB).intel_mlperf_mi355x_engine_count
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int]
+    return int(f(int(device)))
+
+
+def release_engines():
+    """Free the operator library's idle engines on every device (device memory); the next op call
+    creates and loads a new one.  -> engines freed."""
+    import ctypes
+    load_library()
+    f = ctypes.CDLL(OPS_LIB).intel_mlperf_mi355x_release_engines
+    f.restype = ctypes.c_int
+    return int(f())
+
+
+def release_thread_engines():
+    """Round-4 name of release_engines (engines are no longer owned by threads)."""
+    release_engines()
 
 
 def lstm_amx_int8(x, hx, cx, weights, rb_scale, in_scale, out_scale, skip_quant_y):

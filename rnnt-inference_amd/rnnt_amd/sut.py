@@ -278,40 +278,60 @@ class OfflineSUT:
         return rlh, res[:, : max(1, int(rlh.max()))].cpu().numpy()
 
     def _run_batch(self, eng, ids, idx, bi=0, gate=None):
-        st = self._stream_for(eng)
+        """One batch on `eng`: wait for this device's encode turn, encode, hand the turn and the
+        encode gate on, decode, complete.  The turn and the gate are handed on exactly once on every
+        path -- also when getting the stream, the device scope or the turn wait raises (ADVICE r04:
+        a gate held by a failed worker would block the device's other workers forever)."""
         n = len(ids)
         n_pad = pad_batch(n)
-        with self._device_scope(eng, st):
-            # encoders on one GPU take turns in batch order (longest first): the longest batch's
-            # decode overlaps the most encoding, and the last encode is the shortest batch's.  Every
-            # step after the wait is under the finally, so a failing batch still hands the turn on.
-            cv, turn = self._enc_turns[eng.device]
+        cv, turn = self._enc_turns[eng.device]
+        handed = [False]
+        encoded = [False]
+
+        def hand_on():
+            if handed[0]:
+                return
+            handed[0] = True
             with cv:
-                cv.wait_for(lambda: turn[0] == bi)
-                self.encode_order.append(bi)
-            encoded = False
-            try:
-                enc = self._encode(eng, st, ids, idx, n, n_pad)
-                encoded = True
-            finally:
-                with cv:
+                if turn and turn[0] == bi:
                     turn.popleft()
-                    cv.notify_all()
-                if gate is not None:  # the device's encoder is free: the next claim may go
-                    gate.release()
-                h = self._hold
-                if h is not None:  # counted even when the encode raised, so the held decodes never wait forever
-                    with h["cv"]:
-                        h["done"] += 1
-                        h["failed"] = h["failed"] or not encoded
-                        h["cv"].notify_all()
+                else:  # failed before our turn came: drop our place so later batches are not blocked
+                    try:
+                        turn.remove(bi)
+                    except ValueError:
+                        pass
+                cv.notify_all()
+            if gate is not None:  # the device's encoder is free: the next claim may go
+                gate.release()
             h = self._hold
-            if h is not None and bi >= h["k"]:
+            if h is not None:  # counted even when the encode raised, so the held decodes never wait forever
                 with h["cv"]:
-                    h["cv"].wait_for(lambda: h["done"] == h["nb"] or h["failed"])
-                    if h["failed"]:
-                        raise RuntimeError("OfflineSUT: an encode of this query failed; held decode abandoned")
-            rlh, toks = self._decode(eng, st, enc)
+                    h["done"] += 1
+                    h["failed"] = h["failed"] or not encoded[0]
+                    h["cv"].notify_all()
+
+        try:
+            st = self._stream_for(eng)
+            with self._device_scope(eng, st):
+                # encoders on one GPU take turns in batch order (longest first): the longest batch's
+                # decode overlaps the most encoding, and the last encode is the shortest batch's
+                with cv:
+                    cv.wait_for(lambda: turn[0] == bi)
+                    self.encode_order.append(bi)
+                try:
+                    enc = self._encode(eng, st, ids, idx, n, n_pad)
+                    encoded[0] = True
+                finally:
+                    hand_on()
+                h = self._hold
+                if h is not None and bi >= h["k"]:
+                    with h["cv"]:
+                        h["cv"].wait_for(lambda: h["done"] == h["nb"] or h["failed"])
+                        if h["failed"]:
+                            raise RuntimeError("OfflineSUT: an encode of this query failed; held decode abandoned")
+                rlh, toks = self._decode(eng, st, enc)
+        finally:
+            hand_on()
         self.query_samples_complete(ids, idx, toks, rlh)
 
     def query_samples_complete(self, ids, idx, toks, lens):

@@ -68,7 +68,7 @@ def _worker(rank, world, port, slow_rank, queries, q):
     lengths = np.random.default_rng(5).integers(47, 501, 900).astype(np.int32)
     qsl = RNNTQSL([None] * len(lengths), lengths)
     ids, idx = rdist.query_arrays(len(lengths), 3000)
-    slow = 6.0 if rank == slow_rank else 1.0
+    slow = 20.0 if rank == slow_rank else 1.0
     sut = _HostSUT([_HostEngine(0, slow) for _ in range(2)], qsl)
     out = []
     for qn in range(queries):
@@ -107,9 +107,10 @@ def _check(outs, world, slow_rank, queries):
         claimed = [outs[r][qn][0] for r in range(world)]
         flat = sorted(i for c in claimed for i in c)
         assert flat == list(range(30)), "every batch claimed exactly once"
-        # longest first: each rank's claims are increasing and every rank takes part
-        for c in claimed:
-            assert c == sorted(c) and len(c) > 0
+        # longest first: each rank's claims are increasing and every fast rank takes part (the slowed
+        # one may start after the others took every batch of a query)
+        for r, c in enumerate(claimed):
+            assert c == sorted(c) and (len(c) > 0 or r == slow_rank)
         gids, glens, gtoks = outs[0][qn][2]
         assert sorted(gids) == list(range(3000))
         off = 0
@@ -118,10 +119,11 @@ def _check(outs, world, slow_rank, queries):
             off += L
         assert off == len(gtoks)
         assert all(outs[r][qn][2] is None for r in range(1, world))
-    # the slowed rank sheds work to the others
+    # the slowed rank (20x) sheds work to the others: a weak ordering, so a loaded runner's schedule
+    # cannot break it; exactly-once and the payloads above are the strict checks
     fr = {r: sum(outs[r][qn][1] for qn in range(queries)) for r in range(world)}
     fast = [fr[r] for r in range(world) if r != slow_rank]
-    assert fr[slow_rank] < 0.6 * min(fast), fr
+    assert fr[slow_rank] < min(fast), fr
 
 
 def test_dynamic_claims_two_ranks_one_slow():
@@ -142,3 +144,42 @@ def test_batch_claim_counter_semantics():
     st.set_timeout(datetime.timedelta(seconds=5))
     a, b = rdist.BatchClaim(st, "k0", 3), rdist.BatchClaim(st, "k1", 1)
     assert [a(), a(), b(), a(), a(), b()] == [0, 1, 0, 2, None, None]
+
+
+def test_failing_batch_releases_the_encode_gate():
+    """a worker whose batch fails before its encode starts (here: entering the device
+    scope raises) must still hand the device's encode gate and its turn on, so issue_batches raises
+    the error instead of the device's other workers blocking on the gate forever."""
+    import datetime
+    import threading
+    from torch.distributed import HashStore
+
+    class _Failing(_HostSUT):
+        calls = 0
+
+        def _device_scope(self, eng, st):
+            type(self).calls += 1
+            if type(self).calls == 2:
+                raise RuntimeError("injected device-scope failure")
+            return contextlib.nullcontext()
+
+    lengths = np.random.default_rng(6).integers(47, 501, 300).astype(np.int32)
+    qsl = RNNTQSL([None] * len(lengths), lengths)
+    ids, idx = rdist.query_arrays(len(lengths), 600)
+    batches = make_batches(qsl, ids, idx, 100)
+    st = HashStore()
+    st.set_timeout(datetime.timedelta(seconds=5))
+    sut = _Failing([_HostEngine(0, 0.01) for _ in range(3)], qsl)
+    err = []
+
+    def run():
+        try:
+            sut.issue_batches(batches, claim=rdist.BatchClaim(st, "q", len(batches)))
+        except RuntimeError as e:
+            err.append(e)
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    t.join(timeout=60)
+    assert not t.is_alive(), "issue_batches hung after a failed batch (encode gate never released)"
+    assert err and "injected" in str(err[0])

@@ -276,3 +276,25 @@ def test_featurizer_beside_concurrent_decode():
         assert bad == 0, f"{bad} of {iters} featurizer batches differ from the quiet result beside {decodes[0]} decodes"
     finally:
         eng.close()
+
+
+def test_own_cu_switch_same_features(fz, monkeypatch):
+    """RNNT_FZ_OWN_CU=1: the round-3 CU-owning LDS request, kept as a runtime fallback
+    behind the shipped guard (no packed FP32 in any kernel).  Off by default; on, the logmel launch
+    requests the rest of the CU's LDS and the features are bit-identical to the default build's."""
+    from rnnt_amd import _lib
+    from rnnt_amd.featurizer import AudioProcessing
+    assert _lib.lib().rnnt_featurizer_own_cu_lds(fz._h) == 0
+    monkeypatch.setenv("RNNT_FZ_OWN_CU", "1")
+    own = AudioProcessing("quant", **INPUT_EVAL).featurizer
+    try:
+        assert _lib.lib().rnnt_featurizer_own_cu_lds(own._h) > 0
+        wavs = synthetic.make_wavs(LENS, seed=23)
+        x, lens = _batch(wavs)
+        a, la = fz.featurize(x, lens.cuda(), lens.numpy(), n_pad=16, T_out=505)
+        b, lb = own.featurize(x, lens.cuda(), lens.numpy(), n_pad=16, T_out=505)
+        torch.cuda.synchronize()
+        assert torch.equal(la, lb)
+        assert np.array_equal(a.cpu().numpy().view(np.uint32), b.cpu().numpy().view(np.uint32))
+    finally:
+        own.close()

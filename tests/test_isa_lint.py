@@ -82,8 +82,8 @@ def test_lint_sees_through_shl_or():
 
 def _ir(src, out):
     flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only", "-S", "-emit-llvm"]
-    if os.path.basename(src) == "encoder.hip":
-        flags.append("-fno-slp-vectorize")
+    if os.path.dirname(os.path.abspath(src)) == CSRC:
+        flags += _nopk_flags()
     subprocess.run([HIPCC, *flags, src, "-o", out], check=True, cwd=CSRC, capture_output=True)
     return open(out).read()
 
@@ -108,22 +108,70 @@ def test_no_masked_wide_multiply_in_kernels():
     assert not bad, f"masked 24-bit values in 64-bit multiplies (miscompiled by ROCm 7.2): {bad}"
 
 
-def test_featurizer_has_no_packed_fp32():
-    """featurizer.hip is built with -fno-slp-vectorize (Makefile): packed FP32 VALU
-    (v_pk_add / mul / fma_f32) in fz_logmel's FFT gave wrong results in lanes 48-63 of a wave while
-    decode step kernels shared the CU (tools/r04_fzdiag.sh, the corrupted frames move
-    with those lanes; without packed FP32 0 of ~100k batches).  The gfx950 ISA of the file, built
-    with the Makefile's flags, must not contain them."""
+PACKED_FP32 = re.compile(r"^\s*(v_pk_(?:add|mul|fma)_f32)\b", re.M)
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _nopk_flags():
+    mk = open(os.path.join(CSRC, "Makefile")).read()
+    m = re.search(r"^NOPK := (.+)$", mk, re.M)
+    assert m, "Makefile lost NOPK"
+    assert re.search(r"^FLAGS := .*\$\(NOPK\)", mk, re.M), "NOPK is not in every kernel's FLAGS"
+    return m.group(1).split()
+
+
+def test_no_packed_fp32_in_any_kernel_source():
+    """Every kernel source, compiled with the Makefile's NOPK flags, has no packed FP32 VALU
+    (v_pk_add / mul / fma_f32).  In fz_logmel's FFT they gave wrong results in lanes 48-63 of a wave
+    while decode step kernels shared the CU (the corrupted frames move with those
+    lanes; without packed FP32 0 of ~100k batches); any kernel may share a CU with the featurizer, so
+    none carries them."""
     if not shutil.which(HIPCC) and not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    mk = open(os.path.join(CSRC, "Makefile")).read()
-    assert re.search(r"^featurizer\.o: FLAGS \+= -fno-slp-vectorize", mk, re.M), "Makefile lost the featurizer flag"
+    flags = _nopk_flags()
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+    def isa(src):
+        with tempfile.TemporaryDirectory() as td:
+            out = os.path.join(td, "k.s")
+            subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-w", *flags,
+                            "--cuda-device-only", "-S", os.path.basename(src), "-o", out],
+                           check=True, cwd=CSRC, capture_output=True)
+            return open(out).read()
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        isas = dict(zip(srcs, ex.map(isa, srcs)))
+    assert "fz_logmel_kernel" in isas[os.path.join(CSRC, "featurizer.hip")]
+    bad = {os.path.basename(s): sorted(set(PACKED_FP32.findall(t))) for s, t in isas.items()}
+    bad = {k: v for k, v in bad.items() if v}
+    assert not bad, f"packed FP32 in kernel ISA: {bad}"
+    # the flag is what removes them: without it the decoder has some (so the check can fail)
     with tempfile.TemporaryDirectory() as td:
-        out = os.path.join(td, "fz.s")
+        out = os.path.join(td, "d.s")
         subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-w",
-                        "-fno-slp-vectorize", "--cuda-device-only", "-S", "featurizer.hip", "-o", out],
-                       check=True, cwd=CSRC, capture_output=True)
-        isa = open(out).read()
-    assert "fz_logmel_kernel" in isa
-    hits = re.findall(r"^\s*(v_pk_(?:add|mul|fma)_f32)\b", isa, re.M)
-    assert not hits, f"packed FP32 in featurizer.hip's ISA: {sorted(set(hits))}"
+                        "--cuda-device-only", "-S", "decoder.hip", "-o", out], check=True, cwd=CSRC, capture_output=True)
+        assert PACKED_FP32.search(open(out).read())
+
+
+def test_no_packed_fp32_in_built_objects():
+    """The objects linked into librnnt_mi355x.so (what ships to the GPU box) carry no packed FP32:
+    each object's gfx950 code object is unbundled from .hip_fatbin and disassembled."""
+    objs = sorted(glob.glob(os.path.join(CSRC, "*.o")))
+    if not objs or not os.path.exists(os.path.join(LLVM, "clang-offload-bundler")):
+        pytest.skip("library not built here")
+    srcs = {os.path.splitext(os.path.basename(p))[0] for p in glob.glob(os.path.join(CSRC, "*.hip"))}
+    assert srcs <= {os.path.splitext(os.path.basename(p))[0] for p in objs}, "some kernel objects are not built"
+    bad = {}
+    with tempfile.TemporaryDirectory() as td:
+        for o in objs:
+            b, co = os.path.join(td, "x.bundle"), os.path.join(td, "x.co")
+            subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={b}", o], check=True, capture_output=True)
+            subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={b}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+            dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", co], check=True, capture_output=True,
+                                 text=True).stdout
+            assert "s_endpgm" in dis
+            hits = sorted(set(re.findall(r"\b(v_pk_(?:add|mul|fma)_f32)\b", dis)))
+            if hits:
+                bad[os.path.basename(o)] = hits
+    assert not bad, f"packed FP32 in built objects (rebuild: make -C {CSRC}): {bad}"

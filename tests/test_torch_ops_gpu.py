@@ -264,3 +264,49 @@ def test_ops_concurrent_threads_equal_serial(pm, W):
             assert torch.equal(a[0].cpu(), b[0].cpu())
             for u, v in zip(a[1] + a[2], b[1] + b[2]):
                 assert torch.equal(u.cpu(), v.cpu())
+
+
+def test_short_lived_threads_do_not_grow_the_pool(pm, W):
+    """engines were owned by (device, thread) and leaked when threads exited.  Now each
+    call leases one from the device's pool: 24 short-lived threads, one call each, one after the
+    other, leave the pool at the size it had (at most one new engine) and device memory flat; 4 at
+    a time grow it to at most 4 more.  release_engines frees the idle ones."""
+    import threading
+    N = 16
+    gen = torch.Generator().manual_seed(43)
+    g = torch.randn((1, N, 320), generator=gen).to(torch.bfloat16).cuda()
+    hx = [torch.zeros((N, 320), dtype=torch.bfloat16, device="cuda") for _ in range(2)]
+    cx = [torch.zeros((N, 320), dtype=torch.float32, device="cuda") for _ in range(2)]
+    want = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0].cpu()
+    torch.cuda.synchronize()
+    n0 = ops.op_engine_count(0)
+    free0 = torch.cuda.mem_get_info()[0]
+    errs = []
+
+    def one():
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                out = torch.ops.intel_mlperf.lstm_amx_bf16(g, hx, cx, W["pred"])[0]
+                torch.cuda.current_stream().synchronize()
+            assert torch.equal(out.cpu(), want)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    for _ in range(24):
+        t = threading.Thread(target=one)
+        t.start()
+        t.join()
+    assert not errs, errs
+    assert ops.op_engine_count(0) <= n0 + 1
+    torch.cuda.synchronize()
+    assert torch.cuda.mem_get_info()[0] >= free0 - (256 << 20), "device memory grew with short-lived threads"
+    for _ in range(3):
+        th = [threading.Thread(target=one) for _ in range(4)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    assert not errs, errs
+    assert ops.op_engine_count(0) <= n0 + 4
+    ops.release_engines()
+    assert ops.op_engine_count(0) == 0
