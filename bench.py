@@ -470,7 +470,7 @@ def main():
         "achieved": round(achieved, 2), "peak": INT8_DENSE_PEAK_TOPS, "unit": "TFLOP/s",
         "frac": round(achieved / INT8_DENSE_PEAK_TOPS, 4), "traffic": traffic,
         "traffic_source": ("HBM bytes per tick launch, rocprofv3 PMC pass of this round's profile "
-                           "(tools/profile_round.sh; (2 FETCH_SIZE + WRITE_SIZE) x 1024): " + str(traffic_src))
+                           "(tools/gpu.sh profile; (2 FETCH_SIZE + WRITE_SIZE) x 1024): " + str(traffic_src))
         if traffic is not None else None,
         "measured_on": "HIP events around every encode call on its own stream, timed region (encode overlaps "
                        "other batches' decode); rank 0's share of the query",

@@ -42,7 +42,15 @@ def _tensor(seed, key_id, shape, scale):
 # the strength of the planted "label already emitted" suppression (see _plant_anti_repeat)
 RECIPE = dict(enc=4.0 / 32.0, pred=2.0 / np.sqrt(320.0), embed=1.7, fc1=0.1 * np.sqrt(3.0),
               fc1_b=0.05, fc2=0.3 * np.sqrt(3.0), fc2_b=0.1, blank_bias=13.0, anti_repeat=2.0,
-              fc1_pred_noise=0.2)
+              fc1_pred_noise=0.2, fc1_pred_scale=1.0)
+
+
+# A checkpoint whose joint is decided by the encoder frame alone (prediction half x0.3, no planted
+# anti-repeat prior, blank bias 7): on some frames one non-blank label wins every time, so the
+# frame emits max_symbols_per_step (30) symbols and the cap forces the advance
+# (reference decoder.py:131-136, 153-167); other frames are blank.  tests/golden/make_golden.py
+# asserts that the reference's greedy_decode_f32 hits the cap on it.
+CAP_RECIPE = dict(anti_repeat=0.0, fc1_pred_scale=0.3, blank_bias=7.0)
 
 
 def _plant_anti_repeat(sd, gamma, noise):
@@ -115,6 +123,8 @@ def make_checkpoint(seed=DEFAULT_SEED, recipe=None):
     sd["joint_net.3.bias"][R.BLANK] += np.float32(rc["blank_bias"])
     if rc["anti_repeat"]:
         _plant_anti_repeat(sd, rc["anti_repeat"], rc["fc1_pred_noise"])
+    if rc["fc1_pred_scale"] != 1.0:  # weaken (or strengthen) the prediction network's say in the joint
+        sd["joint_net.0.weight"][:, H:] *= np.float32(rc["fc1_pred_scale"])
     return sd
 
 

@@ -184,6 +184,48 @@ def main():
                                  zs[:2], zs[:2], zs[2:], zs[2:])
         out["a_fq_f"] = f.numpy()
     print("fake_quant lens", out["a_fq_len"])
+
+    # ---------------- the 30-symbols-per-frame cap (decoder.py:131-136, 153-167) ----------------
+    # A checkpoint variant (synthetic.CAP_RECIPE) whose joint prefers one non-blank label on some
+    # frames whatever the prediction: the reference's greedy_decode_f32 emits 30 symbols there and
+    # the cap forces the advance.  The joint is wrapped to count those forced advances per row
+    # (symbols_added == max_symbols_per_step, argmax non-blank, row not finished), and the
+    # generator asserts that they happen, beside blank advances, on most rows.
+    cap_ck = synthetic.make_checkpoint(seed, synthetic.CAP_RECIPE)
+    out["cap_digest"] = np.frombuffer(synthetic.checkpoint_digest(cap_ck).encode(), np.uint8)
+    cap_path = os.path.join(tmp, "rnnt_cap.pt")
+    torch.save({k: torch.from_numpy(v.copy()) for k, v in cap_ck.items()}, cap_path)
+    Tc, Nc = 60, 6
+    cap_lens = np.array([60, 53, 40, 29, 9, 3], np.int32)
+    xcap = synthetic.make_features(Tc, Nc, seed=7, lens=cap_lens)[:, :, :240]
+    rcap = ref_model.RNNT(cap_path, "f32").eval()
+    dcap = ref_decoder.GreedyDecoder(rcap, "f32", False, -1, Nc)
+    caps = np.zeros(Nc, np.int32)
+    joint = rcap.joint
+
+    class _CountCaps(torch.nn.Module):
+        def forward(self, fi, g, padded):
+            y = joint(fi, g, padded)
+            sym = torch.argmax(y, dim=1)
+            hit = dcap.symbols_added.eq(30) & sym.ne(28) & ~dcap.finish
+            caps[:] += hit.numpy()[:Nc].astype(np.int32)
+            return y
+
+    rcap.joint = _CountCaps()
+    with torch.no_grad():
+        res, res_len = dcap(torch.from_numpy(xcap.copy()), torch.from_numpy(cap_lens.astype(np.int64)))
+        zs = [torch.zeros(Nc, 1024) for _ in range(5)]
+        rcap.joint = joint
+        fcap, *_ = rcap.transcription(torch.from_numpy(xcap.copy()), torch.from_numpy(cap_lens.astype(np.int64)),
+                                      zs[:2], zs[:2], zs[2:], zs[2:])
+    steps = dcap.step.numpy().astype(np.int32)
+    assert caps.max() > 0 and (caps > 0).sum() >= 3, f"no row hits the 30-symbol cap: {caps}"
+    assert (steps[:, 0] > caps).sum() >= 3, "cap rows also need blank advances (a mixed decode)"
+    out["cap_x"], out["cap_lens"] = xcap, cap_lens
+    out["cap_f32_res"], out["cap_f32_len"] = res.numpy().astype(np.int32), res_len.numpy().astype(np.int32)
+    out["cap_f32_steps"], out["cap_f32_caps"] = steps, caps
+    out["cap_f32_f"] = fcap.numpy()
+    print("cap lens", out["cap_f32_len"], "caps", caps, "steps", steps.tolist())
     _check_no_pycache()
     np.savez_compressed(OUT, **out)
     print("wrote", OUT, os.path.getsize(OUT), "bytes")

@@ -61,7 +61,7 @@ def test_world_disagreeing_with_gpus_fails():
 
 def test_dumped_responses_equal_across_rank_counts(tmp_path):
     """--dump-responses + tools/compare_responses.py (the GPU rehearsal's check,
-    tools/r04_multirank.sh) on the mock path: the query served by 2 ranks with dynamic claims and by
+    tools/gpu.sh multirank) on the mock path: the query served by 2 ranks with dynamic claims and by
     3 ranks with the static deal gathers the same rows as 1 rank; a changed row is reported."""
     import numpy as np
 

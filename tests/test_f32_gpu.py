@@ -62,9 +62,9 @@ def test_f32_encoder_matches_reference_fixture(f32_engine, golden):
 
 
 def test_config2_full_size(f32_engine, f32_layers, oracle):
-    """Config 2 shape: N=32, 15 s (T=500) on the GPU.  Size-independent checks: the LSTM stack is
-    causal and no frame is masked before T, so the first 16 stacked frames equal a T=32 run of
-    the restatement bit-for-bit; the whole output is finite and deterministic."""
+    """Config 2 at its full shape: N=32, 15 s (T=500) on the GPU.  Every one of the 250 stacked
+    frames of every row is compared with the restatement (SURVEY 8d asks <= 1e-3 max-abs; the
+    k-ordered fma chains make it bit-exact), and the output is deterministic run to run."""
     N, T = 32, 500
     x = synthetic.make_features(T, N, seed=2)[:, :, :240]
     lens = np.full(N, T, np.int32)
@@ -72,5 +72,7 @@ def test_config2_full_size(f32_engine, f32_layers, oracle):
     f2 = _run(f32_engine, x, lens)
     assert f1.shape == (250, N, 1024) and np.isfinite(f1).all()
     np.testing.assert_array_equal(f1, f2)
-    fo = oracle.encoder_f32(f32_layers, x[:32], np.full(N, 32, np.int32))
-    np.testing.assert_array_equal(f1[:16], fo[:16])
+    fo = oracle.encoder_f32(f32_layers, x, lens)  # ~15 s of host time for the whole batch
+    assert fo.shape == f1.shape
+    assert float(np.abs(f1 - fo).max()) <= 1e-3
+    np.testing.assert_array_equal(f1.view(np.uint32), fo.view(np.uint32))

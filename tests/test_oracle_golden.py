@@ -132,3 +132,46 @@ def test_numerics_primitives(oracle):
 def C_float(x):
     import ctypes
     return ctypes.c_float(float(x))
+
+
+# ---- the 30-symbols-per-frame cap (decoder.py:131-136, 153-167)
+@pytest.fixture(scope="module")
+def cap_ckpt(golden):
+    ck = synthetic.make_checkpoint(synthetic.DEFAULT_SEED, synthetic.CAP_RECIPE)
+    assert synthetic.checkpoint_digest(ck) == bytes(golden["cap_digest"]).decode()
+    return ck
+
+
+def test_cap_f32_decode_matches_reference(oracle, cap_ckpt, golden):
+    """The reference's greedy_decode_f32 on the cap checkpoint (make_golden.py asserts it hits
+    max_symbols_per_step on most rows): the restatement reproduces its tokens, its (advance, emit)
+    counters and its count of cap-forced advances per row."""
+    sd = weights.migrate_state_dict(cap_ckpt)
+    layers = [weights.enc_layer_params(sd, l) for l in range(5)]
+    x, lens = golden["cap_x"], golden["cap_lens"]
+    f = oracle.encoder_f32(layers, x, lens)
+    fl = (lens + 1) // 2
+    ref = golden["cap_f32_f"]
+    for n in range(len(lens)):
+        assert np.abs(f[: fl[n], n] - ref[: fl[n], n]).max() < 2e-4
+    pm = weights.prepare_model(cap_ckpt, np.ones(5, np.float32), bf16=False)
+    res, rl, steps, caps = oracle.greedy_decode_caps(pm, f, fl)
+    assert caps.max() > 0
+    np.testing.assert_array_equal(caps, golden["cap_f32_caps"])
+    np.testing.assert_array_equal(steps, golden["cap_f32_steps"])
+    np.testing.assert_array_equal(rl, golden["cap_f32_len"])
+    for n in range(len(rl)):
+        np.testing.assert_array_equal(res[n, : rl[n]], golden["cap_f32_res"][n, : rl[n]])
+
+
+def test_cap_int8_bf16_restatement_hits_the_cap(oracle, cap_ckpt, golden):
+    """The int8 encoder + bf16 decoder restatement on the cap model reaches the cap branch too
+    (the case tests/test_cap_gpu.py runs the GPU paths on)."""
+    from rnnt_amd.config import RNNTParam as R
+    x, lens = golden["cap_x"], golden["cap_lens"]
+    amax = weights.calibrate_amax(weights.migrate_state_dict(cap_ckpt), np.pad(x, ((0, 0), (0, 0), (0, 16))), lens)
+    pm = weights.prepare_model(cap_ckpt, amax, bf16=True)
+    f = oracle.encoder_i8(pm, np.pad(x, ((0, 0), (0, 0), (0, 16))), lens)
+    res, rl, steps, caps = oracle.greedy_decode_caps(pm, f, (lens + 1) // 2)
+    assert (caps > 0).sum() >= 3, caps
+    assert (steps[:, 1] >= R.max_symbols_per_step * caps).all()
