@@ -124,17 +124,24 @@ def greedy_decode(pm, f, f_lens, max_res=None):
 
 def greedy_decode_caps(pm, f, f_lens, max_res=None):
     """greedy_decode + caps [N]: advances forced by the 30-symbols-per-frame cap (decoder.py:131-136)."""
+    return greedy_decode_walks(pm, f, f_lens, max_res)[:4]
+
+
+def greedy_decode_walks(pm, f, f_lens, max_res=None):
+    """greedy_decode_caps + walks [N,5]: lock-step steps per row when one joint launch may walk up to
+    1, 2, 3, 4, 8 frames (diagnostics for the engine's walk cap)."""
     f = _c(f, np.float32); f_lens = _c(f_lens, np.int32)
     Tp, N, _ = f.shape
     max_res = max_res or max(1, Tp * 30)
     res = np.empty((N, max_res), np.int32); res_len = np.empty(N, np.int32); steps = np.empty((N, 2), np.int32)
     caps = np.empty(N, np.int32)
+    walks = np.empty((N, 5), np.int32)
     k = _dec_args(pm)
-    lib().oracle_greedy_decode_caps(Tp, N, _p(f), _p(f_lens), int(bool(pm.bf16)), _p(k["embed"]), _ptrs(k["wih"]),
+    lib().oracle_greedy_decode_walks(Tp, N, _p(f), _p(f_lens), int(bool(pm.bf16)), _p(k["embed"]), _ptrs(k["wih"]),
                                     _ptrs(k["whh"]), _ptrs(k["bih"]), _ptrs(k["bhh"]), _p(k["w1t"]), _p(k["w1p"]),
                                     _p(k["bt"]), _p(k["bp"]), _p(k["w2"]), _p(k["b2"]), _p(res), _p(res_len),
-                                    max_res, _p(steps), _p(caps))
-    return res, res_len, steps, caps
+                                    max_res, _p(steps), _p(caps), _p(walks))
+    return res, res_len, steps, caps, walks
 
 
 def joint(pm, f, g):

@@ -97,6 +97,13 @@ void oracle_greedy_decode_caps(int Tp, int N, const float* f, const int32_t* f_l
                           const float* const* pbhh, const float* W1t, const float* W1p,
                           const float* bt, const float* bp, const float* W2, const float* b2,
                           int32_t* res, int32_t* res_len, int max_res, int32_t* steps, int32_t* caps);
+void oracle_greedy_decode_walks(int Tp, int N, const float* f, const int32_t* f_lens, int bf16,
+                          const float* embed, const float* const* pWih,
+                          const float* const* pWhh, const float* const* pbih,
+                          const float* const* pbhh, const float* W1t, const float* W1p,
+                          const float* bt, const float* bp, const float* W2, const float* b2,
+                          int32_t* res, int32_t* res_len, int max_res, int32_t* steps, int32_t* caps,
+                                int32_t* walks);
 
 /* Joint logits for explicit inputs (amx_linear_bf16_accum_relu + amx_linear_i16o32,
  * modeling_rnnt.py:259-289): f [N][1024], g [N][320] -> logits [N][29]. */

@@ -8,6 +8,7 @@
 #   kernels                encoder layer-step microbenchmarks (tools/bench_kernels.py)
 #   profile                kernel-trace stats of the bench + separate PMC passes (summaries in $OUT/summary)
 #   multirank              2 / 3 ranks on one GPU (gloo, --share-device) vs one rank, responses compared
+#   timeline               kernel trace of warmup + one timed query: per-batch encode / decode spans (trace_query.py)
 #
 # A variant is NAME[:VAR=VAL[,VAR=VAL...]]: NAME "main" is the shipped library, any other NAME loads
 # build_dev/lib_NAME.so (RNNT_MI355X_LIB); the VAR=VAL pairs are set in that run's environment.
@@ -93,6 +94,12 @@ profile)
   find $OUT -name "*_kernel_trace.csv" -delete
   find $OUT -name "*_counter_collection.csv" -size +8M -delete
   ;;
+timeline)
+  timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tl -- \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/trace.log 2>&1 || die "trace rc=$?" $OUT/trace.log
+  python3 tools/trace_query.py $OUT/trace > $OUT/timeline.txt && cat $OUT/timeline.txt
+  [ -n "$KEEP_TRACE" ] || find $OUT/trace -name "*_kernel_trace.csv" -delete
+  ;;
 multirank)
   # bench.py's multi-rank data path on a 1-GPU box (the 8-GPU run is the driver's): ranks launched by
   # bench.py itself, every rank on cuda:0 with real engines, gloo control plane, dynamic claims and the
@@ -112,5 +119,5 @@ multirank)
   done
   ;;
 *)
-  echo "unknown task $TASK (check | ab | decab | kernels | profile | multirank)"; exit 2 ;;
+  echo "unknown task $TASK (check | ab | decab | kernels | profile | multirank | timeline)"; exit 2 ;;
 esac
