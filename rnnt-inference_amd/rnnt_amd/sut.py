@@ -270,10 +270,28 @@ class OfflineSUT:
         st.synchronize()
         return res, rl
 
+    def _dec_stream_for(self, eng):
+        """Development knob RNNT_SUT_DEC_PRIORITY=1: the decode of each engine runs on a second,
+        high-priority stream (the engine orders its calls across streams by its state event)."""
+        import os
+        import torch
+        if os.environ.get("RNNT_SUT_DEC_PRIORITY", "0") != "1":
+            return None
+        key = ("dec", id(eng))
+        if key not in self._streams:
+            lo, hi = torch.cuda.Stream.priority_range()
+            self._streams[key] = torch.cuda.Stream(device=eng.device, priority=min(lo, hi))
+        return self._streams[key]
+
     def _decode(self, eng, st, enc):
         """The greedy decode of the encoded batch -> (lengths int32 [n] host, tokens [n, >=max len] host)."""
         res, rl = enc
-        eng.decode(res, rl, stream=st)
+        dst = self._dec_stream_for(eng)
+        if dst is None:
+            eng.decode(res, rl, stream=st)
+        else:
+            eng.decode(res, rl, stream=dst)
+            dst.synchronize()
         rlh = rl.cpu().numpy()
         return rlh, res[:, : max(1, int(rlh.max()))].cpu().numpy()
 
