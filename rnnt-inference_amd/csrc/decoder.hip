@@ -382,23 +382,53 @@ constexpr int PRED_ROW_GROUPS = 24;
 constexpr int G_ROW_GROUPS = 48;
 constexpr int JOINT_GROUPS = 512;
 
-// NW waves per workgroup (NW gate tiles; 4: 8-wave workgroups measured no faster, DESIGN.md)
-template <int LAYER, int NW>
-__global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity) {
+// ---- stores of data another workgroup of the SAME launch reads (persistent mode, PS = true): written
+// through (`sc1`: the line leaves the XCD's L2), 4- or 16-byte, as the MI355X guide's hand-off rows
+// require (Guideline 16, the flow encoder's recipe: sc1 stores, every wave's vmcnt(0), a workgroup
+// barrier, one relaxed agent-scope counter add; the consumer polls, acquires, meets at a barrier).
+// PS = false: plain stores (the step kernels hand off at kernel boundaries).
+typedef unsigned int dec_u32x4 __attribute__((ext_vector_type(4)));
+#ifndef RNNT_EMU
+template <bool PS>
+__device__ __forceinline__ void st_b32(void* p, uint32_t v) {
+  if (PS) __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *(uint32_t*)p = v;
+}
+template <bool PS>
+__device__ __forceinline__ void st_b128(void* p, uint4 v) {
+  if (PS) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7ffffff0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(dec_u32x4{v.x, v.y, v.z, v.w}, r, 0, 0, 16);  // aux 16 = sc1
+  } else {
+    *(uint4*)p = v;
+  }
+}
+#else  // host emulation (tools/emu): the step kernels only, plain stores
+template <bool PS>
+inline void st_b32(void* p, uint32_t v) { *(uint32_t*)p = v; }
+template <bool PS>
+inline void st_b128(void* p, uint4 v) { *(uint4*)p = v; }
+#endif
+
+// One prediction LSTM layer for the emit list's rows (see dec_pred_kernel).  The body runs one
+// launch's work: in the step kernel once, in the persistent decode once per step with the weight
+// slice kept in registers across steps (wl: loaded).  X / ents_all: the caller's LDS.
+template <int LAYER>
+struct PredRegs {
+  uint4 wh[P / 32], wx[LAYER ? P / 32 : 1];
+  float4 bh, bx;
+  bool wl = false;
+};
+constexpr int pred_xp(int layer) { return (layer ? 2 * P : P) + 16; }
+template <int LAYER, int NW, bool PS>
+__device__ __forceinline__ void dec_pred_body(const DecArgs& a, int parity, const GridXY gxy,
+                                              uint16_t (*X)[pred_xp(LAYER)], int (*ents_all)[DEC_RT], PredRegs<LAYER>& W) {
   constexpr int PRED_THREADS = NW * 64;
-  constexpr int NT = 1;                  // gate tiles per wave
   constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
-  // bf16 pitch +32 B per row: every ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows c, 16-B
-  // column q) lands on 16 distinct bank quads; the round-2 +16 B pitch put rows c and c+8 on the same
-  // quads (2-way, 36-37 % of the LDS cycles of these kernels in the r02 PMC pass)
-  constexpr int XP = KX + 16;
-  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][XP];
   constexpr int NK = PRED_THREADS / DEC_RT;  // row tiles whose list entries load up front
-  __shared__ int ents_all[NK][DEC_RT];
   const DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
-  const GridXY gxy = xcd_grid(PG4 / (16 * (PRED_THREADS / 64)));
   const int* list = s.list + parity * a.Npad;
   // the entries of this workgroup's first NK row tiles load beside the list length (one round
   // trip for all of them; indices past Npad -- XCD rounding, long strides -- are guarded)
@@ -408,11 +438,7 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
-  const int t0 = (gxy.x * (PRED_THREADS / 64) + wave) * NT;  // this wave's gate tiles t0 .. t0 + NT - 1
-  // the weight slice (10 / 20 x 16 B per lane) is issued after the first tile's input loads:
-  // vmcnt retires in order, so loads issued first would hold up the staging that needs the inputs
-  uint4 wh[NT][P / 32], wx[NT][LAYER ? P / 32 : 1];
-  float4 bh[NT], bx[NT];
+  const int t0 = gxy.x * (PRED_THREADS / 64) + wave;  // this wave's gate tile
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT)  // past the prefetched tiles (the slot's tile is done)
@@ -421,18 +447,14 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     ST_MARK(st1);
     // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and, layer 0, its
     // label-table input halves, fetched beside the input staging
-    float cp[DEC_SUB][NT];
-    float4 xt[DEC_SUB][NT];
+    float cp[DEC_SUB];
+    float4 xt[DEC_SUB];
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       int ec = ents[16 * st + c];
       if (ec >= 0 && !dec_ok(entry_row(ec) < a.Npad && entry_label(ec) <= 28, 0)) ec = -1;
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        cp[st][tt] = ec >= 0 ? hc_part(a.hc, entry_row(ec), entry_slot(ec), 2 + LAYER)[(t0 + tt) * 4 + q] : 0.0f;
-        if (!LAYER)
-          xt[st][tt] = *(const float4*)(a.w.xtab + (size_t)(ec >= 0 ? entry_label(ec) : 28) * PG4 + (t0 + tt) * 16 + 4 * q);
-      }
+      cp[st] = ec >= 0 ? hc_part(a.hc, entry_row(ec), entry_slot(ec), 2 + LAYER)[t0 * 4 + q] : 0.0f;
+      if (!LAYER) xt[st] = *(const float4*)(a.w.xtab + (size_t)(ec >= 0 ? entry_label(ec) : 28) * PG4 + t0 * 16 + 4 * q);
     }
     // stage the listed rows' inputs as bf16: layer 0 h0 (committed slot); layer 1
     // [h0 of the candidate slot | h1 committed]
@@ -458,19 +480,17 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
-    if (it == 0) {
+    if (!W.wl) {
+      W.wl = true;
+      const uint16_t* wr = a.w.wp[LAYER] + (size_t)(t0 * 16 + c) * 640 + 8 * q;
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        const uint16_t* wr = a.w.wp[LAYER] + (size_t)((t0 + tt) * 16 + c) * 640 + 8 * q;
+      for (int b = 0; b < P / 32; ++b) W.wh[b] = *(const uint4*)(wr + P + 32 * b);
+      if (LAYER) {
 #pragma unroll
-        for (int b = 0; b < P / 32; ++b) wh[tt][b] = *(const uint4*)(wr + P + 32 * b);
-        if (LAYER) {
-#pragma unroll
-          for (int b = 0; b < P / 32; ++b) wx[tt][b] = *(const uint4*)(wr + 32 * b);
-          bx[tt] = *(const float4*)(a.w.bih_p[LAYER] + (t0 + tt) * 16 + 4 * q);
-        }
-        bh[tt] = *(const float4*)(a.w.bhh_p[LAYER] + (t0 + tt) * 16 + 4 * q);
+        for (int b = 0; b < P / 32; ++b) W.wx[b] = *(const uint4*)(wr + 32 * b);
+        W.bx = *(const float4*)(a.w.bih_p[LAYER] + t0 * 16 + 4 * q);
       }
+      W.bh = *(const float4*)(a.w.bhh_p[LAYER] + t0 * 16 + 4 * q);
     }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
@@ -486,40 +506,43 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
     // time, so each block's fragment reads overlap the previous block's MFMAs (sub-tiles past the
     // list end run on the staged zeros; their results are not stored).  Each chain is still the
     // contract's natural-k sequence from its bias.
-    static_assert(NT == 1, "one gate tile per wave");
     int ecs[DEC_SUB];
     v4f ahs[DEC_SUB], axs[DEC_SUB];
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       ecs[st] = ents[16 * st + c];
-      ahs[st] = v4f{bh[0].x, bh[0].y, bh[0].z, bh[0].w};
-      axs[st] = LAYER ? v4f{bx[0].x, bx[0].y, bx[0].z, bx[0].w} : v4f{xt[st][0].x, xt[st][0].y, xt[st][0].z, xt[st][0].w};
+      ahs[st] = v4f{W.bh.x, W.bh.y, W.bh.z, W.bh.w};
+      axs[st] = LAYER ? v4f{W.bx.x, W.bx.y, W.bx.z, W.bx.w} : v4f{xt[st].x, xt[st].y, xt[st].z, xt[st].w};
     }
 #pragma unroll
     for (int b = 0; b < P / 32; ++b) {
 #pragma unroll
       for (int st = 0; st < DEC_SUB; ++st) {
         const uint16_t* xr = &X[16 * st + c][8 * q];
-        ahs[st] = mfma_bf16(wh[0][b], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ahs[st]);
-        if (LAYER) axs[st] = mfma_bf16(wx[0][LAYER ? b : 0], *(const uint4*)(xr + 32 * b), axs[st]);
+        ahs[st] = mfma_bf16(W.wh[b], *(const uint4*)(xr + (LAYER ? P : 0) + 32 * b), ahs[st]);
+        if (LAYER) axs[st] = mfma_bf16(W.wx[LAYER ? b : 0], *(const uint4*)(xr + 32 * b), axs[st]);
       }
     }
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ecs[st];
       const int row = ec >= 0 && dec_ok(entry_row(ec) < a.Npad, 2) ? entry_row(ec) : -1, sl = ec >= 0 ? entry_slot(ec) : 0;
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        const v4f ah = ahs[st], ax = axs[st];
+      const v4f gs = axs[st] + ahs[st];
+      const int u = t0 * 4 + q;
+      const float ig = det_sigmoid(gs[0]), fg = det_sigmoid(gs[1]), gg = det_tanh(gs[2]), og = det_sigmoid(gs[3]);
+      const float cn = fg * cp[st] + ig * gg;
+      const float hh = bf_round_ftz(og * det_tanh(cn));
+      const uint32_t hb = __float_as_uint(hh) >> 16;  // hh is bf16-exact
+      if (PS) {
+        // 4-byte write-through stores: units u (q even) and u + 1 (lane + 16, same row) in one word
+        const uint32_t hpair = __shfl_xor(hb, 16);
         if (row >= 0) {
-          const v4f gs = ax + ah;
-          const int u = (t0 + tt) * 4 + q;
-          const float ig = det_sigmoid(gs[0]), fg = det_sigmoid(gs[1]), gg = det_tanh(gs[2]), og = det_sigmoid(gs[3]);
-          const float cn = fg * cp[st][tt] + ig * gg;
-          const float hh = bf_round_ftz(og * det_tanh(cn));
-          hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
-          h_bf(a.hc, row, sl ^ 1, LAYER)[u] = (uint16_t)(__float_as_uint(hh) >> 16);  // hh is bf16-exact
+          st_b32<true>(hc_part(a.hc, row, sl ^ 1, 2 + LAYER) + u, __float_as_uint(cn));
+          if ((q & 1) == 0) st_b32<true>(h_bf(a.hc, row, sl ^ 1, LAYER) + u, hb | (hpair << 16));
         }
+      } else if (row >= 0) {
+        hc_part(a.hc, row, sl ^ 1, 2 + LAYER)[u] = cn;
+        h_bf(a.hc, row, sl ^ 1, LAYER)[u] = (uint16_t)hb;
       }
     }
     lds_barrier();  // X (and this entry slot, NK tiles on) are restaged by the next tile
@@ -527,23 +550,39 @@ __global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity
   }
 }
 
+// NW waves per workgroup (NW gate tiles; 4: 8-wave workgroups measured no faster, DESIGN.md)
+template <int LAYER, int NW>
+__global__ void __launch_bounds__(NW * 64) dec_pred_kernel(DecArgs a, int parity) {
+  // bf16 pitch +32 B per row: every ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows c, 16-B
+  // column q) lands on 16 distinct bank quads; the round-2 +16 B pitch put rows c and c+8 on the same
+  // quads (2-way, 36-37 % of the LDS cycles of these kernels in the r02 PMC pass)
+  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][pred_xp(LAYER)];
+  __shared__ int ents_all[NW * 64 / DEC_RT][DEC_RT];
+  PredRegs<LAYER> W;
+  dec_pred_body<LAYER, NW, false>(a, parity, xcd_grid(PG4 / (16 * NW)), X, ents_all, W);
+}
+
 // G = b_p + g . W1p^T for the listed rows' new candidates.  Workgroups of 4 waves, one 16-column
 // tile (10 KB of W1p) per wave in registers: grid x = 8 column groups, y = row groups striding
 // over the emit list's tiles.  Also clears the next step's emit and live lists for the joint
-// that follows.
+// that follows (reset: the workgroup that does it).
 constexpr int GXP = P + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
 constexpr int G_THREADS = 256;  // 4 waves, one 16-column tile each; grid x = 8 column groups
-__global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
-  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
+struct GRegs {
+  uint4 wv[P / 32];
+  float4 b0;
+  bool wl = false;
+};
+template <bool PS>
+__device__ __forceinline__ void dec_g_body(const DecArgs& a, int parity, const GridXY gxy, bool reset,
+                                           uint16_t (*X)[GXP], int (*ents_all)[DEC_RT], GRegs& W) {
   constexpr int NK = G_THREADS / DEC_RT;  // row tiles whose list entries load up front
-  __shared__ int ents_all[NK][DEC_RT];
-  DecState& s = a.s;
+  const DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
-  const GridXY gxy = xcd_grid(J / (16 * (G_THREADS / 64)));
-  if (blockIdx.x == 0 && tid == 0) {
-    s.count[EMIT_N(parity ^ 1)] = 0;
-    s.count[LIVE_N(parity ^ 1)] = 0;
+  if (reset && tid == 0) {
+    st_b32<PS>(&s.count[EMIT_N(parity ^ 1)], 0u);
+    st_b32<PS>(&s.count[LIVE_N(parity ^ 1)], 0u);
   }
   const int* list = s.list + parity * a.Npad;
   const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
@@ -552,9 +591,7 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
   if (gxy.y >= ntiles) return;
   ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
-  constexpr int NJ = 1;  // column tiles per wave
-  uint4 wv[NJ][P / 32];  // issued after the first tile's input loads (see dec_pred_kernel)
-  float4 b0[NJ];
+  const int jt = gxy.x * (G_THREADS / 64) + wave;  // this wave's column tile
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
     if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? list[rt * DEC_RT + tid] : -1;
@@ -578,15 +615,12 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
-    if (it == 0) {
+    if (!W.wl) {
+      W.wl = true;
+      const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
 #pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) {
-        const int jt = (gxy.x * (G_THREADS / 64) + wave) * NJ + jj;
-        const uint16_t* w0 = a.w.w1p + (size_t)(jt * 16 + c) * P + 8 * q;
-#pragma unroll
-        for (int b = 0; b < P / 32; ++b) wv[jj][b] = *(const uint4*)(w0 + 32 * b);
-        b0[jj] = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
-      }
+      for (int b = 0; b < P / 32; ++b) W.wv[b] = *(const uint4*)(w0 + 32 * b);
+      W.b0 = *(const float4*)(a.w.bp + jt * 16 + 4 * q);
     }
 #pragma unroll
     for (int u = 0; u < NIT; ++u) {
@@ -599,26 +633,32 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
     lds_barrier();
     ST_MARK(st2);
     // every sub-tile's chain advances one k block at a time (fragment reads overlap MFMAs)
-    static_assert(NJ == 1, "one column tile per wave");
     v4f accs[DEC_SUB];
 #pragma unroll
-    for (int st = 0; st < DEC_SUB; ++st) accs[st] = v4f{b0[0].x, b0[0].y, b0[0].z, b0[0].w};
+    for (int st = 0; st < DEC_SUB; ++st) accs[st] = v4f{W.b0.x, W.b0.y, W.b0.z, W.b0.w};
 #pragma unroll
     for (int b = 0; b < P / 32; ++b)
 #pragma unroll
       for (int st = 0; st < DEC_SUB; ++st)
-        accs[st] = mfma_bf16(wv[0][b], *(const uint4*)(&X[16 * st + c][8 * q] + 32 * b), accs[st]);
+        accs[st] = mfma_bf16(W.wv[b], *(const uint4*)(&X[16 * st + c][8 * q] + 32 * b), accs[st]);
 #pragma unroll
     for (int st = 0; st < DEC_SUB; ++st) {
       const int ec = ents[16 * st + c];
       const v4f acc = accs[st];
-      const int jt = gxy.x * (G_THREADS / 64) + wave;
       if (ec >= 0 && dec_ok(entry_row(ec) < a.Npad, 5))
-        *(float4*)(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q) = float4{acc[0], acc[1], acc[2], acc[3]};
+        st_b128<PS>(a.G + (size_t)entry_row(ec) * J + jt * 16 + 4 * q,
+                    uint4{__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]), __float_as_uint(acc[3])});
     }
     lds_barrier();
     ST_FLUSH(2, st0, st1, st2, 0ull);
   }
+}
+
+__global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) uint16_t X[DEC_RT][GXP];
+  __shared__ int ents_all[G_THREADS / DEC_RT][DEC_RT];
+  GRegs W;
+  dec_g_body<false>(a, parity, xcd_grid(J / (16 * (G_THREADS / 64))), blockIdx.x == 0, X, ents_all, W);
 }
 
 // joint (y1 = bf16(relu(F[t] + G)), logits = b2 + y1.W2^T) + argmax + greedy_decode_update
@@ -632,40 +672,46 @@ constexpr int JOINT_ITERS = 2;  // 1 / 3 / 4 measured slower (DESIGN.md section 
 
 constexpr int YP = J + 16;  // +32 B: conflict-free fragment reads (see dec_pred_kernel's XP)
 constexpr int JRT = 16;  // joint rows per workgroup tile: the argmax maps 4 waves x 4 rows x 16 lanes onto it
-__global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
-  __shared__ __attribute__((aligned(16))) uint16_t X[JRT][YP];
-  __shared__ float Lp[4][JRT][NLAB_PAD + 1];
-  __shared__ int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT];
-  __shared__ int slot_[JRT], add_[JRT], flen_[JRT], idx_[JRT];
-  DecState& s = a.s;
+struct JointLds {
+  __attribute__((aligned(16))) uint16_t X[JRT][YP];
+  float Lp[4][JRT][NLAB_PAD + 1];
+  int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT];
+  int slot_[JRT], add_[JRT], flen_[JRT], idx_[JRT];
+};
+struct JointRegs {
+  uint4 wv[8];  // W2 fragments: issued after the first tile's F / G loads (see dec_pred_kernel)
+  v4f bias = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+  bool wl = false;
+};
+// jg / njg: this workgroup's index among the joint workgroups and their count (row tiles jg, jg + njg, ...)
+template <bool PS>
+__device__ __forceinline__ void dec_joint_body(const DecArgs& a, int parity, int jg, int njg, JointLds& L, JointRegs& W) {
+  const DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
   const int4* llist = s.live + parity * a.Npad;
   int4* nlist = s.live + (parity ^ 1) * a.Npad;
-  const int4 r_first = tid < JRT ? llist[blockIdx.x * JRT + tid] : int4{0, 0, 0, 0};
+  const int4 r_first = tid < JRT ? llist[jg * JRT + tid] : int4{0, 0, 0, 0};
   const int lcnt = s.count[LIVE_N(parity)];
   const int ntiles = (lcnt + JRT - 1) / JRT;
-  if ((int)blockIdx.x >= ntiles) return;
+  if (jg >= ntiles) return;
   // logits = ((s0 + s1) + s2) + s3, s_b = y1[128b : 128b+128] . W2^T (s0 from b2): wave w runs
   // label half w&1 over k blocks 2(w>>1) and 2(w>>1)+1 as two independent 4-instruction chains
   const int lh = wave & 1, kb0 = 2 * (wave >> 1);
-  uint4 wv[8];  // W2 fragments: issued after the first tile's F / G loads (see dec_pred_kernel)
-  v4f bias = v4f{0.0f, 0.0f, 0.0f, 0.0f};
-  bool w_loaded = false;
-  for (int rt = blockIdx.x; rt < ntiles; rt += gridDim.x) {
+  for (int rt = jg; rt < ntiles; rt += njg) {
     if (tid < JRT) {
       const int i = rt * JRT + tid;
-      const int4 e = i < lcnt && dec_ok(i < a.Npad, 7) ? (rt == (int)blockIdx.x ? r_first : llist[i]) : int4{-1, 0, 0, 0};
+      const int4 e = i < lcnt && dec_ok(i < a.Npad, 7) ? (rt == jg ? r_first : llist[i]) : int4{-1, 0, 0, 0};
       int r = e.x < 0 ? -1 : entry_row(e.x);
       if (r >= 0 && !dec_ok(r < a.Npad && (e.y & 0xffff) < ((e.y >> 16) & 0xffff), 8)) r = -1;
-      rows[tid] = r;
-      walking[tid] = r >= 0;
-      emit_e[tid] = -1;
-      slot_[tid] = (e.x >> 24) & 1;
-      add_[tid] = (e.x >> 25) & 31;
-      tidx[tid] = e.y & 0xffff;
-      flen_[tid] = (e.y >> 16) & 0xffff;
-      idx_[tid] = e.z;
+      L.rows[tid] = r;
+      L.walking[tid] = r >= 0;
+      L.emit_e[tid] = -1;
+      L.slot_[tid] = (e.x >> 24) & 1;
+      L.add_[tid] = (e.x >> 25) & 31;
+      L.tidx[tid] = e.y & 0xffff;
+      L.flen_[tid] = (e.y >> 16) & 0xffff;
+      L.idx_[tid] = e.z;
     }
     lds_barrier();
     ST_MARK(st1);
@@ -676,7 +722,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     float4 gl4[NIT][2];
     for (int it = 0; it < JOINT_ITERS; ++it) {
       bool any = false;
-      for (int m = 0; m < JRT; ++m) any |= walking[m] != 0;
+      for (int m = 0; m < JRT; ++m) any |= L.walking[m] != 0;
       if (!any) break;
       // every load of the tile first (one memory round trip), then y1: rows not walking read a
       // safe cached address (row 0 of frame 0) and stage zeros.  G is the same for every frame
@@ -686,8 +732,8 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
 #pragma unroll
       for (int u = 0; u < NIT; ++u) {
         const int i = tid + 256 * u, m = i / (J / 8), k = (i % (J / 8)) * 8;
-        wk[u] = walking[m] != 0;
-        const int row = wk[u] ? rows[m] : 0, tm = wk[u] ? tidx[m] : 0;
+        wk[u] = L.walking[m] != 0;
+        const int row = wk[u] ? L.rows[m] : 0, tm = wk[u] ? L.tidx[m] : 0;
         const float* fr = a.F + ((size_t)tm * a.Npad + row) * J + k;
         fl4[u][0] = __builtin_nontemporal_load((const v4f*)fr);  // streamed once
         fl4[u][1] = __builtin_nontemporal_load((const v4f*)(fr + 4));
@@ -698,17 +744,17 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (!w_loaded) {
-        w_loaded = true;
+      if (!W.wl) {
+        W.wl = true;
         const uint16_t* wr = a.w.w2 + (size_t)(lh * 16 + c) * J + 8 * q;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          wv[b] = *(const uint4*)(wr + 128 * kb0 + 32 * b);
-          wv[4 + b] = *(const uint4*)(wr + 128 * (kb0 + 1) + 32 * b);
+          W.wv[b] = *(const uint4*)(wr + 128 * kb0 + 32 * b);
+          W.wv[4 + b] = *(const uint4*)(wr + 128 * (kb0 + 1) + 32 * b);
         }
         if (kb0 == 0) {
           const float4 b0 = *(const float4*)(a.w.b2 + lh * 16 + 4 * q);
-          bias = v4f{b0.x, b0.y, b0.z, b0.w};
+          W.bias = v4f{b0.x, b0.y, b0.z, b0.w};
         }
       }
 #pragma unroll
@@ -725,25 +771,23 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           y[4 * h + 2] = bf_round_ftz(s2 > 0.0f ? s2 : 0.0f);
           y[4 * h + 3] = bf_round_ftz(s3 > 0.0f ? s3 : 0.0f);
         }
-        *(uint4*)&X[m][k] = wk[u] ? pack8(float4{y[0], y[1], y[2], y[3]}, float4{y[4], y[5], y[6], y[7]})
-                                  : uint4{0u, 0u, 0u, 0u};
+        *(uint4*)&L.X[m][k] = wk[u] ? pack8(float4{y[0], y[1], y[2], y[3]}, float4{y[4], y[5], y[6], y[7]})
+                                    : uint4{0u, 0u, 0u, 0u};
       }
       lds_barrier();
       ST_SET(st2);
-#pragma unroll
-      for (int st = 0; st < 1; ++st) {
-        if (!__any(walking[16 * st + c] != 0)) continue;
-        const uint16_t* xr = &X[16 * st + c][8 * q];
-        v4f s0 = bias, s1 = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+      if (__any(L.walking[c] != 0)) {
+        const uint16_t* xr = &L.X[c][8 * q];
+        v4f s0 = W.bias, s1 = v4f{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          s0 = mfma_bf16(wv[b], *(const uint4*)(xr + 128 * kb0 + 32 * b), s0);
-          s1 = mfma_bf16(wv[4 + b], *(const uint4*)(xr + 128 * (kb0 + 1) + 32 * b), s1);
+          s0 = mfma_bf16(W.wv[b], *(const uint4*)(xr + 128 * kb0 + 32 * b), s0);
+          s1 = mfma_bf16(W.wv[4 + b], *(const uint4*)(xr + 128 * (kb0 + 1) + 32 * b), s1);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          Lp[kb0][16 * st + c][lh * 16 + 4 * q + r] = s0[r];
-          Lp[kb0 + 1][16 * st + c][lh * 16 + 4 * q + r] = s1[r];
+          L.Lp[kb0][c][lh * 16 + 4 * q + r] = s0[r];
+          L.Lp[kb0 + 1][c][lh * 16 + 4 * q + r] = s1[r];
         }
       }
       lds_barrier();
@@ -758,7 +802,7 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           const int j = l2 + e;
-          const float v = ((Lp[0][m][j] + Lp[1][m][j]) + Lp[2][m][j]) + Lp[3][m][j];
+          const float v = ((L.Lp[0][m][j] + L.Lp[1][m][j]) + L.Lp[2][m][j]) + L.Lp[3][m][j];
           if (j < NLAB && (bl < 0 || v > bv)) {
             bv = v;
             bl = j;
@@ -774,33 +818,33 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
           }
         }
         if ((lane & 15) == 0) {
-          if (walking[m]) {
-            const int row = rows[m], best = bl;
-            if (best != BLANK && add_[m] != MAXSYM) {
-              const int id = idx_[m] + 1;
-              idx_[m] = id;
+          if (L.walking[m]) {
+            const int row = L.rows[m], best = bl;
+            if (best != BLANK && L.add_[m] != MAXSYM) {
+              const int id = L.idx_[m] + 1;
+              L.idx_[m] = id;
               s.idx[row] = id;
               if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
-              s.added[row] = ++add_[m];
+              s.added[row] = ++L.add_[m];
               s.preg[row] = best;
-              const int nsl = slot_[m] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
-              slot_[m] = nsl;
+              const int nsl = L.slot_[m] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+              L.slot_[m] = nsl;
               s.slot[row] = nsl;
-              emit_e[m] = emit_entry(row, nsl, best);
-              walking[m] = 0;
+              L.emit_e[m] = emit_entry(row, nsl, best);
+              L.walking[m] = 0;
             } else {
-              const int fl = flen_[m];
-              int t = tidx[m] + 1;
+              const int fl = L.flen_[m];
+              int t = L.tidx[m] + 1;
               if (t >= fl) {
                 s.fin[row] = 1;
-                walking[m] = 0;
-                rows[m] = -1;  // finished: not in the next live list
+                L.walking[m] = 0;
+                L.rows[m] = -1;  // finished: not in the next live list
                 t = fl - 1;
               }
-              tidx[m] = t;
+              L.tidx[m] = t;
               s.time[row] = t;
               s.added[row] = 0;
-              add_[m] = 0;
+              L.add_[m] = 0;
             }
           }
         }
@@ -810,26 +854,147 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
     // the tile's emitting rows -> next emit list, its unfinished rows -> next live list: ONE
     // 64-bit atomic on the adjacent (emit, live) counters of the next parity returns both bases
     if (wave == 0) {
-      const int e = lane < JRT ? emit_e[lane] : -1;
-      const int r = lane < JRT ? rows[lane] : -1;
+      const int e = lane < JRT ? L.emit_e[lane] : -1;
+      const int r = lane < JRT ? L.rows[lane] : -1;
       const unsigned long long me = __ballot(e >= 0), mr = __ballot(r >= 0);
       unsigned long long base = 0;
-      if (lane == 0 && (me | mr))
-        base = atomicAdd((unsigned long long*)&s.count[EMIT_N(parity ^ 1)],
-                         (unsigned long long)__popcll(me) | ((unsigned long long)__popcll(mr) << 32));
+      if (lane == 0 && (me | mr)) {
+        const unsigned long long inc = (unsigned long long)__popcll(me) | ((unsigned long long)__popcll(mr) << 32);
+#ifndef RNNT_EMU
+        base = PS ? __hip_atomic_fetch_add((unsigned long long*)&s.count[EMIT_N(parity ^ 1)], inc, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                  : atomicAdd((unsigned long long*)&s.count[EMIT_N(parity ^ 1)], inc);
+#else
+        base = atomicAdd((unsigned long long*)&s.count[EMIT_N(parity ^ 1)], inc);
+#endif
+      }
       base = __shfl(base, 0);
       const unsigned long long below = (1ull << lane) - 1;
       if (lane == 0) dec_ok(false, 31);  // ran (the emulator's check that the joint executed)
       if (e >= 0 && dec_ok((int)(base & 0xffffffffu) + __popcll(me & below) < a.Npad, 9))
-        s.list[(parity ^ 1) * a.Npad + (int)(base & 0xffffffffu) + __popcll(me & below)] = e;
-      if (r >= 0 && dec_ok((int)(base >> 32) + __popcll(mr & below) < a.Npad, 10))
-        nlist[(int)(base >> 32) + __popcll(mr & below)] =
-            live_entry(r, slot_[lane], add_[lane], tidx[lane], flen_[lane], idx_[lane]);
+        st_b32<PS>(&s.list[(parity ^ 1) * a.Npad + (int)(base & 0xffffffffu) + __popcll(me & below)], (uint32_t)e);
+      if (r >= 0 && dec_ok((int)(base >> 32) + __popcll(mr & below) < a.Npad, 10)) {
+        const int4 le = live_entry(r, L.slot_[lane], L.add_[lane], L.tidx[lane], L.flen_[lane], L.idx_[lane]);
+        st_b128<PS>(&nlist[(int)(base >> 32) + __popcll(mr & below)], uint4{(uint32_t)le.x, (uint32_t)le.y, (uint32_t)le.z, (uint32_t)le.w});
+      }
     }
     lds_barrier();  // rows / walking / tidx / X are reused by the next row tile
     ST_FLUSH(3, st0, st1, st2, 0ull);
   }
 }
+
+__global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
+  __shared__ JointLds L;
+  JointRegs W;
+  dec_joint_body<false>(a, parity, blockIdx.x, gridDim.x, L, W);
+}
+
+#ifndef RNNT_EMU
+// ---------------------------------------------------------------- persistent tail decode
+// Once few rows are live (the long tail of a length-sorted batch, where a step is four dependent
+// launches of a handful of workgroups), one launch runs every remaining step: each workgroup takes
+// one role for the whole launch -- a prediction layer-0 / layer-1 gate group (20 each), a G column
+// group (8) or a joint row group (nj) -- keeps its weight slice in registers across steps, and
+// runs that role's step body (the SAME code as the step kernels above: identical results) once
+// per step.  Phases hand off through per-role completion counters in device memory (`pc`):
+// pred0(k) waits for joint(k-1), pred1(k) for pred0(k), G(k) for pred1(k), joint(k) for G(k); the
+// data a phase hands on is stored write-through (PS = true).  Every role reads the same live count
+// of step k (written by joint(k-1), complete before any role of step k starts) and stops at 0, or
+// after max_steps; each still publishes, so no role waits for one that left.  Every wait is
+// bounded: past the timeout it raises the abort word and every workgroup leaves (the host reports
+// it).  Control flow around the waits is wave-uniform (wave 0 polls as a whole; see the flow
+// encoder).
+constexpr int PS_P0 = PG4 / (16 * 4), PS_P1 = PS_P0, PS_G = J / (16 * (G_THREADS / 64));  // 20, 20, 8
+enum { PC_P0 = 0, PC_P1 = 1, PC_G = 2, PC_J = 3, PC_ABORT = 4, PC_STEPS = 5, PC_WORDS = 8 };
+__device__ __forceinline__ unsigned pc_load(const uint32_t* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// wave 0 (whole wave): wait until counter `who` reaches `need`, then acquire; false on abort
+__device__ __forceinline__ bool pc_wait(uint32_t* pc, int who, unsigned need, unsigned long long timeout) {
+  const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + timeout;
+  while (pc_load(pc + who) < need) {
+    if (pc_load(pc + PC_ABORT)) return false;
+    if (__builtin_amdgcn_s_memrealtime() > t_end) {
+      __hip_atomic_store(pc + PC_ABORT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return true;
+}
+
+// one role's step loop; Body(parity) runs the step body
+template <class Body>
+__device__ __forceinline__ void ps_loop(const DecArgs& a, uint32_t* pc, int role, int prev, unsigned n_prev, int step0,
+                                        int max_steps, unsigned long long timeout, int* lds_flag, Body&& body) {
+  const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  for (int k = 0;; ++k) {
+    const int parity = (step0 + k) & 1;
+    if (w0) {
+      bool ok = true;
+      if (!(role == PC_P0 && k == 0)) ok = pc_wait(pc, prev, n_prev * (unsigned)(role == PC_P0 ? k : k + 1), timeout);
+      // the step's live count (joint(k-1) wrote it; every role reads the same value)
+      const int live = ok ? (int)__builtin_amdgcn_readfirstlane(*(volatile const int*)&a.s.count[LIVE_N(parity)]) : 0;
+      if (threadIdx.x == 0) lds_flag[0] = (!ok || live <= 0 || k >= max_steps) ? (ok ? 1 : 2) : 0;
+    }
+    __syncthreads();
+    const int stop = __builtin_amdgcn_readfirstlane(lds_flag[0]);
+    if (stop == 2) return;  // aborted: leave without publishing (every waiter sees the abort word)
+    if (!stop) body(parity);
+    // publish: every wave's write-through stores have landed, then one count
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(pc + role, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stop && role == PC_J && blockIdx.x == PS_P0 + PS_P1 + PS_G) __hip_atomic_store(pc + PC_STEPS, (uint32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (stop) return;
+    __syncthreads();  // lds_flag is rewritten by the next step
+  }
+}
+
+constexpr size_t ps_lds_bytes() {
+  const size_t p1 = sizeof(uint16_t) * DEC_RT * pred_xp(1) + sizeof(int) * (256 / DEC_RT) * DEC_RT;
+  const size_t g = sizeof(uint16_t) * DEC_RT * GXP + sizeof(int) * (G_THREADS / DEC_RT) * DEC_RT;
+  const size_t j = sizeof(JointLds);
+  return (p1 > g ? (p1 > j ? p1 : j) : (g > j ? g : j)) + 16;
+}
+
+__global__ void __launch_bounds__(256) dec_persist_kernel(DecArgs a, uint32_t* pc, int step0, int max_steps, int nj,
+                                                          unsigned long long timeout) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t psm[];
+  int* flag = (int*)(psm + ps_lds_bytes() - 16);
+  const int b = blockIdx.x;  // roles: [0,20) pred0 gate groups, [20,40) pred1, [40,48) G, [48,48+nj) joint
+  if (b < PS_P0) {
+    PredRegs<0> W;
+    auto X = (uint16_t(*)[pred_xp(0)])psm;
+    auto E = (int(*)[DEC_RT])(psm + sizeof(uint16_t) * DEC_RT * pred_xp(0));
+    ps_loop(a, pc, PC_P0, PC_J, (unsigned)nj, step0, max_steps, timeout, flag,
+            [&](int p) { dec_pred_body<0, 4, true>(a, p, GridXY{b, 0, 1}, X, E, W); });
+  } else if (b < PS_P0 + PS_P1) {
+    PredRegs<1> W;
+    auto X = (uint16_t(*)[pred_xp(1)])psm;
+    auto E = (int(*)[DEC_RT])(psm + sizeof(uint16_t) * DEC_RT * pred_xp(1));
+    ps_loop(a, pc, PC_P1, PC_P0, (unsigned)PS_P0, step0, max_steps, timeout, flag,
+            [&](int p) { dec_pred_body<1, 4, true>(a, p, GridXY{b - PS_P0, 0, 1}, X, E, W); });
+  } else if (b < PS_P0 + PS_P1 + PS_G) {
+    GRegs W;
+    auto X = (uint16_t(*)[GXP])psm;
+    auto E = (int(*)[DEC_RT])(psm + sizeof(uint16_t) * DEC_RT * GXP);
+    const int g = b - PS_P0 - PS_P1;
+    ps_loop(a, pc, PC_G, PC_P1, (unsigned)PS_P1, step0, max_steps, timeout, flag,
+            [&](int p) { dec_g_body<true>(a, p, GridXY{g, 0, 1}, g == 0, X, E, W); });
+  } else {
+    JointRegs W;
+    JointLds& L = *(JointLds*)psm;
+    const int jg = b - PS_P0 - PS_P1 - PS_G;
+    ps_loop(a, pc, PC_J, PC_G, (unsigned)PS_G, step0, max_steps, timeout, flag,
+            [&](int p) { dec_joint_body<true>(a, p, jg, nj, L, W); });
+  }
+}
+#endif  // RNNT_EMU
 
 __global__ void dec_finish_kernel(DecArgs a) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
@@ -840,7 +1005,7 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   // every buffer the step kernels address (a missing one is a host error here, not a GPU fault)
   const void* need[] = {a.F, a.f_lens, a.hc, a.G, a.res, a.res_len, a.w.xtab, a.w.wp[0], a.w.wp[1], a.w.bih_p[1],
                         a.w.bhh_p[0], a.w.bhh_p[1], a.w.w1p, a.w.bp, a.w.w2, a.w.b2, a.s.time, a.s.added, a.s.idx,
-                        a.s.preg, a.s.slot, a.s.fin, a.s.list, a.s.live, a.s.count};
+                        a.s.preg, a.s.slot, a.s.fin, a.s.list, a.s.live, a.s.count, a.s.pc};
   for (const void* p : need)
     if (!p) return -1;
   if (a.Npad % DEC_RT || a.N > a.Npad || a.Npad >= (1 << 24)) return -1;
@@ -872,10 +1037,37 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const char* v = getenv("RNNT_DEC_SPIN");
     return v && v[0] == '1';
   }();
+  // persistent tail (dec_persist_kernel): once the live rows read back fit a.persist_rows, one launch
+  // runs every remaining step (0 = off; at most 64 rows: 4 joint workgroups)
+#ifndef RNNT_EMU
+  const int PERSIST_ROWS = a.persist_rows < 0 ? 0 : (a.persist_rows > 64 ? 64 : a.persist_rows);
+  static std::atomic<uint64_t> ps_attr{0};
+#else
+  constexpr int PERSIST_ROWS = 0;
+#endif
   int step = 0, chunk = 0;
   int live_bound = a.N;  // unfinished rows at the end of the last chunk read back (an upper bound)
   bool done = false;
   while (!done && step < a.max_iter) {
+#ifndef RNNT_EMU
+    if (PERSIST_ROWS > 0 && chunk > 0 && live_bound <= PERSIST_ROWS) {
+      // the chunks already enqueued run first (stream order); the persistent launch continues at
+      // `step` with at most live_bound rows (live counts only fall)
+      const int nj = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
+      if (set_smem_attr_once((const void*)dec_persist_kernel, (int)ps_lds_bytes(), ps_attr)) return -1;
+      if (hipMemsetAsync(a.s.pc, 0, PC_WORDS * sizeof(uint32_t), st) != hipSuccess) return -1;
+      hipLaunchKernelGGL(dec_persist_kernel, dim3(PS_P0 + PS_P1 + PS_G + nj), dim3(256), ps_lds_bytes(), st, a, a.s.pc,
+                         step, a.max_iter - step, nj, 200000000ull /* 2 s of s_memrealtime (100 MHz) */);
+      if (hipGetLastError() != hipSuccess) return -1;
+      if (hipMemcpyAsync(host_flags + 2, a.s.pc + PC_ABORT, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        return -1;
+      if (host_flags[2]) return -2;  // a wait timed out: the launch drained without finishing
+      step += host_flags[3];  // steps the launch ran (it stopped at step index host_flags[3])
+      done = true;
+      break;
+    }
+#endif
     const int csz = live_bound > TAIL_ROWS ? CHUNK : TAIL_CHUNK;
     // row-tile workgroups per launch: one resident round, and no more than the live rows need
     const int lt = (live_bound + DEC_RT - 1) / DEC_RT < rt ? (live_bound + DEC_RT - 1) / DEC_RT : rt;

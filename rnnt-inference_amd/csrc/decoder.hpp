@@ -27,6 +27,7 @@ struct DecState {           // per-row greedy state, device arrays [Npad]
                              // {row | slot << 24 | symbols_added << 25, time | f_len << 16, idx, 0}
   int32_t* count;            // [4] list lengths {emit p0, live p0, emit p1, live p1} (8-byte aligned)
   int32_t* unfinished;       // [4] live-row counter (the fp32 decode loop)
+  uint32_t* pc;              // [8] persistent tail decode: per-role completion counters, abort word, steps run
 };
 
 struct DecArgs {
@@ -39,6 +40,7 @@ struct DecArgs {
   int32_t* res_len;        // [N]
   DecState s;
   int N, Npad, max_res, max_iter;
+  int persist_rows;        // live rows at or below which one persistent launch runs the rest (0 = off, <= 64)
 };
 
 // F = b_t + bf16(f) . W1t^T for every frame t < Tp and row tile holding a row with f_len > t

@@ -52,6 +52,7 @@ struct rnnt_engine {
   rnnt_opts opts{};
   int np_max = 0, tp_max = 0;
   int tile = ENC_TILE_AUTO;  // tick tile shape / flow (rnnt_engine_set_tile; RNNT_ENC_TILE at create)
+  int persist_rows = 0;      // persistent tail decode threshold (rnnt_engine_set_decode_persist; RNNT_DEC_PERSIST_ROWS at create)
   bool stream_prefix = false;  // stream chunks skip only trailing done tiles (RNNT_STREAM_PREFIX=1: A/B)
   // packed weights
   int8_t* enc_w[5] = {};
@@ -345,6 +346,7 @@ static int alloc_workspace(rnnt_engine* e) {
   r = r ? r : dev_alloc(e, &e->ds.live, 2 * NP);  // int4 entries
   r = r ? r : dev_alloc(e, &e->ds.count, 4);
   r = r ? r : dev_alloc(e, &e->ds.unfinished, 4);
+  r = r ? r : dev_alloc(e, &e->ds.pc, 8);
   if (!r && hipHostMalloc((void**)&e->host_flags, 4 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
     r = fail(RNNT_ENOMEM, "hipHostMalloc failed");
   for (int i = 0; i < 2 && !r; ++i)
@@ -400,6 +402,13 @@ extern "C" int rnnt_engine_set_tile(rnnt_engine* e, const char* tile) {
   return 0;
 }
 
+extern "C" int rnnt_engine_set_decode_persist(rnnt_engine* e, int rows) {
+  if (!e) return fail(RNNT_EINVAL, "null argument");
+  if (rows < 0 || rows > 64) return fail(RNNT_EINVAL, "persistent decode rows must be 0 (off) .. 64");
+  e->persist_rows = rows;
+  return 0;
+}
+
 extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, const rnnt_opts* opts,
                                   rnnt_engine** out) {
   if (!out) return fail(RNNT_EINVAL, "null argument");
@@ -421,6 +430,10 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   if (!r && !dscope.ok) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
   if (!r && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
+  if (const char* pr = getenv("RNNT_DEC_PERSIST_ROWS")) {  // development default, read once per engine
+    const int v = atoi(pr);
+    e->persist_rows = v < 0 ? 0 : (v > 64 ? 64 : v);
+  }
   if (const char* t = getenv("RNNT_ENC_TILE")) {  // development default, read once per engine
     const int v = tile_code(t);
     if (v < 0) r = fail(RNNT_EINVAL, std::string("RNNT_ENC_TILE=") + t + ": auto|ticks|flow|big|small|tiny|mini");
@@ -944,6 +957,7 @@ static int decode_core(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
   a.max_res = max_res;
   a.s = e->ds;
   a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
+  a.persist_rows = e->persist_rows;
   const int steps = launch_greedy_decode(a, e->host_flags, e->poll_ev, st, reset);
   if (steps < 0) return fail(RNNT_EDEVICE, "greedy launch failed");
   e->decode_steps += steps;

@@ -64,6 +64,7 @@ _SIGS = {
                                            C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "rnnt_engine_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "rnnt_engine_set_tile": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "rnnt_engine_set_decode_persist": (C.c_int, [C.c_void_p, C.c_int]),
     "rnnt_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(RnntStats), C.c_int]),
     "rnnt_abi_version": (C.c_int, []),
     "rnnt_stream_create": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),

@@ -220,6 +220,11 @@ class Engine:
         either way (rnnt_engine_set_tile)."""
         _lib.check(self._lib.rnnt_engine_set_tile(self._h, str(tile).encode()), "rnnt_engine_set_tile")
 
+    def set_decode_persist(self, rows):
+        """Run a decode call's last steps, once at most `rows` (1..64) rows are live, as one
+        persistent launch (rnnt_engine_set_decode_persist; 0 = off); tokens are identical."""
+        _lib.check(self._lib.rnnt_engine_set_decode_persist(self._h, int(rows)), "rnnt_engine_set_decode_persist")
+
     def stats(self, reset=True):
         st = _lib.RnntStats()
         _lib.check(self._lib.rnnt_engine_get_stats(self._h, C.byref(st), int(bool(reset))), "rnnt_engine_get_stats")

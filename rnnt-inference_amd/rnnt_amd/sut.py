@@ -244,9 +244,17 @@ class OfflineSUT:
 
     # ---- device hooks (a host-only test stands in for these; tests/test_sut_dist.py)
     def _stream_for(self, eng):
+        import os
         import torch
         if id(eng) not in self._streams:
-            self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
+            k = int(os.environ.get("RNNT_SUT_ENC_RESERVE", "0"))
+            if k > 0:  # development knob: the encoder off the first k CU slots of every XCD
+                from .engine import PartitionedStream, cu_mask_words
+                ps = PartitionedStream(eng.device, cu_mask_words(k, reserved=False))
+                self._streams[("ps", id(eng))] = ps  # keeps the HIP stream alive
+                self._streams[id(eng)] = ps.stream
+            else:
+                self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
         return self._streams[id(eng)]
 
     def _device_scope(self, eng, st):
@@ -271,16 +279,18 @@ class OfflineSUT:
         return res, rl
 
     def _dec_stream_for(self, eng):
-        """Development knob RNNT_SUT_DEC_PRIORITY=1: the decode of each engine runs on a second,
-        high-priority stream (the engine orders its calls across streams by its state event)."""
+        """Development knobs: RNNT_SUT_DEC_PRIORITY=1 runs the decode of each engine on a second,
+        high-priority stream; RNNT_SUT_ENC_RESERVE=k (encoder kept off k CU slots per XCD) runs it on a
+        second unrestricted stream.  The engine orders its calls across streams by its state event."""
         import os
         import torch
-        if os.environ.get("RNNT_SUT_DEC_PRIORITY", "0") != "1":
+        prio = os.environ.get("RNNT_SUT_DEC_PRIORITY", "0") == "1"
+        if not prio and int(os.environ.get("RNNT_SUT_ENC_RESERVE", "0")) <= 0:
             return None
         key = ("dec", id(eng))
         if key not in self._streams:
             lo, hi = torch.cuda.Stream.priority_range()
-            self._streams[key] = torch.cuda.Stream(device=eng.device, priority=min(lo, hi))
+            self._streams[key] = torch.cuda.Stream(device=eng.device, priority=min(lo, hi) if prio else 0)
         return self._streams[key]
 
     def _decode(self, eng, st, enc):

@@ -14,6 +14,7 @@ def fix(text):
     text = text.replace('asm volatile("s_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory")', 'emu_sync()')
     text = text.replace('asm volatile("s_waitcnt vmcnt(0)\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier" ::: "memory")', 'emu_sync()')
     text = text.replace('asm volatile("" : "+v"(c));', '')
+    text = text.replace('asm volatile("s_waitcnt vmcnt(0)" ::: "memory");', '')  # persistent decode (not emulated)
     text = text.replace('asm("v_and_b32 %0, 0xffffff, %1" : "=v"(r) : "v"(e));', 'r = e & 0xffffff;')
     text = re.sub(r'extern __shared__ (__attribute__\(\(aligned\(16\)\)\) )?(\w+) (\w+)\[\];',
                   r'static \1\2 \3[1 << 17];', text)
@@ -32,6 +33,6 @@ FEAT=""
 grep -q "g_dec_err" $SRC/decoder.hip && FEAT="$FEAT -DEMU_HAS_DEC_CHECK"
 grep -q "float\* ah0;" $SRC/decoder.hpp && FEAT="$FEAT -DEMU_HAS_AH"
 $CXX $SAN -g -std=c++20 -ffp-contract=off -pthread $FEAT \
-  -DRNNT_DEC_CHECK ${EMU_CFLAGS} -I$ROOT/tools/emu -I$OUT $ROOT/tools/emu/dec_emu.cpp $ROOT/oracle/rnnt_oracle.c \
+  -DRNNT_DEC_CHECK -DRNNT_EMU ${EMU_CFLAGS} -I$ROOT/tools/emu -I$OUT $ROOT/tools/emu/dec_emu.cpp $ROOT/oracle/rnnt_oracle.c \
   -o $OUT/dec_emu -lm
 echo "built $OUT/dec_emu"

@@ -151,6 +151,7 @@ int main(int argc, char** argv) {
   s.live = dalloc<int4>(2 * (size_t)Npad);
   s.count = dalloc<int32_t>(4);
   s.unfinished = dalloc<int32_t>(4);
+  s.pc = dalloc<uint32_t>(8);  // persistent tail decode counters (not emulated: RNNT_EMU builds it out)
   a.N = N;
   a.Npad = Npad;
   a.max_res = max_res;

@@ -98,6 +98,7 @@ timeline)
   timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace -o tl -- \
     python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/trace.log 2>&1 || die "trace rc=$?" $OUT/trace.log
   python3 tools/trace_query.py $OUT/trace > $OUT/timeline.txt && cat $OUT/timeline.txt
+  python3 tools/dec_overlap.py $OUT/trace > $OUT/dec_overlap.json && cat $OUT/dec_overlap.json
   [ -n "$KEEP_TRACE" ] || find $OUT/trace -name "*_kernel_trace.csv" -delete
   ;;
 multirank)

@@ -25,6 +25,7 @@ def main():
     rows.sort()
     t0 = rows[0][0]
     batches, cur = [], {}
+    dec_cur = {}  # decode queue -> batch (a decode may run on its own stream: RNNT_SUT_DEC_PRIORITY / ENC_RESERVE)
     buckets = (256, 512, 1024, 1 << 30)
     for s, e, n, q, g in rows:
         if n.startswith("quantize"):
@@ -32,16 +33,28 @@ def main():
             batches.append(b)
             cur[q] = b
             continue
-        b = cur.get(q)
-        if b is None:
-            continue
         if n.startswith("lstm_i8_tick_kernel"):
+            b = cur.get(q)
+            if b is None:
+                continue
             b["enc"][1] = e
             b["ticks"] += 1
             k = next(i for i, lim in enumerate(buckets) if g <= lim)
             b["hist"][k][0] += 1
             b["hist"][k][1] += (e - s) / 1e6
         elif n.startswith(("joint_trans", "dec_")):
+            if n.startswith("joint_trans"):
+                # a decode starts: the batch encoded on this queue if it has none yet, else (a decode
+                # on its own stream) the oldest encoded batch still without one
+                b = cur.get(q)
+                if b is None or b["dec"] is not None:
+                    b = next((x for x in batches if x["dec"] is None and x["enc"][1] <= s), None)
+                if b is None:
+                    continue
+                dec_cur[q] = b
+            b = dec_cur.get(q)
+            if b is None:
+                continue
             if b["dec"] is None:
                 b["dec"] = [s, e]
             b["dec"][1] = e
