@@ -823,27 +823,29 @@ __device__ __forceinline__ void dec_joint_body(const DecArgs& a, int parity, int
             if (best != BLANK && L.add_[m] != MAXSYM) {
               const int id = L.idx_[m] + 1;
               L.idx_[m] = id;
-              s.idx[row] = id;
-              if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
-              s.added[row] = ++L.add_[m];
-              s.preg[row] = best;
+              // persistent launch: write-through, as a row's next step may run on another XCD
+              // whose L2 would otherwise write back its own (newer) copy of the line first
+              st_b32<PS>(&s.idx[row], (uint32_t)id);
+              if (id < a.max_res) st_b32<PS>(&a.res[(size_t)row * a.max_res + id], (uint32_t)best);
+              st_b32<PS>(&s.added[row], (uint32_t)++L.add_[m]);
+              st_b32<PS>(&s.preg[row], (uint32_t)best);
               const int nsl = L.slot_[m] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
               L.slot_[m] = nsl;
-              s.slot[row] = nsl;
+              st_b32<PS>(&s.slot[row], (uint32_t)nsl);
               L.emit_e[m] = emit_entry(row, nsl, best);
               L.walking[m] = 0;
             } else {
               const int fl = L.flen_[m];
               int t = L.tidx[m] + 1;
               if (t >= fl) {
-                s.fin[row] = 1;
+                st_b32<PS>(&s.fin[row], 1u);
                 L.walking[m] = 0;
                 L.rows[m] = -1;  // finished: not in the next live list
                 t = fl - 1;
               }
               L.tidx[m] = t;
-              s.time[row] = t;
-              s.added[row] = 0;
+              st_b32<PS>(&s.time[row], (uint32_t)t);
+              st_b32<PS>(&s.added[row], 0u);
               L.add_[m] = 0;
             }
           }
