@@ -223,7 +223,7 @@ int rnnt_engine_set_tile(rnnt_engine* e, const char* tile);
 /* Greedy decode tail: once at most `rows` rows of a decode call are still live, one persistent
  * launch runs every remaining lock-step step (weight slices kept in registers, phases handed off
  * through device counters; results identical) instead of four launches per step.  0 = off,
- * 1..64; the environment variable RNNT_DEC_PERSIST_ROWS sets an engine's initial value.  No
+ * 1..512; the environment variable RNNT_DEC_PERSIST_ROWS sets an engine's initial value.  No
  * reference counterpart (the reference's loop is rnnt_model.hpp:92-124). */
 int rnnt_engine_set_decode_persist(rnnt_engine* e, int rows);
 int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset);

@@ -1040,9 +1040,9 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     return v && v[0] == '1';
   }();
   // persistent tail (dec_persist_kernel): once the live rows read back fit a.persist_rows, one launch
-  // runs every remaining step (0 = off; at most 64 rows: 4 joint workgroups)
+  // runs every remaining step (0 = off; at most DEC_PERSIST_MAX rows)
 #ifndef RNNT_EMU
-  const int PERSIST_ROWS = a.persist_rows < 0 ? 0 : (a.persist_rows > 64 ? 64 : a.persist_rows);
+  const int PERSIST_ROWS = a.persist_rows < 0 ? 0 : (a.persist_rows > DEC_PERSIST_MAX ? DEC_PERSIST_MAX : a.persist_rows);
   static std::atomic<uint64_t> ps_attr{0};
 #else
   constexpr int PERSIST_ROWS = 0;

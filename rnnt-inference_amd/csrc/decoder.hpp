@@ -30,6 +30,9 @@ struct DecState {           // per-row greedy state, device arrays [Npad]
   uint32_t* pc;              // [8] persistent tail decode: per-role completion counters, abort word, steps run
 };
 
+// the persistent tail decode takes at most this many live rows (32 joint workgroups)
+constexpr int DEC_PERSIST_MAX = 512;
+
 struct DecArgs {
   DecWeights w;
   const float* F;          // [Tp][Npad][512] joint trans half, F = b_t + bf16(f).W1t^T
@@ -40,7 +43,7 @@ struct DecArgs {
   int32_t* res_len;        // [N]
   DecState s;
   int N, Npad, max_res, max_iter;
-  int persist_rows;        // live rows at or below which one persistent launch runs the rest (0 = off, <= 64)
+  int persist_rows;        // live rows at or below which one persistent launch runs the rest (0 = off, <= DEC_PERSIST_MAX)
 };
 
 // F = b_t + bf16(f) . W1t^T for every frame t < Tp and row tile holding a row with f_len > t

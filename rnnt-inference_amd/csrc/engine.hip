@@ -404,7 +404,7 @@ extern "C" int rnnt_engine_set_tile(rnnt_engine* e, const char* tile) {
 
 extern "C" int rnnt_engine_set_decode_persist(rnnt_engine* e, int rows) {
   if (!e) return fail(RNNT_EINVAL, "null argument");
-  if (rows < 0 || rows > 64) return fail(RNNT_EINVAL, "persistent decode rows must be 0 (off) .. 64");
+  if (rows < 0 || rows > DEC_PERSIST_MAX) return fail(RNNT_EINVAL, "persistent decode rows must be 0 (off) .. 512");
   e->persist_rows = rows;
   return 0;
 }
@@ -432,7 +432,7 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
   if (const char* pr = getenv("RNNT_DEC_PERSIST_ROWS")) {  // development default, read once per engine
     const int v = atoi(pr);
-    e->persist_rows = v < 0 ? 0 : (v > 64 ? 64 : v);
+    e->persist_rows = v < 0 ? 0 : (v > DEC_PERSIST_MAX ? DEC_PERSIST_MAX : v);
   }
   if (const char* t = getenv("RNNT_ENC_TILE")) {  // development default, read once per engine
     const int v = tile_code(t);

@@ -38,7 +38,7 @@ def _run(pm, x, lens, persist, n_pad=256):
         eng.close()
 
 
-@pytest.mark.parametrize("persist", [1, 16, 64])
+@pytest.mark.parametrize("persist", [1, 16, 64, 512])
 def test_persistent_tail_matches_oracle(model, oracle, persist):
     """40 rows of mixed lengths: the persistent launch takes over after the first 32-step chunk
     (64: nearly the whole decode; 1: only the last row), token-identical to the restatement."""
@@ -54,15 +54,17 @@ def test_persistent_tail_matches_oracle(model, oracle, persist):
 
 
 def test_persistent_tail_equals_four_launch_loop(model):
-    """A 256-row batch of dev-clean-shaped lengths: the persistent tail (32 rows) and the
-    four-launch loop give the same tokens, and the step count agrees."""
-    lens = np.minimum(synthetic.devclean_lengths(256, seed=73), 160).astype(np.int32)
+    """A 512-row batch of dev-clean-shaped lengths: the persistent tail (32, 256 and 512 rows: 2 to
+    32 joint workgroups, prediction workgroups looping over up to 16 row tiles) and the four-launch
+    loop give the same tokens."""
+    lens = np.minimum(synthetic.devclean_lengths(512, seed=73), 160).astype(np.int32)
     T = int(lens.max())
     x = synthetic.make_features(T, len(lens), seed=74, lens=lens)
-    r0, l0, s0, _ = _run(model, x, lens, 0)
-    r1, l1, s1, _ = _run(model, x, lens, 32)
-    np.testing.assert_array_equal(l1, l0)
-    np.testing.assert_array_equal(r1, r0)
+    r0, l0, _, _ = _run(model, x, lens, 0, n_pad=512)
+    for persist in (32, 256, 512):
+        r1, l1, _, _ = _run(model, x, lens, persist, n_pad=512)
+        np.testing.assert_array_equal(l1, l0)
+        np.testing.assert_array_equal(r1, r0)
 
 
 def test_persistent_tail_at_the_cap(golden, oracle):
