@@ -930,7 +930,7 @@ __device__ __forceinline__ bool pc_wait(uint32_t* pc, int who, unsigned need, un
 // one role's step loop; Body(parity) runs the step body
 template <class Body>
 __device__ __forceinline__ void ps_loop(const DecArgs& a, uint32_t* pc, int role, int prev, unsigned n_prev, int step0,
-                                        int max_steps, unsigned long long timeout, int* lds_flag, Body&& body) {
+                                        int max_steps, unsigned long long timeout, int* lds_flag, int last_j, Body&& body) {
   const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
   for (int k = 0;; ++k) {
     const int parity = (step0 + k) & 1;
@@ -944,13 +944,26 @@ __device__ __forceinline__ void ps_loop(const DecArgs& a, uint32_t* pc, int role
     __syncthreads();
     const int stop = __builtin_amdgcn_readfirstlane(lds_flag[0]);
     if (stop == 2) return;  // aborted: leave without publishing (every waiter sees the abort word)
+    ST_MARK(ps0);
     if (!stop) body(parity);
-    // publish: every wave's write-through stores have landed, then one count
+    ST_MARK(ps1);
+    // publish: every wave's stores have landed, then one count
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
+#ifdef RNNT_DEV_STAMPS
+      {  // record (16 + role, workgroup | step << 16, ready, body end, stores drained, published)
+        const unsigned long long ps2 = __builtin_amdgcn_s_memrealtime();
+        const unsigned k_ = atomicAdd(&g_st_n, 1u);
+        if (k_ < (1u << 22) / 6) {
+          g_st[6 * k_] = 16 + role; g_st[6 * k_ + 1] = blockIdx.x + 65536ull * k;
+          g_st[6 * k_ + 2] = ps0; g_st[6 * k_ + 3] = ps1; g_st[6 * k_ + 4] = ps2;
+          g_st[6 * k_ + 5] = __builtin_amdgcn_s_memrealtime();
+        }
+      }
+#endif
       __hip_atomic_fetch_add(pc + role, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (stop && role == PC_J && blockIdx.x == PS_P0 + PS_P1 + PS_G) __hip_atomic_store(pc + PC_STEPS, (uint32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stop && last_j) __hip_atomic_store(pc + PC_STEPS, (uint32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (stop) return;
     __syncthreads();  // lds_flag is rewritten by the next step
@@ -973,26 +986,26 @@ __global__ void __launch_bounds__(256) dec_persist_kernel(DecArgs a, uint32_t* p
     PredRegs<0> W;
     auto X = (uint16_t(*)[pred_xp(0)])psm;
     auto E = (int(*)[DEC_RT])(psm + sizeof(uint16_t) * DEC_RT * pred_xp(0));
-    ps_loop(a, pc, PC_P0, PC_J, (unsigned)nj, step0, max_steps, timeout, flag,
+    ps_loop(a, pc, PC_P0, PC_J, (unsigned)nj, step0, max_steps, timeout, flag, 0,
             [&](int p) { dec_pred_body<0, 4, true>(a, p, GridXY{b, 0, 1}, X, E, W); });
   } else if (b < PS_P0 + PS_P1) {
     PredRegs<1> W;
     auto X = (uint16_t(*)[pred_xp(1)])psm;
     auto E = (int(*)[DEC_RT])(psm + sizeof(uint16_t) * DEC_RT * pred_xp(1));
-    ps_loop(a, pc, PC_P1, PC_P0, (unsigned)PS_P0, step0, max_steps, timeout, flag,
+    ps_loop(a, pc, PC_P1, PC_P0, (unsigned)PS_P0, step0, max_steps, timeout, flag, 0,
             [&](int p) { dec_pred_body<1, 4, true>(a, p, GridXY{b - PS_P0, 0, 1}, X, E, W); });
   } else if (b < PS_P0 + PS_P1 + PS_G) {
     GRegs W;
     auto X = (uint16_t(*)[GXP])psm;
     auto E = (int(*)[DEC_RT])(psm + sizeof(uint16_t) * DEC_RT * GXP);
     const int g = b - PS_P0 - PS_P1;
-    ps_loop(a, pc, PC_G, PC_P1, (unsigned)PS_P1, step0, max_steps, timeout, flag,
+    ps_loop(a, pc, PC_G, PC_P1, (unsigned)PS_P1, step0, max_steps, timeout, flag, 0,
             [&](int p) { dec_g_body<true>(a, p, GridXY{g, 0, 1}, g == 0, X, E, W); });
   } else {
     JointRegs W;
     JointLds& L = *(JointLds*)psm;
     const int jg = b - PS_P0 - PS_P1 - PS_G;
-    ps_loop(a, pc, PC_J, PC_G, (unsigned)PS_G, step0, max_steps, timeout, flag,
+    ps_loop(a, pc, PC_J, PC_G, (unsigned)PS_G, step0, max_steps, timeout, flag, jg == 0,
             [&](int p) { dec_joint_body<true>(a, p, jg, nj, L, W); });
   }
 }
