@@ -1052,6 +1052,16 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const char* v = getenv("RNNT_DEC_SPIN");
     return v && v[0] == '1';
   }();
+  // development knob RNNT_DEC_RG="pred,g,joint": row-group caps of the step kernels' grids
+  static const int* RG = [] {
+    static int rg[3] = {PRED_ROW_GROUPS, G_ROW_GROUPS, JOINT_GROUPS};
+    if (const char* v = getenv("RNNT_DEC_RG")) {
+      int x[3];
+      if (sscanf(v, "%d,%d,%d", &x[0], &x[1], &x[2]) == 3 && x[0] > 0 && x[1] > 0 && x[2] > 0)
+        for (int i = 0; i < 3; ++i) rg[i] = x[i];
+    }
+    return rg;
+  }();
   // persistent tail (dec_persist_kernel): once the live rows read back fit a.persist_rows, one launch
   // runs every remaining step (0 = off; at most DEC_PERSIST_MAX rows)
 #ifndef RNNT_EMU
@@ -1087,10 +1097,10 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     // row-tile workgroups per launch: one resident round, and no more than the live rows need
     const int lt = (live_bound + DEC_RT - 1) / DEC_RT < rt ? (live_bound + DEC_RT - 1) / DEC_RT : rt;
     const int lt1 = lt > 0 ? lt : 1;
-    const int rg_pred = lt1 < PRED_ROW_GROUPS ? lt1 : PRED_ROW_GROUPS;
-    const int rg_g = lt1 < G_ROW_GROUPS ? lt1 : G_ROW_GROUPS;
+    const int rg_pred = lt1 < RG[0] ? lt1 : RG[0];
+    const int rg_g = lt1 < RG[1] ? lt1 : RG[1];
     const int ljt = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
-    const int rg_joint = ljt < JOINT_GROUPS ? ljt : JOINT_GROUPS;
+    const int rg_joint = ljt < RG[2] ? ljt : RG[2];
     for (int i = 0; i < csz && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
       hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
