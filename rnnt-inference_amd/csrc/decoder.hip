@@ -1052,12 +1052,12 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const char* v = getenv("RNNT_DEC_SPIN");
     return v && v[0] == '1';
   }();
-  // development knob RNNT_DEC_RG="pred,g,joint": row-group caps of the step kernels' grids
+  // development knob RNNT_DEC_RG="PxGxJ": row-group caps of the step kernels' grids (pred, G, joint)
   static const int* RG = [] {
     static int rg[3] = {PRED_ROW_GROUPS, G_ROW_GROUPS, JOINT_GROUPS};
     if (const char* v = getenv("RNNT_DEC_RG")) {
       int x[3];
-      if (sscanf(v, "%d,%d,%d", &x[0], &x[1], &x[2]) == 3 && x[0] > 0 && x[1] > 0 && x[2] > 0)
+      if (sscanf(v, "%dx%dx%d", &x[0], &x[1], &x[2]) == 3 && x[0] > 0 && x[1] > 0 && x[2] > 0)
         for (int i = 0; i < 3; ++i) rg[i] = x[i];
     }
     return rg;
