@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--early-decodes", type=int, default=None,
                     help="only the first K batches decode beside the next encoder; the others wait for every encode "
                          "(default: all decode right after their encode)")
+    ap.add_argument("--batch-order", default=None,
+                    help="development: this rank's batches in another order, a permutation of their indices "
+                         "(e.g. 0,5,1,4,2,3; default: longest first)")
     ap.add_argument("--cpu-sample", type=int, default=256, help="utterances timed on the CPU restatement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wav", action="store_true",
@@ -410,6 +413,11 @@ def main():
             claim = dist.claim_for_query(qno[0], len(batches))
         else:
             batches, claim = dist.shard_query(qsl, ids, idx, args.batch, rank, world, sizes), None
+            if args.batch_order:
+                order = [int(v) for v in args.batch_order.split(",")]
+                if sorted(order) != list(range(len(batches))):
+                    raise SystemExit(f"--batch-order must permute 0..{len(batches) - 1}")
+                batches = [batches[i] for i in order]
         stream = dist.ResponseStream(world, ggroup, tag=qno[0]) if world > 1 else None
         qno[0] += 1
         sut.on_batch = stream.push if stream else None
