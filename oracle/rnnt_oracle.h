@@ -66,7 +66,8 @@ void oracle_encoder_i8(int T, int N, const float* feat, const int32_t* lens,
                        int8_t* h_state, uint16_t* c_state);
 
 /* fp32 LSTM layer (QuantLSTMLayer.forward with no quantizers, quant_lstm.py:162-183):
- * gates = (b_ih + x.W_ih^T) + (b_hh + h.W_hh^T), each dot a k-ordered fmaf chain. */
+ * gates = (b_ih + x.W_ih^T) + (b_hh + h.W_hh^T), each dot k-ordered fmaf chains over 512-k
+ * segments summed in segment order (the GPU fp32 encoder's contract). */
 void oracle_lstm_f32_layer(int T, int N, int I, int H, const float* x, const float* Wih,
                            const float* Whh, const float* bih, const float* bhh, float* h,
                            float* c, float* y);

@@ -27,7 +27,9 @@ struct EncF32StepArgs {
   int mode, t, half, zero_next;
 };
 
-int launch_lstm_f32_step(const EncF32StepArgs& a, hipStream_t st);
+// The fp32 contract's chain segment (oracle_lstm_f32_layer): a gate's x and h dot products are
+// k-ordered fma chains over 512-k segments, summed in segment order, the first from the bias.
+constexpr int ENC_F32_SEG = 512;
 
 // One launch = one wavefront tick of the fp32 stack (the int8 encoder's schedule, engine.hip):
 // up to 5 independent layer-steps over the same n rows (n_pad a multiple of 64).

@@ -1,8 +1,9 @@
 """fp32 transcription on the GPU (BASELINE config 2: the encoder LSTM stack only, fp32, N=32).
 
-The GPU path (csrc/encoder_f32.hip) uses k-ordered fp32 fma chains on v_mfma_f32_16x16x4_f32,
-so it is bit-exact with the CPU restatement (oracle_encoder_f32) and inherits its tolerance to
-the reference's own fp32 Transcription output (tests/golden: max |diff| < 2e-4)."""
+The GPU path (csrc/encoder_f32.hip) uses k-ordered fp32 fma chains on v_mfma_f32_16x16x4_f32 over
+512-k segments summed in segment order (one wave per segment), so it is bit-exact with the CPU
+restatement (oracle_encoder_f32, the same segments) and inherits its tolerance to the reference's
+own fp32 Transcription output (tests/golden: max |diff| < 2e-4)."""
 import numpy as np
 import pytest
 import torch
