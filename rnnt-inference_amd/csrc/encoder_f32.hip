@@ -25,121 +25,139 @@ namespace rnnt {
 // 1.3 M MFMAs spread over 3-6x the waves, so the chip's fp32 MFMA pipes, not the longest chain,
 // bound the tick.
 constexpr int F32_NJ = 2;  // 16-row batch tiles per wave
-template <int NJ>
-__device__ __forceinline__ void chain_rows_pf(const float* __restrict__ a, const float* const* b, int K, v4f* acc) {
-  // chain_rows with the next 32-k block's operands loaded before this block's MFMAs
-  const int nb = K >> 5;
-  float4 a0 = *(const float4*)a, a1 = *(const float4*)(a + 4), b0[NJ], b1[NJ];
+#ifndef RNNT_F32_PF  // development: tools/build_variants.sh "pf2:-DRNNT_F32_PF=2"
+#define RNNT_F32_PF 2
+#endif
+#ifndef RNNT_F32_GT  // development: gate tiles per wave
+#define RNNT_F32_GT 2
+#endif
+constexpr int F32_PF = RNNT_F32_PF;  // 32-k blocks of operands in flight per chain
+constexpr int F32_GT = RNNT_F32_GT;  // 16-row gate tiles per wave (sharing each activation block)
+// GT x NJ chains (GT 16-row gate tiles x NJ 16-row batch tiles) over the same k range, with the
+// operands of the next D 32-k blocks in flight (a register ring: block j in slot j % D).  Each
+// activation block feeds GT gate tiles and each weight block NJ batch tiles, so a wave moves
+// (GT + NJ) / (GT NJ) of the bytes one chain would per MFMA.  K's final half block (K & 16:
+// instructions i = 0..3, k = 32 nb + 4i + q) rides in the ring as block nb.
+template <int GT, int NJ, int D>
+__device__ __forceinline__ void chain_tiles(const float* const* a, const float* const* b, int K, v4f (*acc)[NJ]) {
+  const int nb = K >> 5, nl = nb + ((K & 16) ? 1 : 0);  // full blocks, blocks to load
+  float4 ra0[D][GT], ra1[D][GT], rb0[D][NJ], rb1[D][NJ];
+  auto load = [&](int i, int j) __attribute__((always_inline)) {  // block j into slot i
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    b0[j] = *(const float4*)b[j];
-    b1[j] = *(const float4*)(b[j] + 4);
+    for (int g = 0; g < GT; ++g) {
+      ra0[i][g] = *(const float4*)(a[g] + 32 * j);
+      ra1[i][g] = *(const float4*)(a[g] + 32 * j + 4);
+    }
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) {
+      rb0[i][t] = *(const float4*)(b[t] + 32 * j);
+      rb1[i][t] = *(const float4*)(b[t] + 32 * j + 4);
+    }
+  };
+  auto step4 = [&](const float4* av, const float4* bv) __attribute__((always_inline)) {  // 4 k of every chain
+#pragma unroll
+    for (int g = 0; g < GT; ++g)
+#pragma unroll
+      for (int t = 0; t < NJ; ++t) {
+        acc[g][t] = MFMA4(av[g].x, bv[t].x, acc[g][t]);
+        acc[g][t] = MFMA4(av[g].y, bv[t].y, acc[g][t]);
+        acc[g][t] = MFMA4(av[g].z, bv[t].z, acc[g][t]);
+        acc[g][t] = MFMA4(av[g].w, bv[t].w, acc[g][t]);
+      }
+  };
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < nl) load(i, i);
+  for (int blk = 0; blk < nb; blk += D) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      if (blk + i < nb) {  // uniform
+        step4(ra0[i], rb0[i]);
+        step4(ra1[i], rb1[i]);
+        if (blk + i + D < nl) load(i, blk + i + D);
+      }
+    }
   }
-  for (int blk = 0; blk < nb; ++blk) {
-    // next block; after the last full block, the half block (rows are padded to 32-k blocks) or a
-    // harmless re-read of the current one
-    const int nx = (blk + 1 < nb || (K & 16)) ? blk + 1 : blk;
-    const float4 na0 = *(const float4*)(a + 32 * nx), na1 = *(const float4*)(a + 32 * nx + 4);
-    float4 nb0[NJ], nb1[NJ];
+  if (K & 16) {  // the half block, in slot nb % D
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      nb0[j] = *(const float4*)(b[j] + 32 * nx);
-      nb1[j] = *(const float4*)(b[j] + 32 * nx + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      acc[j] = MFMA4(a0.x, b0[j].x, acc[j]);
-      acc[j] = MFMA4(a0.y, b0[j].y, acc[j]);
-      acc[j] = MFMA4(a0.z, b0[j].z, acc[j]);
-      acc[j] = MFMA4(a0.w, b0[j].w, acc[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      acc[j] = MFMA4(a1.x, b1[j].x, acc[j]);
-      acc[j] = MFMA4(a1.y, b1[j].y, acc[j]);
-      acc[j] = MFMA4(a1.z, b1[j].z, acc[j]);
-      acc[j] = MFMA4(a1.w, b1[j].w, acc[j]);
-    }
-    a0 = na0;
-    a1 = na1;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      b0[j] = nb0[j];
-      b1[j] = nb1[j];
-    }
-  }
-  if (K & 16) {  // half block: instructions i = 0..3 (k = 32 nb + 4i + q)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      acc[j] = MFMA4(a0.x, b0[j].x, acc[j]);
-      acc[j] = MFMA4(a0.y, b0[j].y, acc[j]);
-      acc[j] = MFMA4(a0.z, b0[j].z, acc[j]);
-      acc[j] = MFMA4(a0.w, b0[j].w, acc[j]);
-    }
+    for (int i = 0; i < D; ++i)
+      if (i == nb % D) step4(ra0[i], rb0[i]);
   }
 }
 
-// workgroups of one job: 256 gate tiles x the batch groups; jobs longest K first
+// workgroups of one job: 256 / F32_GT gate-tile groups x the batch groups; jobs longest K first
 constexpr int F32_WAVES = (2048 + ENC_F32_SEG - 1) / ENC_F32_SEG + 1024 / ENC_F32_SEG;  // layer 2: 4 + 2
 __global__ void __launch_bounds__(F32_WAVES * 64) lstm_f32_tick_kernel(EncF32TickArgs args, int nbg) {
-  __shared__ v4f part[F32_WAVES][F32_NJ][64];
+  __shared__ v4f part[F32_WAVES][F32_GT][F32_NJ][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane >> 4, c = lane & 15;
-  const int per_job = (G4 / 16) * nbg;
+  constexpr int NGG = G4 / (16 * F32_GT);  // gate-tile groups per layer-step
+  const int per_job = NGG * nbg;
   const int jsel = blockIdx.x / per_job, rest = blockIdx.x % per_job;
   const EncF32StepArgs& a = args.job[jsel];
-  const int gt = rest % (G4 / 16);             // 16-row gate tile = units 4gt .. 4gt+3
-  const int n0 = (rest / (G4 / 16)) * (16 * F32_NJ);
-  const int row = gt * 16 + c;                 // packed gate row fed by this lane (A operand)
+  const int gt0 = (rest % NGG) * F32_GT;       // 16-row gate tiles gt0 .. (units 4gt .. 4gt+3 each)
+  const int n0 = (rest / NGG) * (16 * F32_NJ);
   const int sx = (a.I + ENC_F32_SEG - 1) / ENC_F32_SEG, sh = H / ENC_F32_SEG;
   if (wave < sx + sh) {
     const bool xs = wave < sx;
     const int k0 = (xs ? wave : wave - sx) * ENC_F32_SEG;
     const int K = xs ? (a.I - k0 < ENC_F32_SEG ? a.I - k0 : ENC_F32_SEG) : ENC_F32_SEG;
-    v4f acc[F32_NJ];
+    v4f acc[F32_GT][F32_NJ];
+    const float* ap[F32_GT];
     const float* bp[F32_NJ];
-    float4 b0 = float4{0.0f, 0.0f, 0.0f, 0.0f};  // a chain's first segment starts at its bias
-    if (k0 == 0) b0 = *(const float4*)((xs ? a.bih : a.bhh) + gt * 16 + 4 * q);
 #pragma unroll
-    for (int j = 0; j < F32_NJ; ++j) {
-      acc[j] = v4f{b0.x, b0.y, b0.z, b0.w};
-      bp[j] = (xs ? a.x + (size_t)(n0 + j * 16 + c) * a.Ip : a.h_in + (size_t)(n0 + j * 16 + c) * H) + 8 * q + k0;
+    for (int g = 0; g < F32_GT; ++g) {
+      const int gt = gt0 + g;
+      float4 b0 = float4{0.0f, 0.0f, 0.0f, 0.0f};  // a chain's first segment starts at its bias
+      if (k0 == 0) b0 = *(const float4*)((xs ? a.bih : a.bhh) + gt * 16 + 4 * q);
+#pragma unroll
+      for (int j = 0; j < F32_NJ; ++j) acc[g][j] = v4f{b0.x, b0.y, b0.z, b0.w};
+      const int row = gt * 16 + c;  // packed gate row fed by this lane (A operand)
+      ap[g] = (xs ? a.wih + (size_t)row * a.Ip : a.whh + (size_t)row * H) + 8 * q + k0;
     }
-    chain_rows_pf<F32_NJ>((xs ? a.wih + (size_t)row * a.Ip : a.whh + (size_t)row * H) + 8 * q + k0, bp, K, acc);
 #pragma unroll
-    for (int j = 0; j < F32_NJ; ++j) part[wave][j][lane] = acc[j];
+    for (int j = 0; j < F32_NJ; ++j)
+      bp[j] = (xs ? a.x + (size_t)(n0 + j * 16 + c) * a.Ip : a.h_in + (size_t)(n0 + j * 16 + c) * H) + 8 * q + k0;
+    chain_tiles<F32_GT, F32_NJ, F32_PF>(ap, bp, K, acc);
+#pragma unroll
+    for (int g = 0; g < F32_GT; ++g)
+#pragma unroll
+      for (int j = 0; j < F32_NJ; ++j) part[wave][g][j][lane] = acc[g][j];
   }
   __syncthreads();
   if (wave) return;
-  // C/D: lane (q, c) holds rows 4q..4q+3 of the tile = gates i,f,g,o of unit 4gt+q, batch row c
-  const int u = gt * 4 + q;
+  // C/D: lane (q, c) holds rows 4q..4q+3 of a tile = gates i,f,g,o of unit 4gt+q, batch row c
 #pragma unroll
-  for (int j = 0; j < F32_NJ; ++j) {
-    const int n = n0 + j * 16 + c;
-    if (n >= a.n) continue;
-    v4f ax = part[0][j][lane], ah = part[sx][j][lane];
-    for (int s = 1; s < sx; ++s) ax = ax + part[s][j][lane];  // segment order: ((s0 + s1) + s2) + ...
-    for (int s = 1; s < sh; ++s) ah = ah + part[sx + s][j][lane];
-    const float ig = det_sigmoid(ax[0] + ah[0]);
-    const float fg = det_sigmoid(ax[1] + ah[1]);
-    const float gg = det_tanh(ax[2] + ah[2]);
-    const float og = det_sigmoid(ax[3] + ah[3]);
-    float* cp = a.c + (size_t)n * H + u;
-    const float cn = fg * *cp + ig * gg;
-    *cp = cn;
-    const float hh = og * det_tanh(cn);
-    a.h_out[(size_t)n * H + chain_pos(u)] = hh;
-    if (a.mode == ENC_F32_NEXT) {
-      a.y[(size_t)n * H + chain_pos(u)] = hh;
-    } else if (a.mode == ENC_F32_STACKED) {
-      // StackTime.forward_f32 (modeling_rnnt.py:314-324): frame t -> stacked frame t/2, half
-      // t%2, frames t >= x_lens[n] zeroed, odd-T pad frame zero
-      float* dst = a.y + (size_t)n * 2 * H + chain_pos(u);
-      dst[a.half * H] = a.t < a.lens[n] ? hh : 0.0f;
-      if (a.zero_next) dst[H] = 0.0f;
-    } else {
-      if (a.y) a.y[(size_t)n * H + u] = hh;
-      if (a.y2) a.y2[(size_t)n * H + chain_pos(u)] = hh;
-      if (a.ybf) a.ybf[(size_t)n * H + u] = f2bf_ftz(hh);
+  for (int g = 0; g < F32_GT; ++g) {
+    const int u = (gt0 + g) * 4 + q;
+#pragma unroll
+    for (int j = 0; j < F32_NJ; ++j) {
+      const int n = n0 + j * 16 + c;
+      if (n >= a.n) continue;
+      v4f ax = part[0][g][j][lane], ah = part[sx][g][j][lane];
+      for (int s = 1; s < sx; ++s) ax = ax + part[s][g][j][lane];  // segment order: ((s0 + s1) + s2) + ...
+      for (int s = 1; s < sh; ++s) ah = ah + part[sx + s][g][j][lane];
+      const float ig = det_sigmoid(ax[0] + ah[0]);
+      const float fg = det_sigmoid(ax[1] + ah[1]);
+      const float gg = det_tanh(ax[2] + ah[2]);
+      const float og = det_sigmoid(ax[3] + ah[3]);
+      float* cp = a.c + (size_t)n * H + u;
+      const float cn = fg * *cp + ig * gg;
+      *cp = cn;
+      const float hh = og * det_tanh(cn);
+      a.h_out[(size_t)n * H + chain_pos(u)] = hh;
+      if (a.mode == ENC_F32_NEXT) {
+        a.y[(size_t)n * H + chain_pos(u)] = hh;
+      } else if (a.mode == ENC_F32_STACKED) {
+        // StackTime.forward_f32 (modeling_rnnt.py:314-324): frame t -> stacked frame t/2, half
+        // t%2, frames t >= x_lens[n] zeroed, odd-T pad frame zero
+        float* dst = a.y + (size_t)n * 2 * H + chain_pos(u);
+        dst[a.half * H] = a.t < a.lens[n] ? hh : 0.0f;
+        if (a.zero_next) dst[H] = 0.0f;
+      } else {
+        if (a.y) a.y[(size_t)n * H + u] = hh;
+        if (a.y2) a.y2[(size_t)n * H + chain_pos(u)] = hh;
+        if (a.ybf) a.ybf[(size_t)n * H + u] = f2bf_ftz(hh);
+      }
     }
   }
 }
@@ -153,7 +171,7 @@ int launch_lstm_f32_tick(const EncF32TickArgs& a, hipStream_t st) {
   for (int j = 0; j < a.njobs; ++j)  // the workgroup's waves cover the segments of the widest input
     if ((a.job[j].I + ENC_F32_SEG - 1) / ENC_F32_SEG + H / ENC_F32_SEG > F32_WAVES) return -1;
   const int nbg = (n + 16 * F32_NJ - 1) / (16 * F32_NJ);  // rows < n_pad (a multiple of 64) stay in bounds
-  hipLaunchKernelGGL(lstm_f32_tick_kernel, dim3(a.njobs * (G4 / 16) * nbg), dim3(F32_WAVES * 64), 0, st, a, nbg);
+  hipLaunchKernelGGL(lstm_f32_tick_kernel, dim3(a.njobs * (G4 / (16 * F32_GT)) * nbg), dim3(F32_WAVES * 64), 0, st, a, nbg);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -6,7 +6,7 @@ set -e
 cd "$(dirname "$0")/../rnnt-inference_amd/csrc"
 OUTD=../../build_dev
 mkdir -p $OUTD
-HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w"
+HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w -fno-slp-vectorize -Xclang -target-feature -Xclang -packed-fp32-ops"
 build() {
   local name=$1; shift
   local objs=""
