@@ -3,9 +3,10 @@
 
 Workload (BASELINE.json metric / config 4): LoadGen's Offline scenario over a
 LibriSpeech-dev-clean-shaped QSL of 2513 synthetic utterances (mlperf.conf:13), features resident
-in HBM on every GPU.  One step = one Offline query of --query samples per GPU (default 24576 =
-*.Offline.min_query_count, mlperf.conf:63; LoadGen repeats the QSL), issued exactly as the SUT
-serves it, all inside the timed region:
+in HBM on every GPU.  One step = one Offline query of --query samples per GPU (default 300000 =
+the reference's own Offline.min_query_count, configs/user.conf:6, which launch_sut.sh:46 passes to
+LoadGen; mlperf.conf:63's rule minimum is 24576; LoadGen repeats the QSL), issued exactly as the
+SUT serves it, all inside the timed region:
   * sort the query longest first (rnnt_qsl.cpp:104-133) and split it into batches of --batch;
     with several ranks (one process per GPU) every rank claims the next batch from one shared
     counter whenever its encoder is free (rnnt_amd.dist.BatchClaim; --deal static: snake deal);
@@ -54,7 +55,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--qsl", type=int, default=2513, help="QSL utterances (mlperf.conf:13)")
-    ap.add_argument("--query", type=int, default=24576, help="Offline query samples per GPU (mlperf.conf:63)")
+    ap.add_argument("--query", type=int, default=300000,
+                    help="Offline query samples per GPU (default: the reference's user.conf:6 Offline.min_query_count; "
+                         "mlperf.conf:63's rule minimum is 24576)")
     ap.add_argument("--batch", type=int, default=4096,
                     help="utterances per encode+decode call (4096 x 4 in flight measured 110-112k utt/s vs 106k for "
                          "8192 x 3 and 102k for 3072 x 8 on one box: smaller batches shorten the last batch's decode "
@@ -508,6 +511,8 @@ def main():
                  else "synthetic (seeded dev-clean-shaped lengths, N(0,1) features, random-init RNN-T weights)"),
         "config": {"workload": "MLPerf Offline query over a LibriSpeech-dev-clean-shaped QSL (BASELINE config 4)",
                    "qsl": args.qsl, "query_samples": query, "query_samples_per_gpu": args.query,
+                   "query_source": ("configs/user.conf:6 Offline.min_query_count (the reference's run setting, "
+                                    "launch_sut.sh:46)" if args.query == 300000 else "--query"),
                    "batch_size": args.batch, "batch_sizes": sizes, "batches_in_flight_per_gpu": args.inflight,
                    "input": ("16 kHz audio: GPU featurizer (FilterbankFeatures.forward) in the timed region" if args.wav
                              else "log-mel features resident in HBM, gathered by the encoder's quantize pass"),
