@@ -58,10 +58,10 @@ def parse():
     ap.add_argument("--query", type=int, default=300000,
                     help="Offline query samples per GPU (default: the reference's user.conf:6 Offline.min_query_count; "
                          "mlperf.conf:63's rule minimum is 24576)")
-    ap.add_argument("--batch", type=int, default=4096,
-                    help="utterances per encode+decode call (4096 x 4 in flight measured 110-112k utt/s vs 106k for "
-                         "8192 x 3 and 102k for 3072 x 8 on one box: smaller batches shorten the last batch's decode "
-                         "tail, below 4096 the encoder's tiles underfill the chip)")
+    ap.add_argument("--batch", type=int, default=6144,
+                    help="utterances per encode+decode call (300000-sample query, 4 in flight, one box: 6144 "
+                         "123.1-124.9k utt/s, 4096 121.4-122.6k, 8192 x 3 122.0-123.3k, 8192 x 2 105.5k: with two "
+                         "engines the encoder waits for a free one; MEASUREMENTS.md section 8)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="engines per GPU (one HIP stream + host thread each): one batch's latency-bound greedy "
                          "decode overlaps the next batch's encoder")
