@@ -557,7 +557,7 @@ __device__ __forceinline__ void flow_acquire() {  // wave 0; the other waves mee
 template <int WMT, int WNT, int NBUF>
 __global__ void __launch_bounds__(NWAVE * 64) lstm_i8_flow_kernel(EncFlowArgs f) {
   using C = TileCfg<WMT, WNT, NBUF>;
-  static_assert(C::NGT == ENC_FLOW_NGT, "flow task blocks");
+  static_assert(C::NGT == ENC_FLOW_NGT || C::NGT == ENC_FLOW_BIG_NGT, "flow task blocks");
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   // [0] task index, [1] recurrent input ready (an LDS pointer: ds ops, not flat)
   volatile __attribute__((address_space(3))) int* slot =
@@ -610,8 +610,19 @@ __global__ void __launch_bounds__(NWAVE * 64) lstm_i8_flow_kernel(EncFlowArgs f)
 }
 
 // ---------------------------------------------------------------- host launchers
-int launch_lstm_i8_flow(const EncFlowArgs& f, int grid, hipStream_t st) {
+int launch_lstm_i8_flow(const EncFlowArgs& f, int grid, hipStream_t st, bool big) {
+  if (big) {
+    using C = BigTile;
+    static_assert(C::NGT == ENC_FLOW_BIG_NGT && C::BN == ENC_FLOW_BIG_ROWS, "big flow tile");
+    static std::atomic<uint64_t> attr{0};
+    const void* fn = (const void*)lstm_i8_flow_kernel<C::BM / 64, C::BN / 32, C::NBUF>;
+    if (set_smem_attr_once(fn, C::SMEM + 16, attr)) return -1;
+    hipLaunchKernelGGL((lstm_i8_flow_kernel<C::BM / 64, C::BN / 32, C::NBUF>), dim3(grid), dim3(NWAVE * 64),
+                       C::SMEM + 16, st, f);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   using C = FlowTile;
+  static_assert(C::NGT == ENC_FLOW_NGT, "flow tile");
   static std::atomic<uint64_t> attr{0};
   const void* fn = (const void*)lstm_i8_flow_kernel<C::BM / 64, C::BN / 32, C::NBUF>;
   if (set_smem_attr_once(fn, C::SMEM + 16, attr)) return -1;

@@ -82,6 +82,10 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st, int forced = ENC_T
 // publishes its outputs write-through before counting itself done.
 constexpr int ENC_FLOW_NGT = 32;        // gate tiles per layer-step (the 128 x 128 tile)
 constexpr int ENC_FLOW_MAX_TILES = 2;   // batch tiles (n_pad <= 256)
+// Larger batches (development, RNNT_ENC_TILE=flow): the same dataflow launch over the 256 x 256 tile
+// (16 gate tiles per layer-step, 256-row batch tiles), on RNNT_ENC_FLOW_GRID workgroups (default 256)
+constexpr int ENC_FLOW_BIG_NGT = 16;
+constexpr int ENC_FLOW_BIG_ROWS = 256;
 struct EncFlowStep {
   EncStepArgs a;
   int dep_x, dep_h;       // step whose completion the input frame / the recurrent state needs (-1: none)
@@ -94,6 +98,6 @@ struct EncFlowArgs {
   int n_tasks, n_steps;
   unsigned long long timeout; // s_memrealtime ticks (100 MHz) one wait may spin before it aborts the launch
 };
-int launch_lstm_i8_flow(const EncFlowArgs& f, int grid, hipStream_t st);
+int launch_lstm_i8_flow(const EncFlowArgs& f, int grid, hipStream_t st, bool big = false);
 
 }  // namespace rnnt

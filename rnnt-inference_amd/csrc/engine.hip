@@ -692,13 +692,15 @@ struct EncInput {
 // layer-steps as one launch's task list.  Used for small batches (n_pad <= 256) when the engine's
 // tile setting is "flow" (or "auto", see flow_wanted).
 static bool flow_wanted(const rnnt_engine* e, int n_pad) {
-  return e->tile == ENC_TILE_FLOW && n_pad <= ENC_FLOW_MAX_TILES * ENC_ROW_TILE;
+  (void)n_pad;  // any batch: the 128 x 128 task tile up to 256 rows, the 256 x 256 one beyond
+  return e->tile == ENC_TILE_FLOW;
 }
 
 static int flow_alloc(rnnt_engine* e) {
   if (e->flow_dev) return 0;
   const size_t cap = 2 * (size_t)e->opts.max_frames + 3 * (size_t)e->tp_max + 8;
-  const size_t bytes = cap * sizeof(EncFlowStep) + cap * ENC_FLOW_MAX_TILES * sizeof(uint32_t);
+  const size_t bt = std::max<size_t>(ENC_FLOW_MAX_TILES, (size_t)e->np_max / ENC_FLOW_BIG_ROWS);  // blocks per step
+  const size_t bytes = cap * sizeof(EncFlowStep) + cap * bt * sizeof(uint32_t);
   int r = dev_alloc(e, &e->flow_dev, bytes);
   if (!r) r = dev_alloc(e, &e->flow_ctr, cap + 4);
   if (r) return r;
@@ -735,18 +737,21 @@ static int run_flow(rnnt_engine* e, int T, int n_pad, const int32_t* lens, float
   std::vector<int> snbt;
   for (int l = 0; l < 5; ++l) sid[l].assign(l < 2 ? T : Tp, -1);
   int ns = 0, nb = 0;
-  const unsigned NGT = ENC_FLOW_NGT;
+  const bool big = n_pad > ENC_FLOW_MAX_TILES * ENC_ROW_TILE;  // the 256 x 256 task tile
+  const unsigned NGT = big ? ENC_FLOW_BIG_NGT : ENC_FLOW_NGT;
+  const int max_nbt = big ? n_pad / ENC_FLOW_BIG_ROWS : ENC_FLOW_MAX_TILES;
   auto need = [&](int s) { return s < 0 ? 0u : NGT * (unsigned)snbt[s]; };
   struct Job { int l, t; EncStepArgs a; int nbt; };
+  auto btiles = [&](int thr) { const int t = tiles(thr); return big ? (t + 1) / 2 : t; };  // task batch tiles
   const int n_ticks = std::max(T + 1, 2 * Tp + 4);
   for (int tau = 0; tau < n_ticks; ++tau) {
     Job jobs[5];
     int nj = 0;
     // the tick loop's jobs (encode_impl), ordered by K descending like TickBuilder
-    if (tau < T) jobs[nj++] = {0, tau, make_job(e, 0, tau, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, lens, T), tiles(2 * (tau / 2))};
+    if (tau < T) jobs[nj++] = {0, tau, make_job(e, 0, tau, n_pad, e->x0q, ENC_OUT_I8, e->yA, nullptr, lens, T), btiles(2 * (tau / 2))};
     if (tau >= 1 && tau - 1 < T)
       jobs[nj++] = {1, tau - 1, make_job(e, 1, tau - 1, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, lens, T),
-                    tiles(2 * ((tau - 1) / 2))};
+                    btiles(2 * ((tau - 1) / 2))};
     for (int l = 2; l < 5; ++l) {
       const int d = tau - (l + 1);
       if (d >= 0 && (d & 1) == 0 && d / 2 < Tp) {
@@ -754,14 +759,14 @@ static int run_flow(rnnt_engine* e, int T, int n_pad, const int32_t* lens, float
         EncStepArgs a = l == 2   ? make_job(e, 2, tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, lens, T)
                         : l == 3 ? make_job(e, 3, tp, n_pad, e->yB, ENC_OUT_I8, e->yC, nullptr, lens, T)
                                  : make_job(e, 4, tp, n_pad, e->yC, ENC_OUT_FINAL, e->fbf, f_out, lens, T);
-        jobs[nj++] = {l, tp, a, tiles(2 * tp)};
+        jobs[nj++] = {l, tp, a, btiles(2 * tp)};
       }
     }
     std::stable_sort(jobs, jobs + nj, [](const Job& x, const Job& y) { return x.a.I > y.a.I; });
     for (int j = 0; j < nj; ++j) {
       const Job& jb = jobs[j];
       if (jb.nbt <= 0) continue;
-      if (jb.nbt > ENC_FLOW_MAX_TILES || ns >= (int)e->flow_cap) return fail(RNNT_EINVAL, "flow encode: batch too large");
+      if (jb.nbt > max_nbt || ns >= (int)e->flow_cap) return fail(RNNT_EINVAL, "flow encode: batch too large");
       // input frame: layer l-1 at the same frame (layer 2: the odd half of stacked frame t', i.e.
       // feature frame 2t'+1, or 2t' for an odd-T pad; its completion implies 2t''s); recurrent
       // state: layer l at t-1
@@ -787,15 +792,20 @@ static int run_flow(rnnt_engine* e, int T, int n_pad, const int32_t* lens, float
   f.blocks = (const uint32_t*)(e->flow_dev + e->flow_cap * sizeof(EncFlowStep));
   f.ctr = e->flow_ctr;
   f.n_steps = ns;
-  f.n_tasks = nb * ENC_FLOW_NGT;
+  f.n_tasks = nb * (int)NGT;
   f.timeout = 200000000ull;  // 2 s at 100 MHz: a config-3 encode takes a few ms
   HIPCHK(hipMemcpyAsync(e->flow_dev, e->flow_host, (size_t)ns * sizeof(EncFlowStep), hipMemcpyHostToDevice, st));
   HIPCHK(hipMemcpyAsync((void*)f.blocks, blocks, (size_t)nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   HIPCHK(hipEventRecord(e->flow_up_ev, st));
   e->flow_up_pending = true;
   HIPCHK(hipMemsetAsync(e->flow_ctr, 0, ((size_t)ns + 2 + 3) / 4 * 16, st));
-  const int grid = std::min(f.n_tasks, 256);
-  if (launch_lstm_i8_flow(f, grid, st)) return fail(RNNT_EDEVICE, "flow encode launch failed");
+  static const int big_grid = [] {  // development knob: CUs the big-batch flow launch holds
+    const char* v = getenv("RNNT_ENC_FLOW_GRID");
+    const int g = v ? atoi(v) : 256;
+    return g >= 8 && g <= 256 ? g : 256;
+  }();
+  const int grid = std::min(f.n_tasks, big ? big_grid : 256);
+  if (launch_lstm_i8_flow(f, grid, st, big)) return fail(RNNT_EDEVICE, "flow encode launch failed");
   HIPCHK(hipMemcpyAsync(e->flow_abort, e->flow_ctr + ns + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipEventRecord(e->flow_done_ev, st));
   e->flow_check = true;

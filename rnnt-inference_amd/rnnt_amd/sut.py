@@ -253,6 +253,9 @@ class OfflineSUT:
                 ps = PartitionedStream(eng.device, cu_mask_words(k, reserved=False))
                 self._streams[("ps", id(eng))] = ps  # keeps the HIP stream alive
                 self._streams[id(eng)] = ps.stream
+            elif os.environ.get("RNNT_SUT_ENC_PRIORITY", "0") == "1":  # development knob: see _dec_stream_for
+                lo, hi = torch.cuda.Stream.priority_range()
+                self._streams[id(eng)] = torch.cuda.Stream(device=eng.device, priority=min(lo, hi))
             else:
                 self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
         return self._streams[id(eng)]
@@ -280,12 +283,14 @@ class OfflineSUT:
 
     def _dec_stream_for(self, eng):
         """Development knobs: RNNT_SUT_DEC_PRIORITY=1 runs the decode of each engine on a second,
-        high-priority stream; RNNT_SUT_ENC_RESERVE=k (encoder kept off k CU slots per XCD) runs it on a
-        second unrestricted stream.  The engine orders its calls across streams by its state event."""
+        high-priority stream; RNNT_SUT_ENC_RESERVE=k (encoder kept off k CU slots per XCD) or
+        RNNT_SUT_ENC_PRIORITY=1 (the encode stream high-priority) run it on a second normal stream.
+        The engine orders its calls across streams by its state event."""
         import os
         import torch
         prio = os.environ.get("RNNT_SUT_DEC_PRIORITY", "0") == "1"
-        if not prio and int(os.environ.get("RNNT_SUT_ENC_RESERVE", "0")) <= 0:
+        if (not prio and int(os.environ.get("RNNT_SUT_ENC_RESERVE", "0")) <= 0
+                and os.environ.get("RNNT_SUT_ENC_PRIORITY", "0") != "1"):
             return None
         key = ("dec", id(eng))
         if key not in self._streams:
