@@ -456,7 +456,9 @@ def main():
     for e in engines:
         e.set_profiling(False)
     value = query * args.steps / elapsed_max
-    qlens = np.concatenate([qsl.lengths[b[1]] for b in mine])  # this rank's share
+    # this rank's share (a rank may run no batch: a query of fewer batches than ranks, or claims
+    # taken by faster ranks)
+    qlens = np.concatenate([qsl.lengths[b[1]] for b in mine]) if mine else np.zeros(0, np.int64)
     enc_frames = int(sum(encoder_frames(l) for l in qlens))
     enc_ops = float(sum(encoder_ops(int(l)) for l in qlens))  # SURVEY 8d E(T), valid frames
     emitted = int(got[1].sum()) if got is not None else 0  # whole query (rank 0 holds the gathered responses)
