@@ -863,7 +863,14 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
         if (tm[i] > thr) m |= 1ull << i;
     return m;
   };
-  const int n_ticks = flow_wanted(e, n_pad) ? 0 : std::max(T + 1, 2 * Tp + 4);
+  // development: RNNT_L4_LAG = 6 runs post_rnn layer 4 one tick later (2t' + 6), on the ticks
+  // without layer 2, so odd and even ticks carry 6400 / 7424 K-bytes of work instead of 8448 / 5376
+#ifndef RNNT_L4_LAG
+#define RNNT_L4_LAG 5
+#endif
+  constexpr int L4_LAG = RNNT_L4_LAG;
+  static_assert(L4_LAG == 5 || L4_LAG == 6, "layer 4 runs after layer 3 of the same stacked frame");
+  const int n_ticks = flow_wanted(e, n_pad) ? 0 : std::max(T + 1, 2 * Tp + L4_LAG - 1);
   if (!n_ticks && (r = run_flow(e, T, n_pad, lens, f_out, tiles, st))) return r;
   for (int tau = 0; tau < n_ticks; ++tau) {
     TickBuilder tb;
@@ -874,7 +881,7 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
       tb.add(make_job(e, 1, t, n_pad, e->yA, ENC_OUT_STACKED, e->xs, nullptr, lens, T), tiles(2 * (t / 2)), tmask(2 * (t / 2)));
     }
     for (int l = 2; l < 5; ++l) {
-      const int d = tau - (l + 1);  // = 2t'
+      const int d = tau - (l == 4 ? L4_LAG : l + 1);  // = 2t'
       if (d >= 0 && (d & 1) == 0 && d / 2 < Tp) {
         const int tp = d / 2;
         if (l == 2) tb.add(make_job(e, 2, tp, n_pad, e->xs, ENC_OUT_I8, e->yB, nullptr, lens, T), tiles(2 * tp), tmask(2 * tp));
