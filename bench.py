@@ -380,85 +380,15 @@ def responses_dict(ids, lens, toks):
     return out
 
 
-def main():
-    args = parse()
-    rc = launch_ranks(args)
-    if rc is not None:
-        sys.exit(rc)
-    _, local, world = dist.env_rank()
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but the torchrun world has {world} rank(s)")
-    if args.mock:
-        return mock_main(args)
-    dev = 0 if args.share_device else local
-    torch.cuda.set_device(dev)
-    rank, local, world, ggroup = dist.setup(control_backend(args))
-    device = f"cuda:{dev}"
-    pm, _ = weights.build_model()
-    qsl = build_qsl(args.qsl, seed=4, device=device, wav=args.wav)
-    query = args.query * world
-    ids, idx = dist.query_arrays(args.qsl, query)
-    max_b = max([args.batch] + ([int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else []))
-    engines = [Engine(pm, device=dev, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
-    sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
-    if args.sut_warmup:  # OfflineSUT::warmup (torch_sut.cpp:124-138), before any query
-        sut.warmup(iters=args.sut_warmup, batch_size=args.batch, frames=args.sut_warmup_frames)
-    sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None
-
-    qno = [0]
-
-    def step():
-        """One Offline query: sort + batch, this rank's batches through the SUT (claimed from the
-        shared counter, or dealt), every batch's responses streamed to rank 0 as it completes
-        (dist.ResponseStream, tagged with the query number)."""
-        if world > 1 and args.deal == "dynamic":
-            batches = make_batches(qsl, ids, idx, args.batch, sizes)
-            claim = dist.claim_for_query(qno[0], len(batches))
-        else:
-            batches, claim = dist.shard_query(qsl, ids, idx, args.batch, rank, world, sizes), None
-            if args.batch_order:
-                order = [int(v) for v in args.batch_order.split(",")]
-                if sorted(order) != list(range(len(batches))):
-                    raise SystemExit(f"--batch-order must permute 0..{len(batches) - 1}")
-                batches = [batches[i] for i in order]
-        stream = dist.ResponseStream(world, ggroup, tag=qno[0]) if world > 1 else None
-        qno[0] += 1
-        sut.on_batch = stream.push if stream else None
-        sut.issue_batches(batches, claim=claim)
-        local = sut.take_completed()
-        got = stream.finish() if stream else local
-        return sut.ran_batches(batches), got, int(local[1].sum())
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    for e in engines:  # HIP events around every encode / joint_trans / greedy call, on its stream
-        e.set_profiling(True)
-        e.stats(reset=True)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        mine, got, my_emitted = step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed_max = dist.reduce_max(elapsed)
-    sts = [e.stats(reset=True) for e in engines]
-    st = {k: sum(x[k] for x in sts) for k in sts[0]}
-    batch_engine = [e for e in sut.batch_engine if e is not None]  # aligned with `mine` (the batches this rank ran)
-    # isolated pass (untimed): this rank's batches once more on one engine, back to back, so the
-    # encoder's event time is not shared with an overlapping decode
-    iso_sut = OfflineSUT([engines[0]], qsl)
-    iso_sut.issue_batches(mine)
-    iso_sut.take_completed()
-    iso = engines[0].stats(reset=True)
-    for e in engines:
-        e.set_profiling(False)
+def summarize(args, world, query, elapsed_max, st, iso, lengths, mine, got, my_emitted, sizes):
+    """The JSON line of a measured run (everything but the rank-0-only extras): value, roofline (this
+    rank's share of the query: a rank may run no batch at all -- a query of fewer batches than ranks, or
+    claims taken by faster ranks), config.  st / iso: summed rnnt_engine_get_stats of the timed steps /
+    of the isolated pass; lengths: the QSL's lengths; mine: this rank's (ids, qsl indices) batches."""
     value = query * args.steps / elapsed_max
     # this rank's share (a rank may run no batch: a query of fewer batches than ranks, or claims
     # taken by faster ranks)
-    qlens = np.concatenate([qsl.lengths[b[1]] for b in mine]) if mine else np.zeros(0, np.int64)
+    qlens = np.concatenate([lengths[b[1]] for b in mine]) if mine else np.zeros(0, np.int64)
     enc_frames = int(sum(encoder_frames(l) for l in qlens))
     enc_ops = float(sum(encoder_ops(int(l)) for l in qlens))  # SURVEY 8d E(T), valid frames
     emitted = int(got[1].sum()) if got is not None else 0  # whole query (rank 0 holds the gathered responses)
@@ -529,6 +459,88 @@ def main():
         "roofline": roofline,
         "control_plane": dist.backend_name(),
     }
+    return out
+
+
+def main():
+    args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    _, local, world = dist.env_rank()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the torchrun world has {world} rank(s)")
+    if args.mock:
+        return mock_main(args)
+    from rnnt_amd import _lib
+    # a fatal signal names the shared object of every frame (round 5's exit-time fault named none)
+    _lib.check(_lib.lib().rnnt_install_crash_report(), "rnnt_install_crash_report")
+    dev = 0 if args.share_device else local
+    torch.cuda.set_device(dev)
+    rank, local, world, ggroup = dist.setup(control_backend(args))
+    device = f"cuda:{dev}"
+    pm, _ = weights.build_model()
+    qsl = build_qsl(args.qsl, seed=4, device=device, wav=args.wav)
+    query = args.query * world
+    ids, idx = dist.query_arrays(args.qsl, query)
+    max_b = max([args.batch] + ([int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else []))
+    engines = [Engine(pm, device=dev, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
+    sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
+    if args.sut_warmup:  # OfflineSUT::warmup (torch_sut.cpp:124-138), before any query
+        sut.warmup(iters=args.sut_warmup, batch_size=args.batch, frames=args.sut_warmup_frames)
+    sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None
+
+    qno = [0]
+
+    def step():
+        """One Offline query: sort + batch, this rank's batches through the SUT (claimed from the
+        shared counter, or dealt), every batch's responses streamed to rank 0 as it completes
+        (dist.ResponseStream, tagged with the query number)."""
+        if world > 1 and args.deal == "dynamic":
+            batches = make_batches(qsl, ids, idx, args.batch, sizes)
+            claim = dist.claim_for_query(qno[0], len(batches))
+        else:
+            batches, claim = dist.shard_query(qsl, ids, idx, args.batch, rank, world, sizes), None
+            if args.batch_order:
+                order = [int(v) for v in args.batch_order.split(",")]
+                if sorted(order) != list(range(len(batches))):
+                    raise SystemExit(f"--batch-order must permute 0..{len(batches) - 1}")
+                batches = [batches[i] for i in order]
+        stream = dist.ResponseStream(world, ggroup, tag=qno[0]) if world > 1 else None
+        qno[0] += 1
+        sut.on_batch = stream.push if stream else None
+        sut.issue_batches(batches, claim=claim)
+        local = sut.take_completed()
+        got = stream.finish() if stream else local
+        return sut.ran_batches(batches), got, int(local[1].sum())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    for e in engines:  # HIP events around every encode / joint_trans / greedy call, on its stream
+        e.set_profiling(True)
+        e.stats(reset=True)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mine, got, my_emitted = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = dist.reduce_max(elapsed)
+    sts = [e.stats(reset=True) for e in engines]
+    st = {k: sum(x[k] for x in sts) for k in sts[0]}
+    batch_engine = [e for e in sut.batch_engine if e is not None]  # aligned with `mine` (the batches this rank ran)
+    # isolated pass (untimed): this rank's batches once more on one engine, back to back, so the
+    # encoder's event time is not shared with an overlapping decode
+    iso_sut = OfflineSUT([engines[0]], qsl)
+    iso_sut.issue_batches(mine)
+    iso_sut.take_completed()
+    iso = engines[0].stats(reset=True)
+    for e in engines:
+        e.set_profiling(False)
+    out = summarize(args, world, query, elapsed_max, st, iso, qsl.lengths, mine, got, my_emitted, sizes)
     if rank == 0 and got is not None:
         assert len(got[0]) == query and len(np.unique(got[0])) == query, "gathered responses do not cover the query"
         if args.dump_responses:
@@ -550,8 +562,15 @@ def main():
         out["wer_vs_fp32"] = wer_vs_fp32()
     if rank == 0:
         print(json.dumps(out), flush=True)
+    # teardown in a fixed order, before interpreter exit: the SUTs' threads have all joined (issue_batches),
+    # then every engine is destroyed and the QSL freed while torch's HIP runtime is fully up, the device
+    # drained, and the process group closed; nothing of ours is left to a __del__ or a static destructor
+    del sut, iso_sut
     for e in engines:
         e.close()
+    del engines, qsl
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     if world > 1:
         import torch.distributed as tdist
         tdist.destroy_process_group()

@@ -70,6 +70,11 @@ typedef struct {
 int rnnt_abi_version(void);
 const char* rnnt_last_error(void);
 
+/* Diagnostics, no reference counterpart: on SIGSEGV / SIGBUS / SIGFPE / SIGILL / SIGABRT print each
+ * stack frame as shared object + offset to stderr, then pass the signal to the previously installed
+ * handler.  bench.py installs it first thing. */
+int rnnt_install_crash_report(void);
+
 /* A HIP stream whose kernels run only on the CUs set in cu_mask (mask_words 32-bit words;
  * bit b = CU slot b/8 of XCD b%8 on MI355X; every XCD needs at least one bit), or a plain
  * non-blocking stream when cu_mask is NULL.  bench.py / the SUT keep the encoder off a few CUs
@@ -218,13 +223,16 @@ int rnnt_engine_set_profiling(rnnt_engine* e, int on);
  * (64 x 128, 4-deep) -- results are identical (int32 accumulation); for tests and sweeps.  "flow":
  * whole-call encodes of batches with n_pad <= 256 run as one persistent dataflow launch (opt-in:
  * measured slower than the ticks on config 3); "ticks" = "auto".  The
- * environment variable RNNT_ENC_TILE sets an engine's initial value at create. */
+ * environment variable RNNT_ENC_TILE sets an engine's initial value at create (development builds only). */
 int rnnt_engine_set_tile(rnnt_engine* e, const char* tile);
 /* Greedy decode tail: once at most `rows` rows of a decode call are still live, one persistent
  * launch runs every remaining lock-step step (weight slices kept in registers, phases handed off
  * through device counters; results identical) instead of four launches per step.  0 = off,
- * 1..512; the environment variable RNNT_DEC_PERSIST_ROWS sets an engine's initial value.  No
- * reference counterpart (the reference's loop is rnnt_model.hpp:92-124). */
+ * 1..512; in development builds the environment variable RNNT_DEC_PERSIST_ROWS sets an engine's
+ * initial value.  The launch needs its 48 + (joint row groups, <= 32) workgroups resident at once:
+ * beside other kernels a wait can time out, and rnnt_engine_decode then fails (RNNT_EDEVICE,
+ * "persistent decode timed out").  No reference counterpart (the reference's loop is
+ * rnnt_model.hpp:92-124). */
 int rnnt_engine_set_decode_persist(rnnt_engine* e, int rows);
 int rnnt_engine_get_stats(rnnt_engine* e, rnnt_stats* out, int reset);
 

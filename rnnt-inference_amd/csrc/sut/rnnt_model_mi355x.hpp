@@ -1,185 +1,523 @@
-// rnnt_model_mi355x.hpp -- the body of the reference's TorchModel (csrc/rnnt_model.hpp:39-137) on the
-// MI355X engine, as a maintainer drops it into the C++ LoadGen SUT.
+// rnnt_model_mi355x.hpp -- rnnt::models::TorchModel (the reference's csrc/rnnt_model.hpp:39-137) on the
+// MI355X engine.  A maintainer swaps the include of rnnt_model.hpp for this file; the reference's
+// State / PipelineState (metadata.hpp, metadata.cpp), OfflineSUT / ServerSUT (torch_sut.cpp) and QSL stay
+// as they are.
 //
-// Compiled and run: csrc/sut/sut_harness.cpp drives it exactly as OfflineSUT::thInstance does
-// (state.update -> model.encode -> model.decode -> QuerySamplesComplete, torch_sut.cpp:185-236) and
-// tests/test_sut_harness_gpu.py checks the responses against the CPU restatement.
+// The interface is the reference's: TorchModel(model_file); forward / encode / decode(int which, S& state)
+// for S = State (Offline, any split_len) or PipelineState (Server).  What it reads from the state:
+//   State          f_, f_lens_ / infer_lens_, split_len_ and next() (metadata.cpp:37-86), actual_batch_size_,
+//                  batch_size_, max_res_len_; writes f_lens_ = ceil(infer_lens_ / 2) (rnnt_model.hpp:88-89),
+//                  res_ and res_idx_ (the result contract QuerySamplesComplete reads, torch_sut.cpp:221-236).
+//   PipelineState  additionally finish_idx_ / dequeue_size_ at entry (the slots update() restarted,
+//                  metadata.cpp:122-143) and padded_fea_len_; next() gathers each slot's chunks from F_.
+// The LSTM / prediction state tensors of the State (pre_hx_, pre_cx_, ..., pre_cg_) are not used: that
+// state lives in the engine (int8 h, fp16 c, bf16 / fp32 prediction state in HBM).
 //
-// What stays the reference's: the State contract the SUT reads after decode (metadata.hpp:37-81,
-// metadata.cpp:37-74) -- res_ host int32 [batch][max_res_len_] filled with SOS (-1) past each row's
-// tokens, res_idx_ host int32 [batch] = tokens - 1 (-1 for none), actual_batch_size_ -- and the call
-// shapes encode(which, state) / decode(which, state).  What changes: `which` is a GPU index instead
-// of a socket (torch_sut.cpp:145), the model file is the engine file tools/export_model.py writes
-// (instead of the TorchScript module, rnnt_model.hpp:41-54), and the encoder / decoder state lives
-// in the engine, so State keeps only the batch, its lengths and the results.
+// Threading (the reference runs INTER = 28 Offline instances, which = index & 1, torch_sut.cpp:115-145):
+// every call is re-entrant.  `which` names a CPU socket as in the reference; it selects the half of the
+// node's GPUs attached to that socket (all GPUs when there are fewer than two).  encode() leases an engine
+// -- its HIP stream, pinned staging and device buffers -- on the least-loaded GPU of that group and
+// decode() returns it, so any number of threads may share a GPU: at most engines_per_gpu batches are in
+// flight per GPU (the rest wait), and the encoders of one GPU take turns in arrival order, so each batch's
+// latency-bound greedy decode runs beside the next batch's encoder (the bench's schedule).
+// A PipelineState keeps its engine for its lifetime (its slots' LSTM and greedy state persist in the
+// engine between calls, rnnt_engine_encode_stream / decode_stream).
+//
+// Chunking: the engine runs each slot's whole span of a call in one wavefront encode.  That equals the
+// reference's chunk-by-chunk transcription (h / c carried between chunks, rnnt_model.hpp:64-78) when the
+// chunks pair frames the same way as the whole utterance, i.e. for even split_len (pinned by the
+// split_len = 2 reference fixture, tests/test_oracle_golden.py).  An odd split_len > 0 is rejected.
 #pragma once
 #include <ATen/ATen.h>
+#include <ATen/Parallel.h>
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../../include/rnnt_mi355x.h"
 
 namespace rnnt {
+namespace models {
+namespace mi355x {
 
-enum Params {  // metadata.hpp:19-34
-  STACK_TIME_FACTOR = 2,
-  SOS = -1,
-  BLANK = 28,
-  MAX_SYMBOLS_PER_STEP = 30,
-  MAX_FEA_LEN = 500,
-  PADDED_INPUT_SIZE = 256
-};
+constexpr int kFeat = 240;         // TRANS_INPUT_SIZE (metadata.hpp:22)
+constexpr int kMaxFeaLen = 500;    // MAX_FEA_LEN (metadata.hpp:32)
+constexpr int kMaxSymbols = 30;    // MAX_SYMBOLS_PER_STEP (metadata.hpp:30)
+constexpr int kRowTile = 256;      // the engine's batch tile: n_pad is a multiple of it
+constexpr int32_t kSos = -1;
 
-inline void check(int rc, const char* what) {  // the reference's TORCH_CHECK convention: errors throw
-  if (rc < 0) throw std::runtime_error(std::string(what) + ": " + rnnt_last_error());
+inline void check(int rc, const char* what) {  // return codes -> exceptions, as TORCH_CHECK would throw
+  if (rc < 0) throw std::runtime_error(std::string("TorchModel: ") + what + ": " + rnnt_last_error());
 }
 inline void hcheck(hipError_t rc, const char* what) {
-  if (rc != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(rc));
+  if (rc != hipSuccess) throw std::runtime_error(std::string("TorchModel: ") + what + ": " + hipGetErrorString(rc));
 }
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
-// State (metadata.hpp:37-81), Offline form: the members the SUT and the model driver touch.
-class State {
- public:
-  State() = default;
-  explicit State(int32_t batch_size, int32_t split_len = -1) { init(batch_size, split_len); }
-  void init(int32_t batch_size, int32_t split_len = -1) {  // metadata.cpp:5-35 (results part)
-    batch_size_ = batch_size;
-    split_len_ = split_len;
-    res_ = at::empty({batch_size_, max_res_len_}, at::kInt);
-    res_idx_ = at::empty({batch_size_}, at::kInt);
-  }
-  // metadata.cpp:37-74: x [T, N_pad, C] fp32 features (AssembleSamples layout), x_lens [N_pad]
-  void update(at::Tensor x, at::Tensor x_lens, int32_t split_len = -1, int32_t actual_batch_size = -1) {
-    actual_batch_size_ = actual_batch_size < 0 ? (int32_t)x_lens.size(0) : actual_batch_size;
-    if (x_lens.size(0) != batch_size_) init((int32_t)x_lens.size(0), split_len);
-    split_len_ = split_len;  // chunking is numerically invariant (decoder.py:80-91): the engine walks all T
-    res_.fill_(SOS);
-    res_idx_.fill_(-1);
-    f_ = x;
-    f_lens_ = x_lens.to(at::kInt).contiguous();
-    infer_lens_ = f_lens_;
-    finish_size_ = batch_size_;
-  }
-  int32_t finish_size_ = 0;
-  int32_t actual_batch_size_ = 0;
-  int32_t batch_size_ = 0;
-  int32_t split_len_ = -1;
-  int32_t padded_fea_len_ = MAX_FEA_LEN;
-  int32_t max_res_len_ = MAX_FEA_LEN / 2 * MAX_SYMBOLS_PER_STEP;  // metadata.hpp:58-59
-  at::Tensor f_, f_lens_, infer_lens_;
-  at::Tensor res_, res_idx_;
+// S is a Server PipelineState when it has the slot-refill members (metadata.hpp:84-114)
+template <class S, class = void>
+struct is_pipeline : std::false_type {};
+template <class S>
+struct is_pipeline<S, std::void_t<decltype(std::declval<S&>().F_), decltype(std::declval<S&>().dequeue_size_)>>
+    : std::true_type {};
+
+struct Options {
+  std::vector<int> gpus;     // devices to use (default: every visible GPU; env RNNT_GPUS="0,1,...")
+  int engines_per_gpu = 4;   // Offline batches in flight per GPU (env RNNT_ENGINES_PER_GPU)
+  int sockets = 2;           // `which` values the SUT passes (index & 1, torch_sut.cpp:145)
+  bool encode_turns = true;  // encoders of one GPU take turns (env RNNT_ENCODE_TURNS=0 lets them overlap)
 };
 
-namespace models {
+inline Options options_from_env() {
+  Options o;
+  if (const char* g = std::getenv("RNNT_GPUS")) {
+    for (const char* p = g; *p;) {
+      char* end = nullptr;
+      const long d = std::strtol(p, &end, 10);
+      if (end == p) throw std::runtime_error("TorchModel: bad RNNT_GPUS list");
+      o.gpus.push_back((int)d);
+      p = *end == ',' ? end + 1 : end;
+    }
+  } else {
+    int n = 0;
+    hcheck(hipGetDeviceCount(&n), "hipGetDeviceCount");
+    for (int d = 0; d < n; ++d) o.gpus.push_back(d);
+  }
+  if (o.gpus.empty()) throw std::runtime_error("TorchModel: no GPU");
+  if (const char* k = std::getenv("RNNT_ENGINES_PER_GPU")) o.engines_per_gpu = std::max(1, std::atoi(k));
+  if (const char* t = std::getenv("RNNT_ENCODE_TURNS")) o.encode_turns = std::atoi(t) != 0;
+  return o;
+}
+
+// One batch in flight: an engine, its stream and the buffers one call stages through.
+struct Slot {
+  int device = 0;
+  rnnt_engine* e = nullptr;
+  hipStream_t st = nullptr;
+  int rows = 0, max_frames = 0, max_res = 0;  // engine capacity (rows a multiple of kRowTile)
+  bool sticky = false;                        // a PipelineState's engine (slot state lives in it)
+  char* host = nullptr;                       // pinned staging: [offsets i64][lens i32][reset i32][features]
+  char* dev = nullptr;                        // its device mirror
+  size_t cap = 0;
+  int32_t* d_res = nullptr;   // [rows][max_res]
+  int32_t* d_len = nullptr;   // [rows]
+  int32_t* h_len = nullptr;   // pinned [rows]
+  int32_t* d_reset = nullptr; // points into dev (stream calls)
+  int n = 0;                  // rows of the last encode
+
+  void grow(size_t bytes) {
+    if (bytes <= cap) return;
+    const size_t c = (size_t)round_up((int64_t)std::max(bytes, cap + cap / 2), 1 << 20);
+    if (host) hcheck(hipHostFree(host), "hipHostFree");
+    if (dev) hcheck(hipFree(dev), "hipFree");
+    host = dev = nullptr;
+    cap = 0;
+    hcheck(hipHostMalloc((void**)&host, c, hipHostMallocDefault), "hipHostMalloc staging");
+    hcheck(hipMalloc((void**)&dev, c), "hipMalloc staging");
+    cap = c;
+  }
+  ~Slot() {  // torn down by ~TorchModel, while the HIP runtime is up
+    if (st) (void)hipStreamSynchronize(st);
+    if (host) (void)hipHostFree(host);
+    if (h_len) (void)hipHostFree(h_len);
+    for (void* p : {(void*)dev, (void*)d_res, (void*)d_len})
+      if (p) (void)hipFree(p);
+    if (st) (void)hipStreamDestroy(st);
+    if (e) rnnt_engine_destroy(e);
+  }
+};
+
+// One call's input: each slot's frames of this call, packed back to back (the engine's ragged store).
+struct Chunk {
+  at::Tensor f;     // fp32 [t][rows][C >= 240] (C++ AssembleSamples layout, or one next() chunk)
+  at::Tensor lens;  // int32 [rows]: valid frames of each row in this chunk
+};
+
+// Host-side time of the calls, summed over threads (seconds): what the SUT thread spends packing the batch
+// into pinned memory, copying it to the device, waiting for its GPU's encoder turn, in the encode, and in
+// the decode (greedy loop + result copy).
+struct CallStats {
+  double pack = 0, copy = 0, turn_wait = 0, encode = 0, decode = 0;
+  int64_t calls = 0, frames = 0;
+};
+
+}  // namespace mi355x
 
 class TorchModel {
  public:
-  // model_file: the engine file (tools/export_model.py --engine-file, rnnt_amd.weights.save_engine_file),
-  // one engine per GPU (rnnt_model.hpp:41-47 kept one TorchScript clone per socket)
-  TorchModel(const std::string& model_file, int n_gpus = 1, int max_batch = 4096) {
-    rnnt_opts opts{max_batch, MAX_FEA_LEN, MAX_FEA_LEN / 2 * MAX_SYMBOLS_PER_STEP};
-    gpus_.resize(n_gpus);
-    for (int g = 0; g < n_gpus; ++g) {
-      Gpu& d = gpus_[g];
-      d.max_batch = max_batch;
-      check(rnnt_engine_create_from_file(model_file.c_str(), g, &opts, &d.e), "rnnt_engine_create_from_file");
-      hcheck(hipSetDevice(g), "hipSetDevice");
-      hcheck(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking), "hipStreamCreate");
-      const size_t rows = (size_t)round_up(max_batch, 256);
-      hcheck(hipMalloc(&d.x, (size_t)MAX_FEA_LEN * rows * PADDED_INPUT_SIZE * sizeof(float)), "hipMalloc x");
-      hcheck(hipMalloc(&d.lens, rows * sizeof(int32_t)), "hipMalloc lens");
-      hcheck(hipMalloc(&d.res, rows * (size_t)opts.max_res * sizeof(int32_t)), "hipMalloc res");
-      hcheck(hipMalloc(&d.res_len, rows * sizeof(int32_t)), "hipMalloc res_len");
-    }
+  using Options = mi355x::Options;
+
+  // rnnt_model.hpp:41-47.  model_file: the engine file (tools/export_model.py --engine-file) in place of the
+  // TorchScript model; engines are created on first use, sized to the batches the SUT sends.
+  explicit TorchModel(const std::string& model_file) : TorchModel(model_file, mi355x::options_from_env()) {}
+  TorchModel(const std::string& model_file, Options opts) : file_(model_file), opts_(std::move(opts)) {
+    for (int d : opts_.gpus) gpus_.emplace_back(new Gpu{d});
   }
   ~TorchModel() {
-    for (Gpu& d : gpus_) {
-      if (d.stream) (void)hipStreamSynchronize(d.stream);
-      for (void* p : {(void*)d.x, (void*)d.lens, (void*)d.res, (void*)d.res_len})
-        if (p) (void)hipFree(p);
-      if (d.stream) (void)hipStreamDestroy(d.stream);
-      rnnt_engine_destroy(d.e);
-    }
+    std::lock_guard<std::mutex> l(mu_);
+    for (auto& g : gpus_) g->slots.clear();
   }
   TorchModel(const TorchModel&) = delete;
   TorchModel& operator=(const TorchModel&) = delete;
 
-  template <class T>
-  void forward(int which, T& state) {  // rnnt_model.hpp:56-60
+  template <class S>
+  void forward(int which, S& state) {  // rnnt_model.hpp:56-60
     encode(which, state);
     decode(which, state);
   }
 
-  // rnnt_model.hpp:62-90: the whole transcription; state.f_lens_ becomes ceil(infer_lens / 2)
-  template <class T>
-  void encode(int which, T& state) {
-    Gpu& d = gpus_.at(which);
-    const at::Tensor x = state.f_.to(at::kFloat).contiguous();
-    const int64_t Tn = x.size(0), n_rows = x.size(1), C = x.size(2);
-    const int n = state.actual_batch_size_;
-    if (Tn > MAX_FEA_LEN || n_rows > d.max_batch || C > PADDED_INPUT_SIZE || n > n_rows)
-      throw std::runtime_error("TorchModel::encode: batch exceeds the engine (T <= 500, N <= max_batch, C <= 256)");
-    const int n_pad = (int)round_up(std::max<int64_t>(n_rows, 1), 256);  // the engine's batch tile
-    hcheck(hipSetDevice(which), "hipSetDevice");
-    // AssembleSamples' [T][N_pad][C] host batch -> the engine's [T][n_pad][256] device input: zero the
-    // whole input (pad rows and channels), then each frame's rows as one 2-D copy
-    hcheck(hipMemsetAsync(d.x, 0, (size_t)Tn * n_pad * PADDED_INPUT_SIZE * sizeof(float), d.stream), "memset x");
-    for (int64_t t = 0; t < Tn; ++t)
-      hcheck(hipMemcpy2DAsync(d.x + (size_t)t * n_pad * PADDED_INPUT_SIZE, PADDED_INPUT_SIZE * sizeof(float),
-                              x.data_ptr<float>() + (size_t)t * n_rows * C, C * sizeof(float), C * sizeof(float),
-                              (size_t)n_rows, hipMemcpyHostToDevice, d.stream),
-             "copy x");
-    std::vector<int32_t> lens(n_pad, 0);
-    const at::Tensor il = state.infer_lens_.to(at::kInt).contiguous();
-    std::memcpy(lens.data(), il.data_ptr<int32_t>(), sizeof(int32_t) * std::min<int64_t>(il.numel(), n_rows));
-    hcheck(hipMemcpyAsync(d.lens, lens.data(), sizeof(int32_t) * n_pad, hipMemcpyHostToDevice, d.stream), "copy lens");
-    hcheck(hipStreamSynchronize(d.stream), "sync");  // `lens` is a host temporary
-    check(rnnt_engine_encode(d.e, d.x, d.lens, lens.data(), (int)Tn, n, n_pad, nullptr, d.stream), "rnnt_engine_encode");
-    state.f_lens_ = ((state.infer_lens_ + 1) / STACK_TIME_FACTOR).to(at::kInt);  // ceil(len / 2)
+  // rnnt_model.hpp:62-90.  The batch's features (the whole f_, or every chunk next() yields) go to the
+  // engine in one staged copy and one wavefront encode; f_lens_ = ceil(infer_lens_ / 2).
+  template <class S>
+  void encode(int which, S& state) {
+    constexpr bool pipe = mi355x::is_pipeline<S>::value;
+    if (state.split_len_ > 0 && (state.split_len_ & 1))
+      throw std::runtime_error("TorchModel::encode: odd split_len pairs StackTime frames across chunks; use an even one");
+    // the slots update() restarted (its masked_fill_ set, metadata.cpp:122-143): read before next() moves them
+    std::vector<int32_t> reset;
+    if constexpr (pipe) {
+      const at::Tensor fi = state.finish_idx_.to(at::kInt).contiguous();
+      reset.assign(fi.data_ptr<int32_t>(), fi.data_ptr<int32_t>() + fi.numel());
+      if (state.dequeue_size_ == 0) std::fill(reset.begin(), reset.end(), 0);
+    }
+    std::vector<mi355x::Chunk> chunks;
+    if (state.split_len_ > 0) {
+      while (state.next()) chunks.push_back({state.f_, state.f_lens_});
+      if (chunks.empty()) throw std::runtime_error("TorchModel::encode: the state has no chunk to encode");
+    } else {
+      chunks.push_back({state.f_, state.infer_lens_});
+    }
+    const int rows = (int)state.batch_size_;
+    const int n = pipe ? rows : (state.actual_batch_size_ > 0 ? std::min<int>(state.actual_batch_size_, rows) : rows);
+    const int max_frames = pipe ? std::max<int>(state.padded_fea_len_, mi355x::kMaxFeaLen) : mi355x::kMaxFeaLen;
+    Lease ls = lease(which, &state, pipe, rows, max_frames, (int)state.max_res_len_);
+    try {
+      run_encode(ls, chunks, n, rows, pipe ? reset.data() : nullptr);
+    } catch (...) {
+      release(&state, /*failed=*/true);
+      throw;
+    }
+    state.f_lens_ = (state.infer_lens_ + 1).div(2, "floor").to(at::kInt);  // ceil(infer_lens / STACK_TIME_FACTOR)
   }
 
-  // rnnt_model.hpp:92-124: the greedy loop; results in the State contract (res_ SOS-filled, res_idx_)
-  template <class T>
-  void decode(int which, T& state) {
-    Gpu& d = gpus_.at(which);
-    const int n = state.actual_batch_size_;
-    const int max_res = state.max_res_len_;
-    hcheck(hipSetDevice(which), "hipSetDevice");
-    check(rnnt_engine_decode(d.e, d.res, d.res_len, max_res, d.stream), "rnnt_engine_decode");
-    std::vector<int32_t> len(n);
-    hcheck(hipMemcpyAsync(len.data(), d.res_len, sizeof(int32_t) * n, hipMemcpyDeviceToHost, d.stream), "copy res_len");
-    hcheck(hipStreamSynchronize(d.stream), "sync");
-    int32_t widest = 0;
-    int32_t* idx = state.res_idx_.template data_ptr<int32_t>();
-    for (int i = 0; i < n; ++i) {
-      idx[i] = len[i] - 1;  // metadata.cpp:59-60 / torch_sut.cpp:224: response size = (res_idx_ + 1) * 4
-      widest = std::max(widest, len[i]);
+  // rnnt_model.hpp:92-124: the greedy loop; res_ / res_idx_ as the reference leaves them (res_idx_ =
+  // tokens - 1; res_ keeps update()'s SOS fill past each row's tokens).
+  template <class S>
+  void decode(int which, S& state) {
+    (void)which;
+    constexpr bool pipe = mi355x::is_pipeline<S>::value;
+    Lease ls = find(&state);
+    mi355x::Slot& s = *ls.slot;
+    const auto t0 = Clock::now();
+    try {
+      hcheck(hipSetDevice(s.device), "hipSetDevice");
+      const int n = s.n;
+      if (pipe)
+        mi355x::check(rnnt_engine_decode_stream(s.e, s.d_res, s.d_len, s.max_res, s.d_reset, s.st), "rnnt_engine_decode_stream");
+      else
+        mi355x::check(rnnt_engine_decode(s.e, s.d_res, s.d_len, s.max_res, s.st), "rnnt_engine_decode");
+      hcheck(hipMemcpyAsync(s.h_len, s.d_len, sizeof(int32_t) * n, hipMemcpyDeviceToHost, s.st), "copy res_len");
+      hcheck(hipStreamSynchronize(s.st), "sync");
+      at::Tensor& res = state.res_;
+      at::Tensor& res_idx = state.res_idx_;
+      if (!res.is_contiguous() || res.scalar_type() != at::kInt || res.size(0) < n || res.size(1) > s.max_res ||
+          res_idx.scalar_type() != at::kInt || res_idx.numel() < n)
+        throw std::runtime_error("TorchModel::decode: res_ / res_idx_ are not the State's int32 [batch][max_res_len]");
+      int32_t widest = 0;
+      int32_t* idx = res_idx.data_ptr<int32_t>();
+      for (int i = 0; i < n; ++i) {
+        const int32_t len = std::min<int32_t>(s.h_len[i], (int32_t)res.size(1));
+        idx[i] = len - 1;  // metadata.cpp:59-60; QuerySamplesComplete sends (res_idx_ + 1) * 4 bytes
+        widest = std::max(widest, len);
+      }
+      if (widest > 0)  // only the written columns travel
+        hcheck(hipMemcpy2DAsync(res.data_ptr<int32_t>(), (size_t)res.size(1) * sizeof(int32_t), s.d_res,
+                                (size_t)s.max_res * sizeof(int32_t), (size_t)widest * sizeof(int32_t), (size_t)n,
+                                hipMemcpyDeviceToHost, s.st),
+               "copy res");
+      hcheck(hipStreamSynchronize(s.st), "sync");
+    } catch (...) {
+      release(&state, true);
+      throw;
     }
-    if (widest > 0)  // only the written columns travel; the rest of res_ keeps update()'s SOS fill
-      hcheck(hipMemcpy2DAsync(state.res_.template data_ptr<int32_t>(), (size_t)state.res_.size(1) * sizeof(int32_t),
-                              d.res, (size_t)max_res * sizeof(int32_t), (size_t)widest * sizeof(int32_t), n,
-                              hipMemcpyDeviceToHost, d.stream),
-             "copy res");
-    hcheck(hipStreamSynchronize(d.stream), "sync");
+    release(&state, false);
+    std::lock_guard<std::mutex> l(stats_mu_);
+    stats_.decode += secs(t0, Clock::now());
+  }
+
+  mi355x::CallStats stats(bool reset = false) {
+    std::lock_guard<std::mutex> l(stats_mu_);
+    const mi355x::CallStats s = stats_;
+    if (reset) stats_ = {};
+    return s;
+  }
+
+  // engines created so far per GPU (for tests and logs)
+  std::vector<int> engines_per_gpu() const {
+    std::lock_guard<std::mutex> l(mu_);
+    std::vector<int> v;
+    for (auto& g : gpus_) v.push_back((int)g->slots.size());
+    return v;
   }
 
  private:
-  static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
   struct Gpu {
-    rnnt_engine* e = nullptr;
-    hipStream_t stream = nullptr;
-    int max_batch = 0;
-    float* x = nullptr;
-    int32_t* lens = nullptr;
-    int32_t* res = nullptr;
-    int32_t* res_len = nullptr;
+    int device;
+    std::vector<std::unique_ptr<mi355x::Slot>> slots;  // owned
+    std::vector<mi355x::Slot*> idle;
+    int transient = 0;  // Offline leases out
+    int active = 0;     // every lease out (+ reservations)
+    std::mutex turn_mu;  // encoders take turns: a FIFO ticket lock
+    std::condition_variable turn_cv;
+    uint64_t next_ticket = 0, serving = 0;
   };
-  std::vector<Gpu> gpus_;
+  struct Lease {
+    Gpu* gpu = nullptr;
+    mi355x::Slot* slot = nullptr;
+  };
+
+  std::vector<int> group(int which) const {
+    const int n = (int)gpus_.size(), k = std::max(1, opts_.sockets);
+    std::vector<int> g;
+    if (n >= k) {
+      const int w = ((which % k) + k) % k;
+      for (int i = w * n / k; i < (w + 1) * n / k; ++i) g.push_back(i);
+    }
+    if (g.empty())
+      for (int i = 0; i < n; ++i) g.push_back(i);
+    return g;
+  }
+
+  // An engine for `key`'s batch: the one it already holds (re-encode, or a PipelineState's own), an idle
+  // one on the least-loaded GPU of the socket's group that fits, or a new one.
+  Lease lease(int which, const void* key, bool sticky, int rows, int max_frames, int max_res) {
+    const int need_rows = (int)mi355x::round_up(std::max(rows, 1), mi355x::kRowTile);
+    std::unique_lock<std::mutex> l(mu_);
+    auto it = leases_.find(key);
+    if (it != leases_.end()) {
+      mi355x::Slot* s = it->second.slot;
+      if (s->rows < need_rows || s->max_frames < max_frames || s->max_res < max_res)
+        throw std::runtime_error("TorchModel::encode: the state's batch outgrew the engine it holds");
+      return it->second;
+    }
+    const std::vector<int> grp = group(which);
+    Gpu* g = nullptr;
+    lease_cv_.wait(l, [&] {
+      g = nullptr;
+      for (int i : grp) {
+        Gpu* c = gpus_[i].get();
+        if (!sticky && c->transient >= opts_.engines_per_gpu) continue;
+        if (!g || c->active < g->active) g = c;
+      }
+      return g != nullptr;
+    });
+    mi355x::Slot* s = nullptr;
+    for (size_t i = 0; i < g->idle.size(); ++i) {
+      mi355x::Slot* c = g->idle[i];
+      if (c->rows >= need_rows && c->max_frames >= max_frames && c->max_res >= max_res) {
+        s = c;
+        g->idle.erase(g->idle.begin() + (long)i);
+        break;
+      }
+    }
+    if (!sticky) g->transient++;
+    g->active++;
+    if (!s) {  // create outside the lock (reads the engine file, packs the weights)
+      l.unlock();
+      std::unique_ptr<mi355x::Slot> ns;
+      try {
+        ns = make_slot(g->device, need_rows, max_frames, max_res);
+      } catch (...) {
+        l.lock();
+        if (!sticky) g->transient--;
+        g->active--;
+        lease_cv_.notify_all();
+        throw;
+      }
+      l.lock();
+      s = ns.get();
+      g->slots.push_back(std::move(ns));
+    }
+    s->sticky = sticky;
+    Lease ls{g, s};
+    leases_[key] = ls;
+    return ls;
+  }
+
+  Lease find(const void* key) {
+    std::lock_guard<std::mutex> l(mu_);
+    auto it = leases_.find(key);
+    if (it == leases_.end()) throw std::runtime_error("TorchModel::decode: no encode of this state to decode");
+    return it->second;
+  }
+
+  // back to the GPU's idle list after decode (a PipelineState keeps its engine unless a call failed)
+  void release(const void* key, bool failed) {
+    std::lock_guard<std::mutex> l(mu_);
+    auto it = leases_.find(key);
+    if (it == leases_.end()) return;
+    Lease ls = it->second;
+    if (ls.slot->sticky && !failed) return;
+    leases_.erase(it);
+    if (!ls.slot->sticky) ls.gpu->transient--;
+    ls.gpu->active--;
+    if (failed) {  // the engine's state is unknown: drop it
+      auto& v = ls.gpu->slots;
+      v.erase(std::remove_if(v.begin(), v.end(), [&](const std::unique_ptr<mi355x::Slot>& p) { return p.get() == ls.slot; }),
+              v.end());
+    } else {
+      ls.gpu->idle.push_back(ls.slot);
+    }
+    lease_cv_.notify_all();
+  }
+
+  std::unique_ptr<mi355x::Slot> make_slot(int device, int rows, int max_frames, int max_res) {
+    auto s = std::make_unique<mi355x::Slot>();
+    s->device = device;
+    s->rows = rows;
+    s->max_frames = max_frames;
+    s->max_res = max_res;
+    rnnt_opts o{rows, max_frames, max_res};
+    mi355x::check(rnnt_engine_create_from_file(file_.c_str(), device, &o, &s->e), "rnnt_engine_create_from_file");
+    hcheck(hipSetDevice(device), "hipSetDevice");
+    hcheck(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking), "hipStreamCreate");
+    hcheck(hipMalloc((void**)&s->d_res, (size_t)rows * max_res * sizeof(int32_t)), "hipMalloc res");
+    hcheck(hipMalloc((void**)&s->d_len, (size_t)rows * sizeof(int32_t)), "hipMalloc res_len");
+    hcheck(hipHostMalloc((void**)&s->h_len, (size_t)rows * sizeof(int32_t), hipHostMallocDefault), "hipHostMalloc res_len");
+    return s;
+  }
+
+  static void hcheck(hipError_t rc, const char* what) { mi355x::hcheck(rc, what); }
+  using Clock = std::chrono::steady_clock;
+  static double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+  // Packs every row's frames of this call into the slot's pinned staging area (row i's frames back to
+  // back from offsets[i], only the 240 real channels: AssembleSamples leaves channels 240..255 zero and
+  // the engine's layer-0 weights there are zero), one copy to the device, then the encode -- after the
+  // GPU's earlier encoders (turns in arrival order).
+  void run_encode(const Lease& ls, const std::vector<mi355x::Chunk>& chunks, int n, int rows, const int32_t* reset) {
+    mi355x::Slot& s = *ls.slot;
+    std::vector<at::Tensor> f(chunks.size()), cl(chunks.size());
+    for (size_t c = 0; c < chunks.size(); ++c) {
+      f[c] = chunks[c].f.to(at::kCPU, at::kFloat).contiguous();
+      cl[c] = chunks[c].lens.to(at::kCPU, at::kInt).contiguous();
+      if (f[c].dim() != 3 || f[c].size(1) < rows || f[c].size(2) < mi355x::kFeat || cl[c].numel() < rows)
+        throw std::runtime_error("TorchModel::encode: features are not [T][batch][C >= 240] with a length per row");
+    }
+    const int n_pad = (int)mi355x::round_up(std::max(n, 1), mi355x::kRowTile);
+    std::vector<int64_t> off(n_pad, 0);
+    std::vector<int32_t> len(n_pad, 0);
+    int64_t total = 0;
+    int T = 1;
+    for (int i = 0; i < n; ++i) {
+      int64_t li = 0;
+      for (size_t c = 0; c < chunks.size(); ++c) {
+        const int32_t v = cl[c].data_ptr<int32_t>()[i];
+        if (v < 0 || v > f[c].size(0)) throw std::runtime_error("TorchModel::encode: a length exceeds its frames");
+        li += v;
+      }
+      off[i] = total;
+      len[i] = (int32_t)li;
+      total += li;
+      T = std::max<int>(T, (int)li);
+    }
+    if (T > s.max_frames) throw std::runtime_error("TorchModel::encode: more frames than the engine holds");
+    const size_t o_off = 0, o_len = o_off + sizeof(int64_t) * n_pad, o_rst = o_len + sizeof(int32_t) * n_pad,
+                 o_feat = (size_t)mi355x::round_up((int64_t)(o_rst + sizeof(int32_t) * n_pad), 256);
+    const size_t bytes = o_feat + (size_t)total * mi355x::kFeat * sizeof(float);
+    hcheck(hipSetDevice(s.device), "hipSetDevice");
+    hcheck(hipStreamSynchronize(s.st), "sync");  // the staging area's previous copy has landed
+    s.grow(bytes);
+    std::memcpy(s.host + o_off, off.data(), sizeof(int64_t) * n_pad);
+    std::memcpy(s.host + o_len, len.data(), sizeof(int32_t) * n_pad);
+    int32_t* hr = (int32_t*)(s.host + o_rst);
+    for (int i = 0; i < n_pad; ++i) hr[i] = reset && i < n ? (reset[i] ? 1 : 0) : 0;
+    float* feat = (float*)(s.host + o_feat);
+    const auto t0 = Clock::now();
+    // blocks of 32 rows, frames outer: each frame's 32 source rows are one contiguous run of the
+    // frame-major input, and the block writes 32 sequential destination streams (row-by-row packing
+    // would touch a new page per 960-byte frame: the rows of one frame are n x 1 KB apart)
+    at::parallel_for(0, (n + 31) / 32, 1, [&](int64_t b, int64_t e) {
+      for (int64_t blk = b; blk < e; ++blk) {
+        const int64_t i0 = blk * 32, i1 = std::min<int64_t>(n, i0 + 32);
+        int64_t base[32];
+        for (int64_t i = i0; i < i1; ++i) base[i - i0] = off[i];
+        for (size_t c = 0; c < chunks.size(); ++c) {
+          const int32_t* lc = cl[c].data_ptr<int32_t>();
+          const int64_t R = f[c].size(1), C = f[c].size(2);
+          int32_t tmax = 0;
+          for (int64_t i = i0; i < i1; ++i) tmax = std::max(tmax, lc[i]);
+          for (int32_t t = 0; t < tmax; ++t) {
+            const float* src = f[c].data_ptr<float>() + (int64_t)t * R * C;
+            for (int64_t i = i0; i < i1; ++i)
+              if (t < lc[i]) std::memcpy(feat + (base[i - i0] + t) * mi355x::kFeat, src + i * C, mi355x::kFeat * sizeof(float));
+          }
+          for (int64_t i = i0; i < i1; ++i) base[i - i0] += lc[i];
+        }
+      }
+    });
+    const auto t1 = Clock::now();
+    hcheck(hipMemcpyAsync(s.dev, s.host, bytes, hipMemcpyHostToDevice, s.st), "copy batch");
+    hcheck(hipStreamSynchronize(s.st), "sync");
+    const auto t2 = Clock::now();
+    const int64_t* d_off = (const int64_t*)(s.dev + o_off);
+    const int32_t* d_len = (const int32_t*)(s.dev + o_len);
+    s.d_reset = (int32_t*)(s.dev + o_rst);
+    const float* store = (const float*)(s.dev + o_feat);
+    Gpu& g = *ls.gpu;
+    uint64_t ticket = 0;
+    if (opts_.encode_turns) {
+      std::unique_lock<std::mutex> l(g.turn_mu);
+      ticket = g.next_ticket++;
+      g.turn_cv.wait(l, [&] { return g.serving == ticket; });
+    }
+    const auto t3 = Clock::now();
+    int rc = 0;
+    hipError_t hr_sync = hipSuccess;
+    if (reset)
+      rc = rnnt_engine_encode_stream(s.e, store, d_off, d_len, len.data(), s.d_reset, T, n, n_pad, s.st);
+    else
+      rc = rnnt_engine_encode_gather(s.e, store, d_off, d_len, len.data(), T, n, n_pad, nullptr, s.st);
+    if (rc == 0) hr_sync = hipStreamSynchronize(s.st);  // the encoder is free again: the next turn may go
+    if (opts_.encode_turns) {
+      std::lock_guard<std::mutex> l(g.turn_mu);
+      g.serving++;
+      g.turn_cv.notify_all();
+    }
+    const auto t4 = Clock::now();
+    mi355x::check(rc, reset ? "rnnt_engine_encode_stream" : "rnnt_engine_encode_gather");
+    hcheck(hr_sync, "sync");
+    s.n = n;
+    std::lock_guard<std::mutex> l(stats_mu_);
+    stats_.pack += secs(t0, t1);
+    stats_.copy += secs(t1, t2);
+    stats_.turn_wait += secs(t2, t3);
+    stats_.encode += secs(t3, t4);
+    stats_.calls++;
+    stats_.frames += total;
+  }
+
+  std::string file_;
+  Options opts_;
+  std::vector<std::unique_ptr<Gpu>> gpus_;
+  mutable std::mutex mu_;
+  std::condition_variable lease_cv_;
+  std::unordered_map<const void*, Lease> leases_;
+  mutable std::mutex stats_mu_;
+  mi355x::CallStats stats_;
 };
 
 }  // namespace models

@@ -1,39 +1,59 @@
-// sut_harness.cpp -- runs the TorchModel replacement (rnnt_model_mi355x.hpp) the way the reference's
-// OfflineSUT::thInstance runs TorchModel (csrc/torch_sut.cpp:140-236), for a test to check:
-//   sort the samples longest first (RNNTQuerySampleLibrary::Sort, rnnt_qsl.cpp:104-133), take up to
-//   batch_size of them, AssembleSamples into [T_max][N_pad][256] zero-padded fp32 (rnnt_qsl.cpp:150-188,
-//   N_pad a multiple of 32 -- the intent of torch_sut.cpp:203, whose integer division floors),
-//   state.update(x, x_lens, split_len, actual_batch_size) -> model.encode(which, state) ->
-//   model.decode(which, state) -> QuerySamplesComplete: per sample the response is
-//   (state.res_[i].data_ptr(), (res_idx_[i] + 1) * 4 bytes) (torch_sut.cpp:221-236).
-// No LoadGen here: the "completion" writes (sample index, bytes, payload) records to out_file, and the
-// State contract is checked per row (res_idx_ = length - 1, SOS (-1) in every column past it).
+// sut_harness.cpp -- drives the TorchModel replacement (rnnt_model_mi355x.hpp) the way the reference's SUT
+// drives TorchModel, with the reference's own State protocol (restated in sut_state.hpp), for tests and
+// throughput runs.  No LoadGen: "QuerySamplesComplete" writes (query position, bytes, payload) records.
 //
-//   rnnt_sut_harness <engine_file> <feats.bin fp32 [N][T_max][240]> <lens.bin int32 [N]> <N> <T_max>
-//                    <batch_size> <out_file>
-// Prints one JSON line: batches, responses, rows whose res_ fill or res_idx_ broke the contract.
+// --scenario offline (OfflineSUT, torch_sut.cpp:88-236): the query is sorted longest first
+//   (RNNTQuerySampleLibrary::Sort, rnnt_qsl.cpp:104-133); --threads instances, instance `index` calling
+//   the model with which = index & 1 (torch_sut.cpp:145), each with its own State(batch, split_len):
+//   warm up (dummy N(0,1) batches of MAX_FEA_LEN frames, torch_sut.cpp:124-138), then repeatedly take up
+//   to --batch samples off the shared queue under the mutex (:167-182), AssembleSamples into
+//   [T][N_pad][256] (rnnt_qsl.cpp:150-188; N_pad a multiple of 32, the intent of torch_sut.cpp:203, whose
+//   integer division floors), state.update(x, x_lens, split_len, actual_batch_size), model.encode,
+//   model.decode, and answer each sample with (res_[i], (res_idx_[i] + 1) * 4 bytes) (:221-236).
+// --scenario server (ServerSUT, torch_sut.cpp:238-571, no audio processor): one producer assembles
+//   --pro-batch samples at a time and queues each as ([T][1][256], length) (:436-461); --threads consumers,
+//   each with a PipelineState(batch, split_len, response) (:470-540): dequeue up to finish_size_ samples,
+//   state.update, model.encode, model.decode, answer every slot with finish_idx_ && F_lens_ > 0 (:542-571).
+//
+//   rnnt_sut_harness --engine F --feats F --lens F [--query F] [--scenario offline|server] [--threads K]
+//                    [--batch B] [--split-len L] [--response R] [--pro-batch P] [--warmup W] [--intra C]
+//                    --out F
+// --feats: fp32 [sum(lens)][240], the samples' frames back to back; --lens: int32 [N]; --query: int32 QSL
+// indices (default 0..N-1).  Prints one JSON line.
 #include <link.h>
 #include <limits.h>
 #include <stdlib.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdio>
+#include <deque>
 #include <fstream>
-#include <set>
 #include <iostream>
+#include <list>
+#include <map>
 #include <numeric>
+#include <set>
+#include <thread>
 
 #include "rnnt_model_mi355x.hpp"
+#include "sut_state.hpp"
 
 namespace {
+
 template <class T>
-std::vector<T> read_file(const char* path, size_t count) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) throw std::runtime_error(std::string("cannot open ") + path);
-  std::vector<T> v(count);
-  f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)(count * sizeof(T)));
-  if ((size_t)f.gcount() != count * sizeof(T)) throw std::runtime_error(std::string("short file ") + path);
+std::vector<T> read_file(const std::string& path) {
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  const std::streamsize bytes = f.tellg();
+  if (bytes % (std::streamsize)sizeof(T)) throw std::runtime_error("ragged file " + path);
+  std::vector<T> v((size_t)bytes / sizeof(T));
+  f.seekg(0);
+  f.read(reinterpret_cast<char*>(v.data()), bytes);
+  if (f.gcount() != bytes) throw std::runtime_error("short read " + path);
   return v;
 }
+
 // distinct files mapped as a HIP runtime (two would mean two HIP runtimes: torch's and the system's)
 int hip_runtimes() {
   std::set<std::string> files;
@@ -49,6 +69,218 @@ int hip_runtimes() {
       &files);
   return (int)files.size();
 }
+
+// The QSL: every sample's [len][240] frames in host memory (LoadSamplesToRam).
+struct Qsl {
+  std::vector<float> feats;
+  std::vector<int32_t> lens;
+  std::vector<int64_t> first;  // first frame row of each sample
+  int max_len = 0;
+  at::Tensor sample(int64_t idx) const {  // [len][240] view (x_set_[index])
+    return at::from_blob(const_cast<float*>(feats.data()) + first[idx] * rnnt::dims::kInput,
+                         {lens[idx], rnnt::dims::kInput}, at::kFloat);
+  }
+  // RNNTQuerySampleLibrary::AssembleSamples, features mode (rnnt_qsl.cpp:150-188): x [T_max][padded][256]
+  // zero except each sample's frames in channels 0..239.  `buf` (optional, per thread) is reused across
+  // batches: only what the samples do not overwrite is zeroed, instead of a fresh zero-filled tensor per
+  // batch (whose page faults and fill would dominate a large batch's host time)
+  std::pair<at::Tensor, at::Tensor> assemble(const std::vector<int64_t>& idx, int64_t padded, at::Tensor* buf = nullptr) const {
+    const int64_t n = (int64_t)idx.size();
+    constexpr int64_t C = rnnt::dims::kPaddedInput, I = rnnt::dims::kInput;
+    int32_t T = 0;
+    for (int64_t i : idx) T = std::max(T, lens[i]);
+    at::Tensor x;
+    if (buf) {
+      const int64_t need = (int64_t)T * padded * C;
+      if (!buf->defined() || buf->numel() < need) *buf = at::empty({std::max<int64_t>(need, 1)}, at::kFloat);
+      x = buf->narrow(0, 0, need).view({T, padded, C});
+    } else {
+      x = at::zeros({T, padded, C}, at::kFloat);
+    }
+    at::Tensor x_lens = at::zeros({padded}, at::kInt);
+    float* xp = x.data_ptr<float>();
+    int32_t* lp = x_lens.data_ptr<int32_t>();
+    for (int64_t i = 0; i < n; ++i) lp[i] = lens[idx[i]];
+    // blocks of 32 rows, frames outer (each frame's rows are one contiguous run of x)
+    at::parallel_for(0, (padded + 31) / 32, 1, [&](int64_t b, int64_t e) {
+      for (int64_t blk = b; blk < e; ++blk) {
+        const int64_t i0 = blk * 32, i1 = std::min<int64_t>(padded, i0 + 32);
+        for (int32_t t = 0; t < T; ++t) {
+          for (int64_t i = i0; i < i1; ++i) {
+            const int32_t L = i < n ? lens[idx[i]] : 0;
+            float* dst = xp + ((int64_t)t * padded + i) * C;
+            if (t < L) {
+              std::memcpy(dst, feats.data() + (first[idx[i]] + t) * I, I * sizeof(float));
+              if (buf) std::memset(dst + I, 0, (C - I) * sizeof(float));
+            } else if (buf) {
+              std::memset(dst, 0, C * sizeof(float));
+            }
+          }
+        }
+      }
+    });
+    return {x, x_lens};
+  }
+};
+
+// "QuerySamplesComplete": records + the State contract per answered row: res_idx_ in range and, for a State
+// (Offline), SOS past the row's tokens (update() refills res_ per batch, metadata.cpp:59).  A PipelineState
+// only resets res_idx_ when it refills a slot (metadata.cpp:142), so past a Server row's tokens res_ may
+// hold the slot's previous utterance, in the reference as here; nothing reads it.
+struct Responder {
+  bool check_fill = true;
+  std::mutex mu;
+  std::ofstream out;
+  int64_t responses = 0, bad_fill = 0, bad_idx = 0;
+  std::chrono::steady_clock::time_point last;
+  void complete(const rnnt::Sample& s, const at::Tensor& res_row, int32_t res_len, int32_t max_res) {
+    const int32_t* row = res_row.data_ptr<int32_t>();
+    int fill_bad = 0;
+    for (int32_t j = std::max(res_len, 0); check_fill && j < max_res; ++j)
+      if (row[j] != rnnt::dims::kSos) {
+        fill_bad = 1;
+        break;
+      }
+    const int32_t id = (int32_t)s.id, size = std::max(res_len, 0) * 4;
+    std::lock_guard<std::mutex> l(mu);
+    if (res_len < 0 || res_len > max_res) ++bad_idx;
+    bad_fill += fill_bad;
+    out.write(reinterpret_cast<const char*>(&id), 4);
+    out.write(reinterpret_cast<const char*>(&size), 4);
+    out.write(reinterpret_cast<const char*>(row), size);
+    ++responses;
+    last = std::chrono::steady_clock::now();
+  }
+};
+
+struct Args {
+  std::map<std::string, std::string> kv;
+  std::string get(const std::string& k, const std::string& d = "") const {
+    auto it = kv.find(k);
+    return it == kv.end() ? d : it->second;
+  }
+  int num(const std::string& k, int d) const { return std::atoi(get(k, std::to_string(d)).c_str()); }
+};
+
+int usage(const char* argv0) {
+  std::fprintf(stderr,
+               "usage: %s --engine F --feats F --lens F --out F [--query F] [--scenario offline|server] [--threads K]\n"
+               "          [--batch B] [--split-len L] [--response R] [--pro-batch P] [--warmup W] [--intra C] [--progress S]\n",
+               argv0);
+  return 2;
+}
+
+using Clock = std::chrono::steady_clock;
+
+// the first exception of any instance thread, rethrown by main (an escaping one would terminate)
+std::mutex g_err_mu;
+std::exception_ptr g_err;
+bool failed() {
+  std::lock_guard<std::mutex> l(g_err_mu);
+  return (bool)g_err;
+}
+template <class F>
+void guarded(F f) {
+  try {
+    f();
+  } catch (...) {
+    std::lock_guard<std::mutex> l(g_err_mu);
+    if (!g_err) g_err = std::current_exception();
+  }
+}
+
+// OfflineSUT::thInstance (torch_sut.cpp:140-219)
+void offline_instance(int index, rnnt::models::TorchModel& model, const Qsl& qsl, std::list<rnnt::Sample>& queue,
+                      std::mutex& qmu, Responder& resp, int bs, int split_len, int warmup, int intra,
+                      std::atomic<int>& warm, std::atomic<bool>& go, std::atomic<int64_t>& batches) {
+  const int which = index & 1;
+  if (intra > 0) at::set_num_threads(intra);  // this instance's team (the reference pins INTRA threads, :143-149)
+  at::Tensor xbuf;
+  for (int i = 0; i < warmup; ++i) {  // OfflineSUT::warmup (:124-138), GenerateDummySamples (rnnt_qsl.cpp:136-147)
+    rnnt::State ws(bs, split_len);
+    at::Tensor x = at::randn({bs, rnnt::dims::kPaddedInput, rnnt::dims::kMaxFeaLen}).permute({2, 0, 1}).contiguous();
+    at::Tensor x_lens = at::full({bs}, rnnt::dims::kMaxFeaLen, at::kInt);
+    ws.update(x, x_lens, split_len);
+    model.forward(which, ws);
+  }
+  warm++;
+  while (!go) std::this_thread::yield();
+  rnnt::State state(bs, split_len);
+  while (true) {
+    std::vector<rnnt::Sample> samples;
+    {
+      std::lock_guard<std::mutex> l(qmu);
+      if (queue.empty()) break;
+      const size_t k = std::min(queue.size(), (size_t)bs);
+      auto it = queue.begin();
+      std::advance(it, k);
+      samples.assign(queue.begin(), it);
+      queue.erase(queue.begin(), it);
+    }
+    std::vector<int64_t> idx(samples.size());
+    for (size_t i = 0; i < samples.size(); ++i) idx[i] = (int64_t)samples[i].index;
+    const int n = (int)samples.size();
+    auto [x, x_lens] = qsl.assemble(idx, (n + 31) / 32 * 32, &xbuf);
+    state.update(x, x_lens, split_len, n);
+    model.encode(which, state);
+    model.decode(which, state);
+    const at::Tensor res_lens = state.res_idx_ + 1;
+    for (int i = 0; i < n; ++i)
+      resp.complete(samples[i], state.res_[i], res_lens[i].item<int32_t>(), state.max_res_len_);
+    batches++;
+  }
+}
+
+// ServerSUT::thConsumer (torch_sut.cpp:470-540) and QuerySamplesComplete (:542-571)
+void server_consumer(int index, rnnt::models::TorchModel& model, std::deque<rnnt::PipelineState::Entry>& processed,
+                     std::mutex& pmu, std::atomic<bool>& produced, Responder& resp, int bs, int split_len,
+                     int response, int warmup, int intra, std::atomic<int>& warm, std::atomic<bool>& go,
+                     std::atomic<int64_t>& batches) {
+  const int which = index & 1;
+  if (intra > 0) at::set_num_threads(intra);
+  for (int i = 0; i < warmup; ++i) {  // ServerSUT::warmup, consumer (:341-346)
+    rnnt::State ws(bs, split_len);
+    at::Tensor x = at::randn({bs, rnnt::dims::kPaddedInput, rnnt::dims::kMaxFeaLen}).permute({2, 0, 1}).contiguous();
+    ws.update(x, at::full({bs}, rnnt::dims::kMaxFeaLen, at::kInt), split_len);
+    model.forward(which, ws);
+  }
+  warm++;
+  while (!go) std::this_thread::yield();
+  std::vector<rnnt::Sample> samples(bs);
+  rnnt::PipelineState state(bs, split_len, response);
+  while (true) {
+    std::vector<rnnt::PipelineState::Entry> dq;
+    int32_t dequeue_size = 0;
+    bool finish_dequeue = false;
+    while (!finish_dequeue && dequeue_size == 0 && state.finish_size_ != 0) {
+      {
+        std::lock_guard<std::mutex> l(pmu);
+        if (produced && processed.empty()) {  // no new samples left
+          finish_dequeue = true;
+          break;
+        }
+        while (!processed.empty() && dequeue_size < state.finish_size_) {  // wait_dequeue_bulk_timed(.., 0)
+          dq.push_back(std::move(processed.front()));
+          processed.pop_front();
+          ++dequeue_size;
+        }
+      }
+      if (state.remain_size_ != 0) break;
+      if (dequeue_size == 0) std::this_thread::yield();
+    }
+    if (finish_dequeue && state.remain_size_ == 0) break;
+    state.update(dq, samples, dequeue_size, split_len);
+    model.encode(which, state);
+    model.decode(which, state);
+    const at::Tensor res_lens = state.res_idx_ + 1;
+    const bool* fin = state.finish_idx_.data_ptr<bool>();
+    const int32_t* Fl = state.F_lens_.data_ptr<int32_t>();
+    for (int i = 0; i < bs; ++i)
+      if (fin[i] && Fl[i] > 0) resp.complete(samples[i], state.res_[i], res_lens[i].item<int32_t>(), state.max_res_len_);
+    batches++;
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -56,66 +288,142 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "rnnt_sut_harness: %d HIP runtimes mapped (expected torch's only)\n", hip_runtimes());
     return 3;
   }
-  if (argc != 8) {
-    std::fprintf(stderr, "usage: %s engine_file feats.bin lens.bin N T_max batch_size out_file\n", argv[0]);
-    return 2;
+  Args a;
+  for (int i = 1; i < argc; ++i) {
+    const std::string k = argv[i];
+    if (k.rfind("--", 0) != 0 || i + 1 >= argc) return usage(argv[0]);
+    a.kv[k.substr(2)] = argv[++i];
   }
+  if (a.get("engine").empty() || a.get("feats").empty() || a.get("lens").empty() || a.get("out").empty())
+    return usage(argv[0]);
   try {
-    const int N = std::atoi(argv[4]), T_max = std::atoi(argv[5]), bs = std::atoi(argv[6]);
-    if (N <= 0 || T_max <= 0 || T_max > rnnt::MAX_FEA_LEN || bs <= 0) throw std::runtime_error("bad N / T_max / batch_size");
-    const std::vector<float> feats = read_file<float>(argv[2], (size_t)N * T_max * 240);
-    const std::vector<int32_t> lens = read_file<int32_t>(argv[3], (size_t)N);
-    for (int32_t l : lens)
-      if (l < 0 || l > T_max) throw std::runtime_error("sample length out of range");
-    rnnt::models::TorchModel model(argv[1], /*n_gpus=*/1, /*max_batch=*/(bs + 255) / 256 * 256);
-    // Sort: longest first, stable (rnnt_qsl.cpp:104-133 buckets by length)
-    std::vector<int> order(N);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lens[a] > lens[b]; });
-    std::ofstream out(argv[7], std::ios::binary);
-    rnnt::State state(bs);
-    int batches = 0, responses = 0, bad_fill = 0, bad_idx = 0;
-    for (int s0 = 0; s0 < N; s0 += bs) {
-      const int n = std::min(bs, N - s0);
-      const int n_pad = (n + 31) / 32 * 32;
-      int t_b = 0;
-      for (int i = 0; i < n; ++i) t_b = std::max(t_b, lens[order[s0 + i]]);
-      t_b = std::max(t_b, 1);
-      at::Tensor x = at::zeros({t_b, n_pad, rnnt::PADDED_INPUT_SIZE}, at::kFloat);  // AssembleSamples
-      at::Tensor x_lens = at::zeros({n_pad}, at::kInt);
-      float* xp = x.data_ptr<float>();
-      for (int i = 0; i < n; ++i) {
-        const int s = order[s0 + i];
-        x_lens.data_ptr<int32_t>()[i] = lens[s];
-        for (int t = 0; t < lens[s]; ++t)
-          std::memcpy(xp + ((size_t)t * n_pad + i) * rnnt::PADDED_INPUT_SIZE, &feats[((size_t)s * T_max + t) * 240],
-                      240 * sizeof(float));
-      }
-      state.update(x, x_lens, /*split_len=*/-1, n);
-      model.encode(0, state);
-      model.decode(0, state);
-      // QuerySamplesComplete (torch_sut.cpp:221-236)
-      const at::Tensor res_lens = state.res_idx_ + 1;
-      for (int i = 0; i < n; ++i) {
-        const int32_t res_len = res_lens[i].item().toInt();
-        const int32_t* row = state.res_[i].data_ptr<int32_t>();
-        const int32_t size = res_len * 4;
-        if (res_len < 0 || res_len > state.max_res_len_) ++bad_idx;
-        for (int j = std::max(res_len, 0); j < state.max_res_len_; ++j)
-          if (row[j] != rnnt::SOS) {
-            ++bad_fill;
-            break;
-          }
-        const int32_t sid = order[s0 + i];
-        out.write(reinterpret_cast<const char*>(&sid), 4);
-        out.write(reinterpret_cast<const char*>(&size), 4);
-        out.write(reinterpret_cast<const char*>(row), size);
-        ++responses;
-      }
-      ++batches;
+    const std::string scenario = a.get("scenario", "offline");
+    const int threads = a.num("threads", 1), bs = a.num("batch", 256), split_len = a.num("split-len", -1);
+    const int warmup = a.num("warmup", 0), intra = a.num("intra", 0);
+    if (threads <= 0 || bs <= 0 || (scenario != "offline" && scenario != "server")) return usage(argv[0]);
+    if (intra > 0) at::set_num_threads(intra);
+    Qsl qsl;
+    qsl.lens = read_file<int32_t>(a.get("lens"));
+    qsl.feats = read_file<float>(a.get("feats"));
+    int64_t rows = 0;
+    for (int32_t l : qsl.lens) {
+      if (l < 0 || l > rnnt::dims::kMaxFeaLen) throw std::runtime_error("sample length out of range");
+      qsl.first.push_back(rows);
+      rows += l;
+      qsl.max_len = std::max(qsl.max_len, l);
     }
-    std::cout << "{\"batches\": " << batches << ", \"responses\": " << responses << ", \"bad_sos_fill_rows\": "
-              << bad_fill << ", \"bad_res_idx_rows\": " << bad_idx << "}" << std::endl;
+    if ((int64_t)qsl.feats.size() != rows * rnnt::dims::kInput) throw std::runtime_error("feats do not match lens");
+    std::vector<int32_t> query;
+    if (!a.get("query").empty()) {
+      query = read_file<int32_t>(a.get("query"));
+    } else {
+      query.resize(qsl.lens.size());
+      std::iota(query.begin(), query.end(), 0);
+    }
+    for (int32_t q : query)
+      if (q < 0 || q >= (int32_t)qsl.lens.size()) throw std::runtime_error("query index out of range");
+
+    rnnt::models::TorchModel model(a.get("engine"));
+    Responder resp;
+    // progress on stderr every --progress seconds (a long run stays visibly alive)
+    const int progress = a.num("progress", 10);
+    std::atomic<bool> done{false};
+    const Clock::time_point t_start = Clock::now();
+    std::thread monitor([&] {
+      auto next = t_start;
+      while (!done) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        if (progress <= 0 || Clock::now() < next) continue;
+        next += std::chrono::seconds(progress);
+        int64_t n;
+        {
+          std::lock_guard<std::mutex> l(resp.mu);
+          n = resp.responses;
+        }
+        const auto cs = model.stats();
+        std::fprintf(stderr, "[harness %.0f s] responses %lld, encode calls %lld (pack %.1f s, copy %.1f s, turn wait %.1f s, "
+                     "encode %.1f s, decode %.1f s)\n", std::chrono::duration<double>(Clock::now() - t_start).count(),
+                     (long long)n, (long long)cs.calls, cs.pack, cs.copy, cs.turn_wait, cs.encode, cs.decode);
+      }
+    });
+    struct Join {
+      std::atomic<bool>& d;
+      std::thread& t;
+      ~Join() {
+        d = true;
+        t.join();
+      }
+    } join_monitor{done, monitor};
+    resp.out.open(a.get("out"), std::ios::binary);
+    std::atomic<int> warm{0};
+    std::atomic<bool> go{false};
+    std::atomic<int64_t> batches{0};
+    std::vector<std::thread> th;
+    Clock::time_point t0;
+    if (scenario == "offline") {
+      // IssueQuery: Sort longest first (stable within a length)
+      std::vector<rnnt::Sample> s(query.size());
+      for (size_t i = 0; i < query.size(); ++i) s[i] = {(uint64_t)i, (uint64_t)query[i]};
+      std::stable_sort(s.begin(), s.end(), [&](const rnnt::Sample& x, const rnnt::Sample& y) {
+        return qsl.lens[x.index] > qsl.lens[y.index];
+      });
+      std::list<rnnt::Sample> queue(s.begin(), s.end());
+      std::mutex qmu;
+      for (int i = 0; i < threads; ++i)
+        th.emplace_back([&, i] {
+          guarded([&] { offline_instance(i, model, qsl, queue, qmu, resp, bs, split_len, warmup, intra, warm, go, batches); });
+        });
+      while (warm < threads && !failed()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      model.stats(/*reset=*/true);  // the warmups' calls are not counted
+      t0 = Clock::now();
+      go = true;
+      for (auto& t : th) t.join();
+    } else {
+      const int response = a.num("response", bs), pro_bs = a.num("pro-batch", 4);
+      resp.check_fill = false;
+      std::deque<rnnt::PipelineState::Entry> processed;
+      std::mutex pmu;
+      std::atomic<bool> produced{false};
+      for (int i = 0; i < threads; ++i)
+        th.emplace_back([&, i] {
+          guarded([&] {
+            server_consumer(i, model, processed, pmu, produced, resp, bs, split_len, response, warmup, intra, warm,
+                            go, batches);
+          });
+        });
+      while (warm < threads && !failed()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      model.stats(/*reset=*/true);  // the warmups' calls are not counted
+      t0 = Clock::now();
+      go = true;
+      // ServerSUT::thProducer without the audio processor (:436-461): samples in arrival order
+      for (size_t s0 = 0; s0 < query.size(); s0 += (size_t)pro_bs) {
+        const size_t n = std::min(query.size() - s0, (size_t)pro_bs);
+        std::vector<int64_t> idx(n);
+        for (size_t i = 0; i < n; ++i) idx[i] = query[s0 + i];
+        auto [x, x_lens] = qsl.assemble(idx, (int64_t)n);
+        std::vector<rnnt::PipelineState::Entry> items;
+        for (size_t i = 0; i < n; ++i)
+          items.emplace_back(rnnt::Sample{(uint64_t)(s0 + i), (uint64_t)idx[i]},
+                             x.narrow(1, (int64_t)i, 1).contiguous(), x_lens.narrow(0, (int64_t)i, 1).clone());
+        std::lock_guard<std::mutex> l(pmu);
+        for (auto& it : items) processed.push_back(std::move(it));
+      }
+      produced = true;
+      for (auto& t : th) t.join();
+    }
+    if (g_err) std::rethrow_exception(g_err);
+    const double secs = std::chrono::duration<double>(resp.last - t0).count();
+    const auto per_gpu = model.engines_per_gpu();
+    std::cout << "{\"scenario\": \"" << scenario << "\", \"threads\": " << threads << ", \"batch\": " << bs
+              << ", \"split_len\": " << split_len << ", \"batches\": " << batches.load() << ", \"responses\": "
+              << resp.responses << ", \"bad_sos_fill_rows\": " << resp.bad_fill << ", \"bad_res_idx_rows\": "
+              << resp.bad_idx << ", \"seconds\": " << secs << ", \"samples_per_s\": "
+              << (secs > 0 ? (double)resp.responses / secs : 0.0) << ", \"engines_per_gpu\": [";
+    for (size_t i = 0; i < per_gpu.size(); ++i) std::cout << (i ? ", " : "") << per_gpu[i];
+    const auto cs = model.stats();
+    std::cout << "], \"model_host_seconds\": {\"pack\": " << cs.pack << ", \"copy\": " << cs.copy
+              << ", \"turn_wait\": " << cs.turn_wait << ", \"encode\": " << cs.encode << ", \"decode\": " << cs.decode
+              << ", \"encode_calls\": " << cs.calls << ", \"frames\": " << cs.frames << "}}" << std::endl;
     return 0;
   } catch (const std::exception& ex) {
     std::fprintf(stderr, "rnnt_sut_harness: %s\n", ex.what());

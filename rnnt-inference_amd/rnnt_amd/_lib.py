@@ -67,6 +67,7 @@ _SIGS = {
     "rnnt_engine_set_decode_persist": (C.c_int, [C.c_void_p, C.c_int]),
     "rnnt_engine_get_stats": (C.c_int, [C.c_void_p, C.POINTER(RnntStats), C.c_int]),
     "rnnt_abi_version": (C.c_int, []),
+    "rnnt_install_crash_report": (C.c_int, []),
     "rnnt_stream_create": (C.c_int, [C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     "rnnt_stream_destroy": (C.c_int, [C.c_void_p]),
     "rnnt_last_error": (C.c_char_p, []),

@@ -1,13 +1,16 @@
 """The compiled TorchModel replacement (rnnt-inference_amd/csrc/sut/rnnt_model_mi355x.hpp, INTEGRATION.md
-section 1) run as the reference's OfflineSUT runs TorchModel.
+section 1) driven through the reference SUT's own State protocol.
 
 The harness (csrc/sut/sut_harness.cpp, built by the Makefile against include/rnnt_mi355x.h and libtorch)
-loads the engine file tools/export_model.py writes, sorts the samples longest first, assembles batches,
-and per batch calls state.update -> model.encode -> model.decode and completes every sample the way
-QuerySamplesComplete does (csrc/torch_sut.cpp:221-236): (state.res_[i].data_ptr(), (res_idx_[i] + 1) * 4
-bytes).  Checked here: every sample answered once; each payload equals the CPU restatement's tokens,
-so res_idx_ = length - 1 (metadata.cpp:59-60); and the harness itself checks the -1 (SOS) fill of
-res_ past each row's tokens."""
+runs the model the way the reference's SUT runs TorchModel, with State / PipelineState restated from
+metadata.cpp (csrc/sut/sut_state.hpp):
+* Offline (OfflineSUT::thInstance, torch_sut.cpp:140-236): several instances at once, instance i calling
+  with which = i & 1, each its own State(batch, split_len); split_len > 0 goes through State::next()
+  exactly as the reference's run.sh Offline setting (LEN=2, INTER=28, run.sh:68-71).
+* Server (ServerSUT::thConsumer, :470-571): consumers with a PipelineState each -- slot refill, chunked
+  next(), answers for finished slots only.
+Checked: every sample answered once; each payload equals the CPU restatement's tokens; the harness
+checks the SOS (-1) fill of res_ past each answered row and res_idx_ = length - 1."""
 import json
 import os
 import subprocess
@@ -35,26 +38,81 @@ def _responses(path):
     return out
 
 
-def test_cpp_torch_model_state_contract(tmp_path, oracle):
-    assert os.path.exists(HARNESS), "harness not built (make -C rnnt-inference_amd/csrc)"
+@pytest.fixture(scope="module")
+def setup(tmp_path_factory, oracle):
+    tmp = tmp_path_factory.mktemp("harness")
     pm, _ = weights.build_model()
-    eng_file = weights.save_engine_file(pm, str(tmp_path / "rnnt.engine"))
-    lens = np.array([57, 0, 31, 12, 44, 3, 50, 29, 38, 9, 61, 22, 47, 17, 5, 33, 26, 1, 40, 60], np.int32)
+    eng_file = weights.save_engine_file(pm, str(tmp / "rnnt.engine"))
+    rng = np.random.default_rng(61)
+    lens = rng.integers(1, 62, 40).astype(np.int32)
+    lens[[3, 17]] = [0, 61]
+    lens[[5, 9, 22]] = [1, 2, 33]
     N, T = len(lens), int(lens.max())
     x = synthetic.make_features(T, N, seed=24, lens=lens)[:, :, :240]  # [T][N][240]
-    np.ascontiguousarray(x.transpose(1, 0, 2)).tofile(tmp_path / "feats.bin")  # [N][T][240]
-    lens.tofile(tmp_path / "lens.bin")
-    out = tmp_path / "responses.bin"
-    env = dict(os.environ)
-    r = subprocess.run([HARNESS, eng_file, str(tmp_path / "feats.bin"), str(tmp_path / "lens.bin"), str(N), str(T),
-                        "8", str(out)], capture_output=True, text=True, timeout=90, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
-    summary = json.loads(r.stdout.strip().splitlines()[-1])
-    assert summary == {"batches": 3, "responses": N, "bad_sos_fill_rows": 0, "bad_res_idx_rows": 0}, summary
-    got = _responses(out)
-    assert sorted(got) == list(range(N))
+    ragged = np.concatenate([x[: lens[i], i] for i in range(N)])  # the QSL's frames back to back
+    ragged.astype(np.float32).tofile(tmp / "feats.bin")
+    lens.tofile(tmp / "lens.bin")
     fo = oracle.encoder_i8(pm, np.pad(x, ((0, 0), (0, 0), (0, 16))), lens)
     ro, rlo, _ = oracle.greedy_decode(pm, fo, (lens + 1) // 2, max_res=(500 // 2) * 30)
-    assert rlo.max() > 3 and rlo[1] == 0
+    assert rlo.max() > 3 and rlo[3] == 0
+    return dict(tmp=tmp, eng=eng_file, lens=lens, want=[ro[i, : rlo[i]] for i in range(N)])
+
+
+def _run(setup, name, env_extra=None, **kw):
+    tmp = setup["tmp"]
+    out = tmp / f"{name}.bin"
+    cmd = [HARNESS, "--engine", setup["eng"], "--feats", str(tmp / "feats.bin"), "--lens", str(tmp / "lens.bin"),
+           "--out", str(out)]
+    for k, v in kw.items():
+        cmd += ["--" + k.replace("_", "-"), str(v)]
+    env = dict(os.environ, **(env_extra or {}))
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    summary = json.loads(r.stdout.strip().splitlines()[-1])
+    assert summary["bad_sos_fill_rows"] == 0 and summary["bad_res_idx_rows"] == 0, summary
+    return summary, _responses(out)
+
+
+@pytest.mark.parametrize("threads,split_len,env", [
+    (1, -1, {}),                                 # one instance, whole batches
+    (8, 2, {}),                                  # run.sh's Offline shape: split_len 2, which = index & 1
+    (4, 2, {"RNNT_ENGINES_PER_GPU": "1"}),       # more instances than engines: leases wait and are reused
+    (6, 4, {"RNNT_ENCODE_TURNS": "0"}),          # encoders of one GPU overlapping
+])
+def test_offline_state_protocol(setup, threads, split_len, env):
+    assert os.path.exists(HARNESS), "harness not built (make -C rnnt-inference_amd/csrc)"
+    N = len(setup["lens"])
+    summary, got = _run(setup, f"off_{threads}_{split_len}", env, scenario="offline", threads=threads, batch=6,
+                        split_len=split_len, warmup=1 if threads == 8 else 0, intra=2)
+    assert summary["responses"] == N and summary["batches"] == -(-N // 6), summary
+    assert sorted(got) == list(range(N))
     for i in range(N):
-        np.testing.assert_array_equal(got[i], ro[i, : rlo[i]], err_msg=f"sample {i}")
+        np.testing.assert_array_equal(got[i], setup["want"][i], err_msg=f"sample {i}")
+    if "RNNT_ENGINES_PER_GPU" in env:
+        assert summary["engines_per_gpu"] == [1], summary
+
+
+def test_offline_odd_split_rejected(setup):
+    tmp = setup["tmp"]
+    r = subprocess.run([HARNESS, "--engine", setup["eng"], "--feats", str(tmp / "feats.bin"), "--lens",
+                        str(tmp / "lens.bin"), "--out", str(tmp / "odd.bin"), "--split-len", "3"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "odd split_len" in r.stderr, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("threads,batch,split_len,response", [(1, 8, 8, 3), (3, 6, 8, 1), (2, 16, 2, 16)])
+def test_server_pipeline_state(setup, threads, batch, split_len, response):
+    """PipelineState slots refilled as they finish, each consumer keeping its engine; zero-length samples
+    are never answered by the reference's Server (F_lens_ > 0, torch_sut.cpp:552), so the query leaves
+    them out."""
+    lens = setup["lens"]
+    query = np.array([i for i in range(len(lens)) if lens[i] > 0], np.int32)
+    qf = setup["tmp"] / "query_server.bin"
+    query.tofile(qf)
+    summary, got = _run(setup, f"srv_{threads}_{batch}_{split_len}", scenario="server", threads=threads,
+                        batch=batch, split_len=split_len, response=response, pro_batch=4, query=qf, intra=2)
+    assert summary["responses"] == len(query), summary
+    assert sorted(got) == list(range(len(query)))
+    for pos, i in enumerate(query):
+        np.testing.assert_array_equal(got[pos], setup["want"][i], err_msg=f"query position {pos} (sample {i})")
+    assert summary["engines_per_gpu"][0] >= threads
