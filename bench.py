@@ -151,10 +151,10 @@ def mock_main(args):
         stream = dist.ResponseStream(world, group, tag=qno[0]) if world > 1 else None
         qno[0] += 1
         got = []
-        for b_ids, _ in mine:  # stand-in responses, shipped batch by batch like the SUT's completions
-            rl = (b_ids % 7).astype(np.int32)
-            toks = np.concatenate([np.full(int(n), int(i) % 29, np.int32) for i, n in zip(b_ids, rl)] +
-                                  [np.zeros(0, np.int32)])
+        for b_ids, b_idx in mine:  # stand-in responses, shipped batch by batch like the SUT's completions
+            # the timed workload's volume: ~0.55 symbols per encoder frame (64.6 per sample in BENCH_r05)
+            rl = (((lens[b_idx] + 1) // 2) * (45 + b_ids % 21) // 100).astype(np.int32)
+            toks = np.repeat((b_ids % 29).astype(np.int32), rl)
             if stream:
                 stream.push(b_ids, rl, toks)
             else:
@@ -177,6 +177,8 @@ def mock_main(args):
             np.savez_compressed(args.dump_responses, ids=got[0], lens=got[1], toks=got[2])
         print(json.dumps({"metric": METRIC, "value": None, "unit": "utterances/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                          "rows_per_s_gathered": round(query * args.steps / elapsed, 1),
+                          "tokens_per_query": int(got[1].sum()),
                           "data": "mock: no engine, stand-in responses (launcher / sharding check, not a measurement)",
                           "control_plane": dist.backend_name(),
                           "config": {"query_samples": query, "gathered": int(len(got[0]))}}), flush=True)

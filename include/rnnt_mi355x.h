@@ -17,8 +17,10 @@
  * Plain pointers and sizes only.  Device pointers are HIP device allocations on the engine's
  * device; `stream` is a hipStream_t used as given (0 = the null stream).  Every entry point
  * returns 0 on success or a negative errno-style code; rnnt_last_error() describes the last
- * failure on the calling thread.  One engine per GPU, driven by one host thread at a time;
- * distinct engines are independent (the reference's per-socket model clones, rnnt_model.hpp:45-46).
+ * failure on the calling thread.  An engine is one batch in flight on one GPU, driven by one host
+ * thread at a time; distinct engines (any number per GPU) are independent (the reference's per-socket
+ * model clones, rnnt_model.hpp:45-46).  The C++ drop-in (csrc/sut/rnnt_model_mi355x.hpp) leases them
+ * per call, so the reference SUT's threads never share one.
  */
 #ifndef RNNT_MI355X_H
 #define RNNT_MI355X_H

@@ -1044,18 +1044,18 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
   // overshoot).  Development knobs for that A/B: RNNT_DEC_TAIL_CHUNK steps per tail chunk,
   // RNNT_DEC_SPIN=1 polls the previous chunk's event without yielding (no gain measured).
   static const int TAIL_CHUNK = [] {
-    const char* v = getenv("RNNT_DEC_TAIL_CHUNK");
+    const char* v = dev_env("RNNT_DEC_TAIL_CHUNK");
     const int c = v ? atoi(v) : 16;
     return c >= 1 && c <= CHUNK ? c : 16;
   }();
   static const bool SPIN = [] {
-    const char* v = getenv("RNNT_DEC_SPIN");
+    const char* v = dev_env("RNNT_DEC_SPIN");
     return v && v[0] == '1';
   }();
   // development knob RNNT_DEC_RG="PxGxJ": row-group caps of the step kernels' grids (pred, G, joint)
   static const int* RG = [] {
     static int rg[3] = {PRED_ROW_GROUPS, G_ROW_GROUPS, JOINT_GROUPS};
-    if (const char* v = getenv("RNNT_DEC_RG")) {
+    if (const char* v = dev_env("RNNT_DEC_RG")) {
       int x[3];
       if (sscanf(v, "%dx%dx%d", &x[0], &x[1], &x[2]) == 3 && x[0] > 0 && x[1] > 0 && x[2] > 0)
         for (int i = 0; i < 3; ++i) rg[i] = x[i];

@@ -430,17 +430,17 @@ extern "C" int rnnt_engine_create(const rnnt_model_desc* model, int device, cons
   if (!r && !dscope.ok) r = fail(RNNT_EDEVICE, "hipSetDevice failed");
   if (!r && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
     r = fail(RNNT_EDEVICE, "hipStreamCreate failed");
-  if (const char* pr = getenv("RNNT_DEC_PERSIST_ROWS")) {  // development default, read once per engine
+  if (const char* pr = dev_env("RNNT_DEC_PERSIST_ROWS")) {  // development default, read once per engine
     const int v = atoi(pr);
     e->persist_rows = v < 0 ? 0 : (v > DEC_PERSIST_MAX ? DEC_PERSIST_MAX : v);
   }
-  if (const char* t = getenv("RNNT_ENC_TILE")) {  // development default, read once per engine
+  if (const char* t = dev_env("RNNT_ENC_TILE")) {  // development default, read once per engine
     const int v = tile_code(t);
     if (v < 0) r = fail(RNNT_EINVAL, std::string("RNNT_ENC_TILE=") + t + ": auto|ticks|flow|big|small|tiny|mini");
     e->tile = v < 0 ? ENC_TILE_AUTO : v;
   }
   {
-    const char* sp = getenv("RNNT_STREAM_PREFIX");
+    const char* sp = dev_env("RNNT_STREAM_PREFIX");
     e->stream_prefix = sp && atoi(sp) != 0;
   }
   if (!r && model) r = pack_model(e, model);
@@ -800,7 +800,7 @@ static int run_flow(rnnt_engine* e, int T, int n_pad, const int32_t* lens, float
   e->flow_up_pending = true;
   HIPCHK(hipMemsetAsync(e->flow_ctr, 0, ((size_t)ns + 2 + 3) / 4 * 16, st));
   static const int big_grid = [] {  // development knob: CUs the big-batch flow launch holds
-    const char* v = getenv("RNNT_ENC_FLOW_GRID");
+    const char* v = dev_env("RNNT_ENC_FLOW_GRID");
     const int g = v ? atoi(v) : 256;
     return g >= 8 && g <= 256 ? g : 256;
   }();
@@ -863,13 +863,7 @@ static int encode_impl(rnnt_engine* e, const EncInput& in, const int32_t* lens, 
         if (tm[i] > thr) m |= 1ull << i;
     return m;
   };
-  // development: RNNT_L4_LAG = 6 runs post_rnn layer 4 one tick later (2t' + 6), on the ticks
-  // without layer 2, so odd and even ticks carry 6400 / 7424 K-bytes of work instead of 8448 / 5376
-#ifndef RNNT_L4_LAG
-#define RNNT_L4_LAG 5
-#endif
-  constexpr int L4_LAG = RNNT_L4_LAG;
-  static_assert(L4_LAG == 5 || L4_LAG == 6, "layer 4 runs after layer 3 of the same stacked frame");
+  constexpr int L4_LAG = 5;  // post_rnn layer 4 at stacked frame t' runs on tick 2t' + 5, right after layer 3
   const int n_ticks = flow_wanted(e, n_pad) ? 0 : std::max(T + 1, 2 * Tp + L4_LAG - 1);
   if (!n_ticks && (r = run_flow(e, T, n_pad, lens, f_out, tiles, st))) return r;
   for (int tau = 0; tau < n_ticks; ++tau) {
@@ -976,6 +970,9 @@ static int decode_core(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
   a.max_iter = Tp * (MAXSYM + 1) + 2;  // every step emits or advances; <= 30 emits per frame
   a.persist_rows = e->persist_rows;
   const int steps = launch_greedy_decode(a, e->host_flags, e->poll_ev, st, reset);
+  if (steps == -2)  // dec_persist_kernel needs its 48 + nj workgroups co-resident (rnnt_engine_set_decode_persist)
+    return fail(RNNT_EDEVICE, "persistent decode timed out: its workgroups were not all resident (other kernels held "
+                              "the CUs); turn the persistent tail off or give the engine the GPU");
   if (steps < 0) return fail(RNNT_EDEVICE, "greedy launch failed");
   e->decode_steps += steps;
   if (e->prof) e->ev_dec.push_back({ev0, ev1, new_event(st)});

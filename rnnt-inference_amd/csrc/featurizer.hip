@@ -475,7 +475,7 @@ static size_t own_cu_lds_bytes(int device) {
     return 0;
   hipFuncAttributes fa{};
   if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fz_logmel_kernel)) != hipSuccess) return 0;
-  // more than half of what is left: a second workgroup of any kernel cannot fit beside it
+  // all of what is left (any amount over half would do): no workgroup of another kernel fits beside it
   const size_t left = (size_t)per_cu > fa.sharedSizeBytes ? (size_t)per_cu - fa.sharedSizeBytes : 0;
   if (left == 0) return 0;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fz_logmel_kernel),

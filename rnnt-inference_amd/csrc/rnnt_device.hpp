@@ -9,9 +9,22 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 
 namespace rnnt {
+
+// Development knobs (the A/B sweeps of MEASUREMENTS.md) are read from the environment only in the
+// build_dev variants (tools/build_variants.sh compiles with -DRNNT_DEV_KNOBS); the product library
+// ignores them and runs its measured defaults.
+inline const char* dev_env(const char* name) {
+#ifdef RNNT_DEV_KNOBS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // ---- host helpers shared by the launchers and the C ABI
 // Every entry point runs on its engine's device and gives the caller's current device back.

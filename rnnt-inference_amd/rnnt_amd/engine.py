@@ -221,8 +221,10 @@ class Engine:
         _lib.check(self._lib.rnnt_engine_set_tile(self._h, str(tile).encode()), "rnnt_engine_set_tile")
 
     def set_decode_persist(self, rows):
-        """Run a decode call's last steps, once at most `rows` (1..64) rows are live, as one
-        persistent launch (rnnt_engine_set_decode_persist; 0 = off); tokens are identical."""
+        """Run a decode call's last steps, once at most `rows` (1..512; 0 = off) rows are live, as one
+        persistent launch (rnnt_engine_set_decode_persist); tokens are identical.  The launch needs all
+        its 48 + (joint row groups) workgroups resident at once: beside other engines' kernels a wait can
+        time out, and the call then fails with "persistent decode timed out"."""
         _lib.check(self._lib.rnnt_engine_set_decode_persist(self._h, int(rows)), "rnnt_engine_set_decode_persist")
 
     def stats(self, reset=True):

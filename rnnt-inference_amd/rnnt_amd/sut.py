@@ -244,20 +244,9 @@ class OfflineSUT:
 
     # ---- device hooks (a host-only test stands in for these; tests/test_sut_dist.py)
     def _stream_for(self, eng):
-        import os
         import torch
         if id(eng) not in self._streams:
-            k = int(os.environ.get("RNNT_SUT_ENC_RESERVE", "0"))
-            if k > 0:  # development knob: the encoder off the first k CU slots of every XCD
-                from .engine import PartitionedStream, cu_mask_words
-                ps = PartitionedStream(eng.device, cu_mask_words(k, reserved=False))
-                self._streams[("ps", id(eng))] = ps  # keeps the HIP stream alive
-                self._streams[id(eng)] = ps.stream
-            elif os.environ.get("RNNT_SUT_ENC_PRIORITY", "0") == "1":  # development knob: see _dec_stream_for
-                lo, hi = torch.cuda.Stream.priority_range()
-                self._streams[id(eng)] = torch.cuda.Stream(device=eng.device, priority=min(lo, hi))
-            else:
-                self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
+            self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
         return self._streams[id(eng)]
 
     def _device_scope(self, eng, st):
@@ -281,32 +270,10 @@ class OfflineSUT:
         st.synchronize()
         return res, rl
 
-    def _dec_stream_for(self, eng):
-        """Development knobs: RNNT_SUT_DEC_PRIORITY=1 runs the decode of each engine on a second,
-        high-priority stream; RNNT_SUT_ENC_RESERVE=k (encoder kept off k CU slots per XCD) or
-        RNNT_SUT_ENC_PRIORITY=1 (the encode stream high-priority) run it on a second normal stream.
-        The engine orders its calls across streams by its state event."""
-        import os
-        import torch
-        prio = os.environ.get("RNNT_SUT_DEC_PRIORITY", "0") == "1"
-        if (not prio and int(os.environ.get("RNNT_SUT_ENC_RESERVE", "0")) <= 0
-                and os.environ.get("RNNT_SUT_ENC_PRIORITY", "0") != "1"):
-            return None
-        key = ("dec", id(eng))
-        if key not in self._streams:
-            lo, hi = torch.cuda.Stream.priority_range()
-            self._streams[key] = torch.cuda.Stream(device=eng.device, priority=min(lo, hi) if prio else 0)
-        return self._streams[key]
-
     def _decode(self, eng, st, enc):
         """The greedy decode of the encoded batch -> (lengths int32 [n] host, tokens [n, >=max len] host)."""
         res, rl = enc
-        dst = self._dec_stream_for(eng)
-        if dst is None:
-            eng.decode(res, rl, stream=st)
-        else:
-            eng.decode(res, rl, stream=dst)
-            dst.synchronize()
+        eng.decode(res, rl, stream=st)
         rlh = rl.cpu().numpy()
         return rlh, res[:, : max(1, int(rlh.max()))].cpu().numpy()
 

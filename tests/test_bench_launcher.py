@@ -86,3 +86,18 @@ def test_dumped_responses_equal_across_rank_counts(tmp_path):
     np.savez(bad, **z)
     out = subprocess.run([sys.executable, cmp, bad, one], capture_output=True, text=True, timeout=60)
     assert out.returncode == 1 and json.loads(out.stdout)["mismatched_rows"] == 1
+
+
+def test_eight_ranks_gather_keeps_up_at_full_volume():
+    """bench.py's 8-rank data path at the default query (300000 samples per rank,
+    6144-row batches, dynamic claims) with stand-in responses of the timed workload's volume (~64
+    tokens per sample): rank 0's ResponseStream receives all 2.4M rows, and the whole step -- sort,
+    claims, the stand-ins and the streamed gather -- runs faster than 8 GPUs produce rows
+    (8 x 121k samples/s, BENCH_r05), so the gather cannot bound an 8-GPU step."""
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--mock", "--steps", "2", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=600, env=_env())
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["config"]["query_samples"] == 8 * 300000 and rec["config"]["gathered"] == 8 * 300000
+    assert 50 * 8 * 300000 < rec["tokens_per_query"] < 80 * 8 * 300000
+    assert rec["rows_per_s_gathered"] > 8 * 121000, rec

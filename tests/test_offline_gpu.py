@@ -1,7 +1,9 @@
 """BASELINE config 4 on the GPU: an MLPerf Offline query over a 2513-sample
-LibriSpeech-dev-clean-shaped QSL through the OfflineSUT bench.py runs -- batches of 4096, three
-engines in flight on one GPU pulling from one shared batch list, AssembleSamples fused into the
-encoder's gather-quantize pass, responses completed through one point.
+LibriSpeech-dev-clean-shaped QSL through the OfflineSUT bench.py runs -- batches of 4096 on three
+engines, and bench.py's shipped shape, batches of 6144 on four engines with more batches than
+engines (engines reused, every decode beside a later encode) -- pulling from one shared batch list
+on one GPU, AssembleSamples fused into the encoder's gather-quantize pass, responses completed
+through one point.
 
 Checks: every sample of the query answered once; every QSL sample answered identically wherever
 LoadGen's repetition put it (different batches, engines, row positions); 64+ responses spanning
@@ -22,21 +24,22 @@ def pm():
     return weights.build_model()[0]
 
 
-def test_config4_offline_query(pm, oracle):
-    count, query, batch = 2513, 3 * 4096, 4096
+@pytest.mark.parametrize("batch,n_engines,n_batches", [(4096, 3, 3), (6144, 4, 6)])
+def test_config4_offline_query(pm, oracle, batch, n_engines, n_batches):
+    count, query = 2513, n_batches * batch
     qsl = GpuQSL(synthetic.devclean_lengths(count, seed=4), seed=4, device="cuda")
-    engines = [Engine(pm, device=0, max_batch=batch, max_frames=500) for _ in range(3)]
+    engines = [Engine(pm, device=0, max_batch=batch, max_frames=500) for _ in range(n_engines)]
     try:
         sut = OfflineSUT(engines, qsl, batch_size=batch)
         sut.warmup(iters=1, batch_size=256)  # OfflineSUT::warmup (torch_sut.cpp:124-138): completes nothing
         assert sut.take_completed()[0].size == 0
         ids, idx = dist.query_arrays(count, query)
         batches = make_batches(qsl, ids, idx, batch)
-        assert len(batches) == 3
+        assert len(batches) == n_batches
         sut.issue_batches(batches)
         torch.cuda.synchronize()
-        assert sorted(set(sut.batch_engine)) == [0, 1, 2]
-        assert sut.encode_order == [0, 1, 2]  # one GPU: encodes in batch order, longest batch first
+        assert sorted(set(sut.batch_engine)) == list(range(n_engines))
+        assert sut.encode_order == list(range(n_batches))  # one GPU: encodes in batch order, longest first
         got_ids, lens, toks = sut.take_completed()
     finally:
         for e in engines:
@@ -56,8 +59,9 @@ def test_config4_offline_query(pm, oracle):
         else:
             first[q] = sid
     # the restatement on rows of the longest and the shortest batch and a middle one
-    pick = np.concatenate([b[1][np.linspace(0, len(b[1]) - 1, 24).round().astype(int)] for b in batches])
-    pick_ids = np.concatenate([b[0][np.linspace(0, len(b[0]) - 1, 24).round().astype(int)] for b in batches])
+    chk = [batches[0], batches[len(batches) // 2], batches[-1]]
+    pick = np.concatenate([b[1][np.linspace(0, len(b[1]) - 1, 24).round().astype(int)] for b in chk])
+    pick_ids = np.concatenate([b[0][np.linspace(0, len(b[0]) - 1, 24).round().astype(int)] for b in chk])
     sl = qsl.lengths[pick].astype(np.int32)
     order = np.argsort(-sl, kind="stable")
     pick, pick_ids, sl = pick[order], pick_ids[order], sl[order]

@@ -1,12 +1,14 @@
 #!/bin/bash
 # Development: build variants of the engine library with extra compile flags into build_dev/
-# (git-ignored; selected at run time with RNNT_MI355X_LIB=build_dev/lib_<name>.so).
+# (git-ignored; selected at run time with RNNT_MI355X_LIB=build_dev/lib_<name>.so).  Variants read the
+# development environment knobs (RNNT_ENC_TILE, RNNT_DEC_PERSIST_ROWS, RNNT_DEC_RG, ...: -DRNNT_DEV_KNOBS);
+# the product library does not.
 #   tools/build_variants.sh base "asm0:-DRNNT_FRAG_ASM=0" "stamps:-DRNNT_DEV_STAMPS"
 set -e
 cd "$(dirname "$0")/../rnnt-inference_amd/csrc"
 OUTD=../../build_dev
 mkdir -p $OUTD
-HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w -fno-slp-vectorize -Xclang -target-feature -Xclang -packed-fp32-ops"
+HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w -DRNNT_DEV_KNOBS -fno-slp-vectorize -Xclang -target-feature -Xclang -packed-fp32-ops"
 build() {
   local name=$1; shift
   local objs=""
