@@ -32,8 +32,11 @@ __device__ unsigned long long g_est[1 << 22];
 __device__ unsigned int g_est_n;
 #define EST_MARK(v) v = __builtin_amdgcn_s_memrealtime()
 // record slot i of this tile's 8-word record (thread 0 stores at once: nothing stays live)
+// 16-word records: 0-7 the tile's timeline; 8, 9, 10: shader clocks of the main loop spent at the stage
+// barriers (wait_stage), from a barrier to the end of the stage's MFMA issue, and stages
+#define EST_W 16
 #define EST_PUT(i, v) \
-  if (threadIdx.x == 0 && est_k < (1u << 22) / 8) g_est[8 * est_k + (i)] = (v)
+  if (threadIdx.x == 0 && est_k < (1u << 22) / EST_W) g_est[EST_W * est_k + (i)] = (v)
 #else
 #define EST_MARK(v)
 #define EST_PUT(i, v)
@@ -143,6 +146,10 @@ __device__ __forceinline__ void wait_stage(int later) {
     static_assert(NBUF <= 4, "ring depth");
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * PPS) : "memory");
   }
+  // the same lgkmcnt(0) as a real instruction (0xC07F: lgkmcnt 0, the other counters untouched): the
+  // compiler does not read inline asm, and without it assumes scalar loads from before the loop may
+  // still be outstanding -- its fragment waits then all become lgkmcnt(0) instead of counted ones
+  __builtin_amdgcn_s_waitcnt(0xC07F);
 }
 
 // 16-byte copy-out store: plain, or write-through (WT: `sc1`, the line leaves the XCD's L2 at
@@ -157,6 +164,13 @@ __device__ __forceinline__ void st16(void* base, size_t off, uint4 v) {
   } else {
     *(uint4*)((char*)base + off) = v;
   }
+}
+// a wave-uniform pointer the compiler can prove uniform (a buffer resource built from it then needs no
+// waterfall loop around every access)
+__device__ __forceinline__ void* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 struct NoWait {
   __device__ void operator()() const {}
@@ -183,7 +197,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   }
   EST_PUT(2, st_t0);
 #endif
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR
   const int wm = wave & 3, wn = wave >> 2;
   const int m0 = mt * BM;  // packed gate row base
   const int n0 = nt * BN;  // batch row base
@@ -212,25 +226,23 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   const uint32_t oA0 = rlA * K + gA0, oA1 = rlA * K + gA1;
   const uint32_t oX0 = rlB * a.I + gB0, oX1 = rlB * a.I + gB1;
   const uint32_t oH0 = rlB * H + gB0, oH1 = rlB * H + gB1;
-#ifdef RNNT_ABL_W1  // profiling ablation only (tools/enc_ablate.sh): every gate tile reads tile 0's weights (L2-resident)
-  const int8_t* wbase = a.W;
-#else
   const int8_t* wbase = a.W + (size_t)m0 * K;
-#endif
-#ifdef RNNT_ABL_X1  // profiling ablation only: every batch tile reads tile 0's activations (L2-resident)
-  const int8_t* xbase = a.x;
-  const int8_t* hbase = a.h_in - a.I;
-#else
   const int8_t* xbase = a.x + (size_t)n0 * a.I;
   const int8_t* hbase = a.h_in + (size_t)n0 * H - a.I;  // k >= I indexes h at k - I
-#endif
+  // LDS-DMA through buffer resources (buffer_load_dwordx4 ... lds): wave-uniform bases in SGPRs,
+  // loop-invariant 32-bit lane offsets, the stage's k in soffset.  Unlike global_load_lds (a FLAT
+  // instruction the compiler must assume may also touch LDS through the LGKM counter), these are
+  // plain vector-memory loads to it, so the fragment waits below stay counted (lgkmcnt(N)).
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)wbase, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc((void*)xbase, (short)0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsH = __builtin_amdgcn_make_buffer_rsrc((void*)hbase, (short)0, 0x7ffffff0, 0x00020000);
   auto issueA = [&](int s) __attribute__((always_inline)) {
     const int k = s * 128;
     lds_char* st = lds + (s % NBUF) * STAGE + wave * (C::PA * 1024);
 #pragma unroll
     for (int j = 0; j < C::PA; ++j)
-      __builtin_amdgcn_global_load_lds((glb_void*)(wbase + (size_t)(8 * j) * K + k + ((j & 1) ? oA1 : oA0)),
-                                       (lds_void*)(st + j * 1024), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)(st + j * 1024), 16, (j & 1) ? oA1 : oA0,
+                                               k + 8 * j * K, 0, 0);
   };
   auto issueB = [&](int s) __attribute__((always_inline)) {
     const int k = s * 128;
@@ -238,8 +250,8 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
     if (k < a.I) {
 #pragma unroll
       for (int j = 0; j < C::PB; ++j)
-        __builtin_amdgcn_global_load_lds((glb_void*)(xbase + (size_t)(8 * j) * a.I + k + ((j & 1) ? oX1 : oX0)),
-                                         (lds_void*)(st + j * 1024), 16, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsX, (lds_void*)(st + j * 1024), 16, (j & 1) ? oX1 : oX0,
+                                                 k + 8 * j * a.I, 0, 0);
     } else {
       if (k == a.I) {
         hwait();
@@ -247,24 +259,25 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       }
 #pragma unroll
       for (int j = 0; j < C::PB; ++j)
-        __builtin_amdgcn_global_load_lds((glb_void*)(hbase + (size_t)(8 * j) * H + k + ((j & 1) ? oH1 : oH0)),
-                                         (lds_void*)(st + j * 1024), 16, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsH, (lds_void*)(st + j * 1024), 16, (j & 1) ? oH1 : oH0,
+                                                 k + 8 * j * H, 0, 0);
     }
   };
   // the tile's fp16 cell state (BN rows x CROW bytes), DMA'd into the buffer the last stage does
   // not occupy once its reads are retired; piece p, lane l: row p (64 / CPR) + l / CPR, chunk
   // (l % CPR) ^ (row % CPR) at slot l % CPR (cimg_off: 2-way instead of 8-way epilogue conflicts)
   const int cbuf = (nS % NBUF) * STAGE;
+  const __amdgpu_buffer_rsrc_t rsC =
+      __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.c + (size_t)n0 * H + (m0 >> 2)), (short)0, 0x7ffffff0, 0x00020000);
   auto issue_c = [&]() __attribute__((always_inline)) {
     constexpr int RPP = 64 / C::CPR, NPC = C::CPIECES >= NWAVE ? C::CPIECES / NWAVE : 1;
     const int cr = lane / C::CPR, cc = lane % C::CPR;
-    const uint16_t* cb = a.c + (size_t)n0 * H + (m0 >> 2) + (cc ^ (cr & (C::CPR - 1))) * 8;
+    const uint32_t vo = (uint32_t)(cr * H + (cc ^ (cr & (C::CPR - 1))) * 8) * 2;  // bytes
 #pragma unroll
     for (int pc = 0; pc < NPC; ++pc) {
       const int p = wave * NPC + pc;
       if (C::CPIECES < NWAVE && p >= C::CPIECES) break;  // wave-uniform
-      __builtin_amdgcn_global_load_lds((glb_void*)(cb + (size_t)(RPP * p + cr) * H), (lds_void*)(lds + cbuf + p * 1024),
-                                       16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, (lds_void*)(lds + cbuf + p * 1024), 16, vo, RPP * p * H * 2, 0, 0);
     }
   };
 
@@ -293,24 +306,50 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   EST_PUT(3, __builtin_amdgcn_s_memrealtime());
   EST_PUT(6, WT ? st_t1 : __builtin_amdgcn_s_memtime());  // flow: its input frame was ready
 #endif
+#ifdef RNNT_DEV_STAMPS
+  unsigned long long est_wait = 0, est_work = 0;
+#endif
   for (int s = 0; s < nS; ++s) {
     // this wave's DMA of stage s has landed (only later stages' pieces may be outstanding) and
     // its LDS reads are drained; after the barrier every wave's has, and every wave is done
     // reading the buffer stage s+NBUF-1 refills
+#ifdef RNNT_DEV_STAMPS
+    unsigned long long w0, w1;  // no LDS read is outstanding here (the stage's last MFMAs waited for all)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w0)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     wait_stage<C::PA + C::PB, NBUF>(nS - 1 - s);
-    if (s + NBUF - 1 < nS) issueA(s + NBUF - 1);
-#ifndef RNNT_ABL_NOC  // profiling ablation only (tools/enc_ablate.sh): the cell state neither read nor written
-    else if (s == nS - 1) issue_c();
+#ifdef RNNT_DEV_STAMPS
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w1)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    est_wait += w1 - w0;
 #endif
     const int8_t* st = smem + (s % NBUF) * STAGE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int cs = ((kk * 4 + q) ^ sw) << 4;
+      // fragment reads in the order the MFMAs consume them (A0, all B, then A1..): LDS returns in
+      // order, so the first MFMA waits for two reads instead of all of them
       v4i fra[WMT], frb[WNT];
-#pragma unroll
-      for (int i = 0; i < WMT; ++i) fra[i] = *(const v4i*)(st + fa0 + cs + i * 2048);
+      fra[0] = *(const v4i*)(st + fa0 + cs);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < WNT; ++j) frb[j] = *(const v4i*)(st + fb0 + cs + j * 2048);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 1; i < WMT; ++i) fra[i] = *(const v4i*)(st + fa0 + cs + i * 2048);
+      __builtin_amdgcn_sched_barrier(0);
+      // the next stage's DMA is issued while these reads are in flight: A after stage s's first
+      // reads, B after its second k step's (the B half lands half a stage later, as measured best)
+      if (kk == 0) {
+        if (s + NBUF - 1 < nS) issueA(s + NBUF - 1);
+        else if (s == nS - 1) issue_c();
+      } else if (s + NBUF - 1 < nS) {
+        issueB(s + NBUF - 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < WMT; ++i)
@@ -318,12 +357,21 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
         for (int j = 0; j < WNT; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fra[i], frb[j], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (kk == 0 && s + NBUF - 1 < nS) {
-        issueB(s + NBUF - 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
     }
+#ifdef RNNT_DEV_STAMPS
+    {
+      unsigned long long w2;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(w2)::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+      est_work += w2 - w1;
+    }
+#endif
   }
+#ifdef RNNT_DEV_STAMPS
+  EST_PUT(8, est_wait);
+  EST_PUT(9, est_work);
+  EST_PUT(10, (unsigned long long)nS);
+#endif
   // the cell-state DMA has landed for every wave, all fragment reads are done
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #ifdef RNNT_DEV_STAMPS
@@ -371,10 +419,6 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
       yb[i] = q8_biased(hh * outs);
     }
     const uint32_t hq = pack_q8(hb[0], hb[1], hb[2], hb[3]), yq = pack_q8(yb[0], yb[1], yb[2], yb[3]);
-#ifdef RNNT_ABL_NOIMG  // profiling ablation only (tools/enc_ablate.sh): results kept live, no LDS image stores
-    asm volatile("" ::"v"(hq), "v"(yq), "v"(cw[0]), "v"(cw[1]));
-    continue;
-#endif
     if (WMT == 4) {
       *(uint2*)(smem + cbuf + cimg_off<C::CROW>(r, ul * 2)) = uint2{cw[0], cw[1]};
       *(uint32_t*)(hs + r * HP + ul) = hq;
@@ -414,9 +458,7 @@ __device__ __forceinline__ void lstm_i8_step(const EncStepArgs& a, int mt, int n
   for (int it = 0; it < (BN * C::CPR + NWAVE * 64 - 1) / (NWAVE * 64); ++it) {  // c (and bf16 f): BN rows x CROW bytes
     const int idx = it * NWAVE * 64 + tid, r = idx / C::CPR, ch = idx % C::CPR;
     if ((BN * C::CPR) % (NWAVE * 64) != 0 && idx >= BN * C::CPR) break;
-#ifndef RNNT_ABL_NOC
     st16<WT>(a.c, ((size_t)(n0 + r) * H + um + ch * 8) * 2, *(const uint4*)(smem + cbuf + cimg_off<C::CROW>(r, ch * 16)));
-#endif
     if (a.mode == ENC_OUT_FINAL)  // read after the launch only: plain
       *(uint4*)(a.fbf + (size_t)(n0 + r) * H + um + ch * 8) = *(const uint4*)(ys + cimg_off<C::CROW>(r, ch * 16));
   }
@@ -706,9 +748,9 @@ int launch_lstm_i8_tick(const EncTickArgs& a, hipStream_t st, int forced) {
 extern "C" int rnnt_dev_read_enc_stamps(unsigned long long* out, int max_records) {
   unsigned int n = 0;
   if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(rnnt::g_est_n), sizeof(n)) != hipSuccess) return -1;
-  if (n > (1u << 22) / 8) n = (1u << 22) / 8;
+  if (n > (1u << 22) / EST_W) n = (1u << 22) / EST_W;
   if ((int)n > max_records) n = max_records;
-  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_est), (size_t)n * 8 * 8) != hipSuccess) return -1;
+  if (n && hipMemcpyFromSymbol(out, HIP_SYMBOL(rnnt::g_est), (size_t)n * EST_W * 8) != hipSuccess) return -1;
   const unsigned int z = 0;
   if (hipMemcpyToSymbol(HIP_SYMBOL(rnnt::g_est_n), &z, sizeof(z)) != hipSuccess) return -1;
   return (int)n;

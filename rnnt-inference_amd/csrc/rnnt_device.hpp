@@ -110,9 +110,6 @@ __device__ __forceinline__ float det_tanh(float x) {
 constexpr int ENC_TAB_N = 2048;
 __device__ __forceinline__ float act_sig_t(const float2* __restrict__ tab, float t) {
   t = __builtin_amdgcn_fmed3f(t, 0.0f, 2047.9998f);  // = min(max(t, 0), 2047.9998) for finite t
-#ifdef RNNT_ABL_NOTAB
-  return __builtin_fmaf(t, 4.8828125e-4f, 0.0f);  // profiling ablation only (tools/enc_ablate.sh): no table read, wrong values
-#endif
   const float2 e = tab[(int)t];
   return __builtin_fmaf(e.y, t, e.x);
 }

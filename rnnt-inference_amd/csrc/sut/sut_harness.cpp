@@ -19,7 +19,9 @@
 //                    [--batch B] [--split-len L] [--response R] [--pro-batch P] [--warmup W] [--intra C]
 //                    --out F
 // --feats: fp32 [sum(lens)][240], the samples' frames back to back; --lens: int32 [N]; --query: int32 QSL
-// indices (default 0..N-1).  Prints one JSON line.
+// indices (default 0..N-1).  --pinned 1: each instance assembles its batches into a reused pinned buffer
+// (a SUT choice the reference does not make; the model then DMAs the batch as it is instead of packing
+// it).  Prints one JSON line.
 #include <link.h>
 #include <limits.h>
 #include <stdlib.h>
@@ -72,6 +74,7 @@ int hip_runtimes() {
 
 // The QSL: every sample's [len][240] frames in host memory (LoadSamplesToRam).
 struct Qsl {
+  bool pinned = false;  // assemble into pinned host memory (--pinned 1)
   std::vector<float> feats;
   std::vector<int32_t> lens;
   std::vector<int64_t> first;  // first frame row of each sample
@@ -92,7 +95,16 @@ struct Qsl {
     at::Tensor x;
     if (buf) {
       const int64_t need = (int64_t)T * padded * C;
-      if (!buf->defined() || buf->numel() < need) *buf = at::empty({std::max<int64_t>(need, 1)}, at::kFloat);
+      if (!buf->defined() || buf->numel() < need) {
+        if (pinned) {  // a SUT assembling into pinned memory: the model DMAs the batch as it is
+          void* p = nullptr;
+          if (hipHostMalloc(&p, (size_t)std::max<int64_t>(need, 1) * sizeof(float), hipHostMallocDefault) != hipSuccess)
+            throw std::runtime_error("hipHostMalloc of the assembly buffer failed");
+          *buf = at::from_blob(p, {std::max<int64_t>(need, 1)}, [](void* q) { (void)hipHostFree(q); }, at::kFloat);
+        } else {
+          *buf = at::empty({std::max<int64_t>(need, 1)}, at::kFloat);
+        }
+      }
       x = buf->narrow(0, 0, need).view({T, padded, C});
     } else {
       x = at::zeros({T, padded, C}, at::kFloat);
@@ -165,7 +177,8 @@ struct Args {
 int usage(const char* argv0) {
   std::fprintf(stderr,
                "usage: %s --engine F --feats F --lens F --out F [--query F] [--scenario offline|server] [--threads K]\n"
-               "          [--batch B] [--split-len L] [--response R] [--pro-batch P] [--warmup W] [--intra C] [--progress S]\n",
+               "          [--batch B] [--split-len L] [--response R] [--pro-batch P] [--warmup W] [--intra C] [--progress S]\n"
+               "          [--pinned 0|1]\n",
                argv0);
   return 2;
 }
@@ -303,6 +316,7 @@ int main(int argc, char** argv) {
     if (threads <= 0 || bs <= 0 || (scenario != "offline" && scenario != "server")) return usage(argv[0]);
     if (intra > 0) at::set_num_threads(intra);
     Qsl qsl;
+    qsl.pinned = a.num("pinned", 0) != 0;
     qsl.lens = read_file<int32_t>(a.get("lens"));
     qsl.feats = read_file<float>(a.get("feats"));
     int64_t rows = 0;
@@ -423,7 +437,9 @@ int main(int argc, char** argv) {
     const auto cs = model.stats();
     std::cout << "], \"model_host_seconds\": {\"pack\": " << cs.pack << ", \"copy\": " << cs.copy
               << ", \"turn_wait\": " << cs.turn_wait << ", \"encode\": " << cs.encode << ", \"decode\": " << cs.decode
-              << ", \"encode_calls\": " << cs.calls << ", \"frames\": " << cs.frames << "}}" << std::endl;
+              << ", \"encode_calls\": " << cs.calls << ", \"dense_pinned_calls\": " << cs.dense_calls
+              << ", \"frames\": " << cs.frames << "}, \"pinned_assembly\": " << (qsl.pinned ? "true" : "false") << "}"
+              << std::endl;
     return 0;
   } catch (const std::exception& ex) {
     std::fprintf(stderr, "rnnt_sut_harness: %s\n", ex.what());

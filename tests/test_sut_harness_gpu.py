@@ -75,6 +75,7 @@ def _run(setup, name, env_extra=None, **kw):
 
 @pytest.mark.parametrize("threads,split_len,env", [
     (1, -1, {}),                                 # one instance, whole batches
+    (3, -1, {"pinned": 1}),                      # batches assembled in pinned memory: DMA'd as they are
     (8, 2, {}),                                  # run.sh's Offline shape: split_len 2, which = index & 1
     (4, 2, {"RNNT_ENGINES_PER_GPU": "1"}),       # more instances than engines: leases wait and are reused
     (6, 4, {"RNNT_ENCODE_TURNS": "0"}),          # encoders of one GPU overlapping
@@ -82,8 +83,11 @@ def _run(setup, name, env_extra=None, **kw):
 def test_offline_state_protocol(setup, threads, split_len, env):
     assert os.path.exists(HARNESS), "harness not built (make -C rnnt-inference_amd/csrc)"
     N = len(setup["lens"])
-    summary, got = _run(setup, f"off_{threads}_{split_len}", env, scenario="offline", threads=threads, batch=6,
-                        split_len=split_len, warmup=1 if threads == 8 else 0, intra=2)
+    env = dict(env)
+    pinned = env.pop("pinned", 0)
+    summary, got = _run(setup, f"off_{threads}_{split_len}_{pinned}", env, scenario="offline", threads=threads, batch=6,
+                        split_len=split_len, warmup=1 if threads == 8 else 0, intra=2, pinned=pinned)
+    assert summary["model_host_seconds"]["dense_pinned_calls"] == (summary["batches"] if pinned else 0), summary
     assert summary["responses"] == N and summary["batches"] == -(-N // 6), summary
     assert sorted(got) == list(range(N))
     for i in range(N):

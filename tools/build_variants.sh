@@ -18,6 +18,8 @@ build() {
     $HIPCC $extra "$@" -c $src.hip -o $OUTD/${src}_$name.o &
     objs="$objs $OUTD/${src}_$name.o"
   done
+  g++ -std=c++17 -O2 -fPIC -c crash_report.cpp -o $OUTD/crash_report_$name.o &
+  objs="$objs $OUTD/crash_report_$name.o"
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs -o $OUTD/lib_$name.so
   echo "built $OUTD/lib_$name.so"

@@ -65,9 +65,10 @@ def main():
     rd(None, 0)
     run()
     torch.cuda.synchronize()
-    buf = np.zeros(8 * (1 << 19), np.uint64)
-    n = rd(C.c_void_p(buf.ctypes.data), len(buf) // 8)
-    r = buf[: 8 * n].reshape(n, 8).astype(np.int64)
+    W = 16  # words per tile record (encoder.hip EST_W)
+    buf = np.zeros(W * (1 << 18), np.uint64)
+    n = rd(C.c_void_p(buf.ctypes.data), len(buf) // W)
+    r = buf[: W * n].reshape(n, W).astype(np.int64)
     # HW_ID bits 8-15 (cu_id, sh_id, se_id) + XCC_ID: one value per CU
     cu = ((r[:, 0] >> 40) & 0xFF) | ((r[:, 1] & 0xFF) << 8)
     clk = (r[:, 7] - r[:, 6]).astype(np.float64)  # shader clocks over the main loop (s_memtime)
@@ -125,6 +126,11 @@ def main():
         "dispatch_lag_us_p10_p50_p90": [pct(lag, 10), pct(lag, 50), pct(lag, 90)],
         "main_loop_clock_ghz_p10_p50_p90": [pct(clk / (main_ * 1e3), 10), pct(clk / (main_ * 1e3), 50),
                                             pct(clk / (main_ * 1e3), 90)],
+        # per stage, shader clocks: at the stage barrier (wait for the stage's DMA + the other waves)
+        # and from the barrier to the end of the stage's MFMA issue (fragment waits + issue), wave 0
+        "stage_clk_barrier_p50": pct(r[:, 8] / np.maximum(r[:, 10], 1), 50),
+        "stage_clk_reads_mfma_issue_p50": pct(r[:, 9] / np.maximum(r[:, 10], 1), 50),
+        "stage_clk_total_p50": pct(clk / np.maximum(r[:, 10], 1), 50),
         "tiles_per_cu_slot": int(np.bincount(np.unique(cu, return_inverse=True)[1]).max()),
         "cu_slots": int(len(np.unique(cu))),
     })

@@ -60,7 +60,7 @@ def main():
     rd = e._lib.rnnt_dev_read_enc_stamps
     rd.restype = C.c_int
     rd.argtypes = [C.c_void_p, C.c_int]
-    buf = np.zeros((1 << 19, 8), np.uint64)
+    buf = np.zeros((1 << 18, 16), np.uint64)  # 16-word tile records (encoder.hip EST_W)
     for _ in range(2):
         e.infer(x, ld, lens, res, rl, n=n)
         torch.cuda.synchronize()

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--split-len", type=int, default=-1)
     ap.add_argument("--intra", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pinned", type=int, default=0, help="1: the harness assembles batches in pinned memory")
     ap.add_argument("--compare", default=None)
     ap.add_argument("--workdir", default=None)
     args = ap.parse_args()
@@ -57,7 +58,7 @@ def main():
     cmd = [HARNESS, "--engine", eng, "--feats", os.path.join(work, "feats.bin"), "--lens", os.path.join(work, "lens.bin"),
            "--query", os.path.join(work, "query.bin"), "--scenario", "offline", "--threads", str(args.threads),
            "--batch", str(args.batch), "--split-len", str(args.split_len), "--intra", str(args.intra),
-           "--warmup", str(args.warmup), "--out", out]
+           "--warmup", str(args.warmup), "--pinned", str(args.pinned), "--out", out]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)  # progress lines pass through on stderr
     if r.returncode != 0:
         sys.exit(r.returncode)
