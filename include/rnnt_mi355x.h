@@ -338,6 +338,10 @@ typedef struct {
 int rnnt_featurizer_create(const rnnt_featurizer_config* cfg, const float* window, const float* fb, int device,
                            rnnt_featurizer** out);
 void rnnt_featurizer_destroy(rnnt_featurizer* f);
+/* The same from the processor file tools/export_model.py --processor-file writes (the RNNTMI01
+ * container: fz_config fp32 [11] = the config fields in order, fz_window fp32 [win_length], fz_fb fp32
+ * [nfilt][n_fft/2+1]); replaces torch::jit::load of the TorchScript processor (rnnt_processor.hpp:17-22). */
+int rnnt_featurizer_create_from_file(const char* path, int device, rnnt_featurizer** out);
 /* Dynamic LDS each fz_logmel workgroup requests so that it owns its CU (environment RNNT_FZ_OWN_CU=1 at
  * create; 0 = off, the default).  A fallback guard beside the shipped one (no packed FP32 in any
  * kernel); no reference counterpart. */

@@ -464,29 +464,31 @@ struct PkEntry {
 static_assert(sizeof(PkEntry) == 48 + 8 + 32 + 16, "packed entry layout");
 }  // namespace
 
-extern "C" int rnnt_engine_create_from_file(const char* path, int device, const rnnt_opts* opts, rnnt_engine** out) {
-  if (!path || !out) return fail(RNNT_EINVAL, "null argument");
-  *out = nullptr;
-  FILE* fp = fopen(path, "rb");
-  if (!fp) return fail(RNNT_EINVAL, std::string("cannot open ") + path);
+// the container read into memory, entries looked up by name with type / shape / extent checked
+struct PackFile {
   std::vector<char> buf;
-  {
+  std::vector<PkEntry> ents;
+  std::string where;
+  int load(const char* path) {
+    FILE* fp = fopen(path, "rb");
+    if (!fp) return fail(RNNT_EINVAL, std::string("cannot open ") + path);
     char tmp[1 << 16];
     size_t k;
     while ((k = fread(tmp, 1, sizeof(tmp), fp)) > 0) buf.insert(buf.end(), tmp, tmp + k);
     fclose(fp);
+    where = std::string(path) + ": ";
+    if (buf.size() < 16 || memcmp(buf.data(), "RNNTMI01", 8) != 0) return fail(RNNT_EINVAL, where + "not an RNNTMI01 file");
+    uint32_t version = 0, count = 0;
+    memcpy(&version, buf.data() + 8, 4);
+    memcpy(&count, buf.data() + 12, 4);
+    if (version != 1 || count > 256 || 16 + (size_t)count * sizeof(PkEntry) > buf.size())
+      return fail(RNNT_EINVAL, where + "bad header");
+    ents.resize(count);
+    memcpy(ents.data(), buf.data() + 16, count * sizeof(PkEntry));
+    return 0;
   }
-  const std::string where = std::string(path) + ": ";
-  if (buf.size() < 16 || memcmp(buf.data(), "RNNTMI01", 8) != 0) return fail(RNNT_EINVAL, where + "not an RNNTMI01 file");
-  uint32_t version = 0, count = 0;
-  memcpy(&version, buf.data() + 8, 4);
-  memcpy(&count, buf.data() + 12, 4);
-  if (version != 1 || count > 256 || 16 + (size_t)count * sizeof(PkEntry) > buf.size())
-    return fail(RNNT_EINVAL, where + "bad header");
-  std::vector<PkEntry> ents(count);
-  memcpy(ents.data(), buf.data() + 16, count * sizeof(PkEntry));
-  // name -> (data, dtype, element count), every entry checked against the file size
-  auto find = [&](const std::string& name, uint32_t dtype, uint64_t elems, const void** ptr) -> int {
+  // name -> data (dtype 0 int8, 1 fp32, 2 bf16 bits; `elems` elements)
+  int find(const std::string& name, uint32_t dtype, uint64_t elems, const void** ptr) const {
     for (const PkEntry& en : ents) {
       if (strncmp(en.name, name.c_str(), sizeof(en.name)) != 0) continue;
       uint64_t n = 1;
@@ -499,6 +501,16 @@ extern "C" int rnnt_engine_create_from_file(const char* path, int device, const 
       return 0;
     }
     return fail(RNNT_EINVAL, where + "missing entry " + name);
+  }
+};
+
+extern "C" int rnnt_engine_create_from_file(const char* path, int device, const rnnt_opts* opts, rnnt_engine** out) {
+  if (!path || !out) return fail(RNNT_EINVAL, "null argument");
+  *out = nullptr;
+  PackFile pf;
+  if (int r0 = pf.load(path)) return r0;
+  auto find = [&](const std::string& name, uint32_t dtype, uint64_t elems, const void** ptr) {
+    return pf.find(name, dtype, elems, ptr);
   };
   rnnt_model_desc d{};
   int r = 0;
@@ -536,6 +548,37 @@ extern "C" int rnnt_engine_create_from_file(const char* path, int device, const 
   // typed pointers into the image are aligned: the vector's storage comes from operator new
   // (>= 16-byte aligned) and every entry offset is a multiple of 64
   return rnnt_engine_create(&d, device, opts, out);
+}
+
+// The audio processor's file (tools/export_model.py --processor-file, rnnt_amd.featurizer.save_processor_file):
+// fz_config fp32 [11] (the rnnt_featurizer_config fields in order), fz_window fp32 [win_length],
+// fz_fb fp32 [nfilt][n_fft/2+1].  Replaces torch::jit::load of the TorchScript processor
+// (csrc/rnnt_processor.hpp:17-22).
+extern "C" int rnnt_featurizer_create_from_file(const char* path, int device, rnnt_featurizer** out) {
+  if (!path || !out) return fail(RNNT_EINVAL, "null argument");
+  *out = nullptr;
+  PackFile pf;
+  if (int r = pf.load(path)) return r;
+  const void* p = nullptr;
+  if (int r = pf.find("fz_config", 1, 11, &p)) return r;
+  const float* c = (const float*)p;
+  rnnt_featurizer_config cfg{};
+  cfg.sample_rate = (int)c[0];
+  cfg.n_fft = (int)c[1];
+  cfg.win_length = (int)c[2];
+  cfg.hop_length = (int)c[3];
+  cfg.nfilt = (int)c[4];
+  cfg.frame_splicing = (int)c[5];
+  cfg.pad_out_feat = (int)c[6];
+  cfg.preemph = c[7];
+  cfg.dither = c[8];
+  cfg.log_guard = c[9];
+  cfg.norm_eps = c[10];
+  const void* win = nullptr;
+  const void* fb = nullptr;
+  if (int r = pf.find("fz_window", 1, (uint64_t)cfg.win_length, &win)) return r;
+  if (int r = pf.find("fz_fb", 1, (uint64_t)cfg.nfilt * (cfg.n_fft / 2 + 1), &fb)) return r;
+  return rnnt_featurizer_create(&cfg, (const float*)win, (const float*)fb, device, out);
 }
 
 // ---- small utility kernels

@@ -428,8 +428,32 @@ class TorchModel {
   // back from offsets[i], only the 240 real channels: AssembleSamples leaves channels 240..255 zero and
   // the engine's layer-0 weights there are zero), one copy to the device, then the encode -- after the
   // GPU's earlier encoders (turns in arrival order).
-  void run_encode(const Lease& ls, const std::vector<mi355x::Chunk>& chunks, int n, int rows, const int32_t* reset) {
+  // split_len chunks that are consecutive slices of one contiguous batch (State::update's torch::split of f,
+  // metadata.cpp:63) -> that batch as one chunk (a non-owning view; the chunks keep it alive for the call)
+  static bool merge_adjacent(const std::vector<mi355x::Chunk>& chunks, std::vector<mi355x::Chunk>& out) {
+    if (chunks.size() < 2) return false;
+    const at::Tensor& f0 = chunks[0].f;
+    if (f0.dim() != 3 || f0.scalar_type() != at::kFloat || !f0.is_contiguous() || !f0.device().is_cpu()) return false;
+    const int64_t R = f0.size(1), C = f0.size(2);
+    const float* next = f0.data_ptr<float>();
+    int64_t T = 0;
+    at::Tensor lens = at::zeros_like(chunks[0].lens.to(at::kCPU, at::kInt));
+    for (const auto& c : chunks) {
+      if (c.f.dim() != 3 || c.f.scalar_type() != at::kFloat || !c.f.is_contiguous() || !c.f.device().is_cpu() ||
+          c.f.size(1) != R || c.f.size(2) != C || c.f.data_ptr<float>() != next)
+        return false;
+      next += c.f.size(0) * R * C;
+      T += c.f.size(0);
+      lens += c.lens.to(at::kCPU, at::kInt);
+    }
+    out.push_back({at::from_blob(f0.data_ptr<float>(), {T, R, C}, at::kFloat), lens});
+    return true;
+  }
+
+  void run_encode(const Lease& ls, const std::vector<mi355x::Chunk>& chunks_in, int n, int rows, const int32_t* reset) {
     mi355x::Slot& s = *ls.slot;
+    std::vector<mi355x::Chunk> merged;
+    const std::vector<mi355x::Chunk>& chunks = !reset && merge_adjacent(chunks_in, merged) ? merged : chunks_in;
     std::vector<at::Tensor> f(chunks.size()), cl(chunks.size());
     for (size_t c = 0; c < chunks.size(); ++c) {
       f[c] = chunks[c].f.to(at::kCPU, at::kFloat).contiguous();

@@ -21,7 +21,10 @@
 // --feats: fp32 [sum(lens)][240], the samples' frames back to back; --lens: int32 [N]; --query: int32 QSL
 // indices (default 0..N-1).  --pinned 1: each instance assembles its batches into a reused pinned buffer
 // (a SUT choice the reference does not make; the model then DMAs the batch as it is instead of packing
-// it).  Prints one JSON line.
+// it).  WAV mode (--processor F --wav F --wav-lens F: fp32 16 kHz audio back to back, int32 samples per
+// utterance): AssembleSamples gathers audio and the AudioProcessor drop-in (rnnt_processor_mi355x.hpp)
+// featurizes each batch on the GPU before the model, as the SUT does with WAV=true (torch_sut.cpp:192-200,
+// 442-461).  Prints one JSON line.
 #include <link.h>
 #include <limits.h>
 #include <stdlib.h>
@@ -39,6 +42,7 @@
 #include <thread>
 
 #include "rnnt_model_mi355x.hpp"
+#include "rnnt_processor_mi355x.hpp"
 #include "sut_state.hpp"
 
 namespace {
@@ -75,6 +79,23 @@ int hip_runtimes() {
 // The QSL: every sample's [len][240] frames in host memory (LoadSamplesToRam).
 struct Qsl {
   bool pinned = false;  // assemble into pinned host memory (--pinned 1)
+  // WAV mode (--wav / --wav-lens / --processor): each sample's 16 kHz audio back to back
+  std::vector<float> wav;
+  std::vector<int32_t> wav_lens;
+  std::vector<int64_t> wav_first;
+  // RNNTQuerySampleLibrary::AssembleSamples, processor mode (rnnt_qsl.cpp:163-179): zeros [N][max len] + audio
+  std::pair<at::Tensor, at::Tensor> assemble_wav(const std::vector<int64_t>& idx) const {
+    const int64_t n = (int64_t)idx.size();
+    int32_t L = 1;
+    for (int64_t i : idx) L = std::max(L, wav_lens[i]);
+    at::Tensor x = at::zeros({n, L}, at::kFloat);
+    at::Tensor xl = at::empty({n}, at::kInt);
+    for (int64_t i = 0; i < n; ++i) {
+      xl.data_ptr<int32_t>()[i] = wav_lens[idx[i]];
+      std::memcpy(x.data_ptr<float>() + i * L, wav.data() + wav_first[idx[i]], sizeof(float) * wav_lens[idx[i]]);
+    }
+    return {x, xl};
+  }
   std::vector<float> feats;
   std::vector<int32_t> lens;
   std::vector<int64_t> first;  // first frame row of each sample
@@ -178,12 +199,15 @@ int usage(const char* argv0) {
   std::fprintf(stderr,
                "usage: %s --engine F --feats F --lens F --out F [--query F] [--scenario offline|server] [--threads K]\n"
                "          [--batch B] [--split-len L] [--response R] [--pro-batch P] [--warmup W] [--intra C] [--progress S]\n"
-               "          [--pinned 0|1]\n",
+               "          [--pinned 0|1]\n"
+               "   or (WAV=true) --wav F --wav-lens F --processor F in place of --feats / --lens\n",
                argv0);
   return 2;
 }
 
 using Clock = std::chrono::steady_clock;
+
+rnnt::models::AudioProcessor* g_processor = nullptr;  // WAV mode (--processor)
 
 // the first exception of any instance thread, rethrown by main (an escaping one would terminate)
 std::mutex g_err_mu;
@@ -211,8 +235,15 @@ void offline_instance(int index, rnnt::models::TorchModel& model, const Qsl& qsl
   at::Tensor xbuf;
   for (int i = 0; i < warmup; ++i) {  // OfflineSUT::warmup (:124-138), GenerateDummySamples (rnnt_qsl.cpp:136-147)
     rnnt::State ws(bs, split_len);
-    at::Tensor x = at::randn({bs, rnnt::dims::kPaddedInput, rnnt::dims::kMaxFeaLen}).permute({2, 0, 1}).contiguous();
-    at::Tensor x_lens = at::full({bs}, rnnt::dims::kMaxFeaLen, at::kInt);
+    at::Tensor x, x_lens;
+    if (g_processor) {
+      at::Tensor w = at::randn({bs, 240000}), wl = at::full({bs}, 240000, at::kInt);  // MAX_WAV_LEN
+      std::tie(x, x_lens) = g_processor->forward(which, w, wl, /*pad_batch_size=*/true);
+      x = x.permute({2, 0, 1}).contiguous();
+    } else {
+      x = at::randn({bs, rnnt::dims::kPaddedInput, rnnt::dims::kMaxFeaLen}).permute({2, 0, 1}).contiguous();
+      x_lens = at::full({bs}, rnnt::dims::kMaxFeaLen, at::kInt);
+    }
     ws.update(x, x_lens, split_len);
     model.forward(which, ws);
   }
@@ -233,7 +264,14 @@ void offline_instance(int index, rnnt::models::TorchModel& model, const Qsl& qsl
     std::vector<int64_t> idx(samples.size());
     for (size_t i = 0; i < samples.size(); ++i) idx[i] = (int64_t)samples[i].index;
     const int n = (int)samples.size();
-    auto [x, x_lens] = qsl.assemble(idx, (n + 31) / 32 * 32, &xbuf);
+    at::Tensor x, x_lens;
+    if (g_processor) {  // torch_sut.cpp:192-200: AssembleSamples (audio), processor, permute to [T][N][C]
+      auto [w, wl] = qsl.assemble_wav(idx);
+      std::tie(x, x_lens) = g_processor->forward(which, w, wl, /*pad_batch_size=*/true);
+      x = x.permute({2, 0, 1}).contiguous();
+    } else {
+      std::tie(x, x_lens) = qsl.assemble(idx, (n + 31) / 32 * 32, &xbuf);
+    }
     state.update(x, x_lens, split_len, n);
     model.encode(which, state);
     model.decode(which, state);
@@ -307,7 +345,9 @@ int main(int argc, char** argv) {
     if (k.rfind("--", 0) != 0 || i + 1 >= argc) return usage(argv[0]);
     a.kv[k.substr(2)] = argv[++i];
   }
-  if (a.get("engine").empty() || a.get("feats").empty() || a.get("lens").empty() || a.get("out").empty())
+  const bool wav_mode = !a.get("processor").empty();
+  if (a.get("engine").empty() || a.get("out").empty() ||
+      (wav_mode ? a.get("wav").empty() || a.get("wav-lens").empty() : a.get("feats").empty() || a.get("lens").empty()))
     return usage(argv[0]);
   try {
     const std::string scenario = a.get("scenario", "offline");
@@ -317,16 +357,30 @@ int main(int argc, char** argv) {
     if (intra > 0) at::set_num_threads(intra);
     Qsl qsl;
     qsl.pinned = a.num("pinned", 0) != 0;
-    qsl.lens = read_file<int32_t>(a.get("lens"));
-    qsl.feats = read_file<float>(a.get("feats"));
-    int64_t rows = 0;
-    for (int32_t l : qsl.lens) {
-      if (l < 0 || l > rnnt::dims::kMaxFeaLen) throw std::runtime_error("sample length out of range");
-      qsl.first.push_back(rows);
-      rows += l;
-      qsl.max_len = std::max(qsl.max_len, l);
+    if (wav_mode) {  // the sort key is the feature length the processor will produce
+      qsl.wav_lens = read_file<int32_t>(a.get("wav-lens"));
+      qsl.wav = read_file<float>(a.get("wav"));
+      int64_t at_ = 0;
+      for (int32_t l : qsl.wav_lens) {
+        if (l < 0) throw std::runtime_error("sample length out of range");
+        qsl.wav_first.push_back(at_);
+        at_ += l;
+        qsl.lens.push_back((int32_t)rnnt_featurizer_frames(l));
+        qsl.first.push_back(0);
+      }
+      if ((int64_t)qsl.wav.size() != at_) throw std::runtime_error("wav does not match wav-lens");
+    } else {
+      qsl.lens = read_file<int32_t>(a.get("lens"));
+      qsl.feats = read_file<float>(a.get("feats"));
+      int64_t rows = 0;
+      for (int32_t l : qsl.lens) {
+        if (l < 0 || l > rnnt::dims::kMaxFeaLen) throw std::runtime_error("sample length out of range");
+        qsl.first.push_back(rows);
+        rows += l;
+        qsl.max_len = std::max(qsl.max_len, l);
+      }
+      if ((int64_t)qsl.feats.size() != rows * rnnt::dims::kInput) throw std::runtime_error("feats do not match lens");
     }
-    if ((int64_t)qsl.feats.size() != rows * rnnt::dims::kInput) throw std::runtime_error("feats do not match lens");
     std::vector<int32_t> query;
     if (!a.get("query").empty()) {
       query = read_file<int32_t>(a.get("query"));
@@ -338,6 +392,11 @@ int main(int argc, char** argv) {
       if (q < 0 || q >= (int32_t)qsl.lens.size()) throw std::runtime_error("query index out of range");
 
     rnnt::models::TorchModel model(a.get("engine"));
+    std::unique_ptr<rnnt::models::AudioProcessor> processor;
+    if (wav_mode) {
+      processor = std::make_unique<rnnt::models::AudioProcessor>(a.get("processor"));
+      g_processor = processor.get();
+    }
     Responder resp;
     // progress on stderr every --progress seconds (a long run stays visibly alive)
     const int progress = a.num("progress", 10);
@@ -414,11 +473,19 @@ int main(int argc, char** argv) {
         const size_t n = std::min(query.size() - s0, (size_t)pro_bs);
         std::vector<int64_t> idx(n);
         for (size_t i = 0; i < n; ++i) idx[i] = query[s0 + i];
-        auto [x, x_lens] = qsl.assemble(idx, (int64_t)n);
         std::vector<rnnt::PipelineState::Entry> items;
-        for (size_t i = 0; i < n; ++i)
-          items.emplace_back(rnnt::Sample{(uint64_t)(s0 + i), (uint64_t)idx[i]},
-                             x.narrow(1, (int64_t)i, 1).contiguous(), x_lens.narrow(0, (int64_t)i, 1).clone());
+        if (g_processor) {  // :442-461 with the processor: [N][C][T] features, one sample at a time as [T][1][C]
+          auto [w, wl] = qsl.assemble_wav(idx);
+          auto [f, fl] = g_processor->forward(0, w, wl, /*pad_batch_size=*/false);
+          for (size_t i = 0; i < n; ++i)
+            items.emplace_back(rnnt::Sample{(uint64_t)(s0 + i), (uint64_t)idx[i]},
+                               f.narrow(0, (int64_t)i, 1).permute({2, 0, 1}).contiguous(), fl.narrow(0, (int64_t)i, 1).clone());
+        } else {
+          auto [x, x_lens] = qsl.assemble(idx, (int64_t)n);
+          for (size_t i = 0; i < n; ++i)
+            items.emplace_back(rnnt::Sample{(uint64_t)(s0 + i), (uint64_t)idx[i]},
+                               x.narrow(1, (int64_t)i, 1).contiguous(), x_lens.narrow(0, (int64_t)i, 1).clone());
+        }
         std::lock_guard<std::mutex> l(pmu);
         for (auto& it : items) processed.push_back(std::move(it));
       }

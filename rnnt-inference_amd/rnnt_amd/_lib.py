@@ -56,6 +56,7 @@ _SIGS = {
     "rnnt_featurizer_create": (C.c_int, [C.POINTER(RnntFeaturizerConfig), C.c_void_p, C.c_void_p, C.c_int,
                                          C.POINTER(C.c_void_p)]),
     "rnnt_featurizer_destroy": (None, [C.c_void_p]),
+    "rnnt_featurizer_create_from_file": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
     "rnnt_featurizer_frames": (C.c_int64, [C.c_int64]),
     "rnnt_featurizer_own_cu_lds": (C.c_size_t, [C.c_void_p]),
     "rnnt_featurizer_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,

@@ -72,6 +72,24 @@ def feature_frames(wav_len):
     return int(_lib.lib().rnnt_featurizer_frames(int(wav_len)))
 
 
+def write_processor_file(path, config=None, window=None, fb=None):
+    """The processor file the C++ AudioProcessor drop-in loads (rnnt_featurizer_create_from_file,
+    csrc/sut/rnnt_processor_mi355x.hpp) in place of the reference's TorchScript processor
+    (rnnt_processor.hpp:17-22): the RNNTMI01 container with fz_config (the rnnt_featurizer_config
+    fields in order), fz_window and fz_fb.  Defaults: configs/rnnt.toml [input_eval] (16 kHz, 20 ms
+    hann window, 10 ms stride, n_fft 512, 80 filters, splicing 3, padded to 256 features)."""
+    from .weights import write_pack_file
+    if config is None:
+        config = [16000, 512, 320, 160, 80, 3, 256, 0.97, 1e-5, 1e-20, 1e-12]
+    if window is None:
+        window = make_window("hann", int(config[2]))
+    if fb is None:
+        fb = mel_filterbank(int(config[0]), int(config[1]), int(config[4]), 0.0, config[0] / 2)
+    return write_pack_file(path, {"fz_config": (1, np.asarray(config, np.float32)),
+                                  "fz_window": (1, np.asarray(window, np.float32)),
+                                  "fz_fb": (1, np.asarray(fb, np.float32))})
+
+
 class FilterbankFeatures:
     """features.py:98-270 on the GPU (one native featurizer per instance and device)."""
 
@@ -100,12 +118,20 @@ class FilterbankFeatures:
         self.device = device
         cfg = _lib.RnntFeaturizerConfig(sample_rate, self.n_fft, self.win_length, self.hop_length, nfilt,
                                         frame_splicing, 256, float(preemph or 0.0), float(dither), 1e-20, 1e-12)
+        self.config = cfg
         L = _lib.lib()
         h = C.c_void_p()
         _lib.check(L.rnnt_featurizer_create(C.byref(cfg), self.window.ctypes.data_as(C.c_void_p),
                                             self.fb.ctypes.data_as(C.c_void_p), device, C.byref(h)),
                    "rnnt_featurizer_create")
         self._h = h
+
+    def save_processor_file(self, path):
+        """This featurizer's processor file (write_processor_file)."""
+        c = self.config
+        return write_processor_file(path, [c.sample_rate, c.n_fft, c.win_length, c.hop_length, c.nfilt,
+                                           c.frame_splicing, c.pad_out_feat, c.preemph, c.dither, c.log_guard,
+                                           c.norm_eps], self.window, self.fb)
 
     @classmethod
     def from_config(cls, cfg, log=False):

@@ -299,8 +299,12 @@ def engine_file_arrays(pm):
 def save_engine_file(pm, path):
     """Write the engine model file: magic, u32 version 1, u32 count, count x {char name[48];
     u32 dtype; u32 ndim; u64 shape[4]; u64 offset; u64 nbytes}, then 64-byte aligned data."""
+    return write_pack_file(path, engine_file_arrays(pm))
+
+
+def write_pack_file(path, arrs):
+    """The RNNTMI01 container of save_engine_file: {name: (dtype code, array)}."""
     import struct
-    arrs = engine_file_arrays(pm)
     head = 16 + len(arrs) * 104
     off = (head + 63) // 64 * 64
     ents, blobs = [], []

@@ -120,3 +120,56 @@ def test_server_pipeline_state(setup, threads, batch, split_len, response):
     for pos, i in enumerate(query):
         np.testing.assert_array_equal(got[pos], setup["want"][i], err_msg=f"query position {pos} (sample {i})")
     assert summary["engines_per_gpu"][0] >= threads
+
+
+@pytest.fixture(scope="module")
+def wav_setup(tmp_path_factory, oracle):
+    """WAV=true (launch_sut.sh:53-55): 16 kHz audio, the processor file, and the expected tokens -- the
+    CPU restatement of the model on the features the GPU featurizer makes of each utterance (the same
+    kernels the AudioProcessor drop-in runs; features are per utterance, so batching does not change them)."""
+    import torch
+    from rnnt_amd.featurizer import write_processor_file
+    from rnnt_amd.sut import GpuWavQSL
+    tmp = tmp_path_factory.mktemp("harness_wav")
+    pm, _ = weights.build_model()
+    eng_file = weights.save_engine_file(pm, str(tmp / "rnnt.engine"))
+    proc_file = write_processor_file(str(tmp / "rnnt.processor"))
+    frames = np.random.default_rng(81).integers(8, 90, 26).astype(np.int64)
+    wav_lens = synthetic.wav_lengths_for_frames(frames, seed=81)
+    wavs = synthetic.make_wavs(wav_lens, seed=81)
+    np.concatenate([w.numpy() for w in wavs]).astype(np.float32).tofile(tmp / "wav.bin")
+    wav_lens.astype(np.int32).tofile(tmp / "wav_lens.bin")
+    q = GpuWavQSL([w.cuda() for w in wavs])
+    idx = list(range(len(wavs)))
+    x, _, bl = q.assemble(idx)
+    feats = np.ascontiguousarray(x.cpu().numpy()[:, : len(idx)])
+    fo = oracle.encoder_i8(pm, feats, bl)
+    ro, rlo, _ = oracle.greedy_decode(pm, fo, (bl + 1) // 2, max_res=250 * 30)
+    assert rlo.max() > 3
+    torch.cuda.synchronize()
+    return dict(tmp=tmp, eng=eng_file, proc=proc_file, want=[ro[i, : rlo[i]] for i in idx])
+
+
+@pytest.mark.parametrize("scenario,threads,batch,split_len", [("offline", 4, 8, 2), ("offline", 2, 8, -1),
+                                                              ("server", 2, 8, 8)])
+def test_wav_processor_drop_in(wav_setup, scenario, threads, batch, split_len):
+    """The AudioProcessor drop-in (csrc/sut/rnnt_processor_mi355x.hpp) featurizes each batch on the GPU
+    and hands the SUT [N_out][256][T] features (a view of pinned memory the model DMAs as it is); every
+    payload equals the restatement on the GPU featurizer's features."""
+    s = wav_setup
+    tmp = s["tmp"]
+    out = tmp / f"wav_{scenario}_{threads}_{split_len}.bin"
+    cmd = [HARNESS, "--engine", s["eng"], "--processor", s["proc"], "--wav", str(tmp / "wav.bin"), "--wav-lens",
+           str(tmp / "wav_lens.bin"), "--out", str(out), "--scenario", scenario, "--threads", str(threads),
+           "--batch", str(batch), "--split-len", str(split_len), "--intra", "2", "--warmup", "0"]
+    if scenario == "server":
+        cmd += ["--response", "2", "--pro-batch", "4"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    summary = json.loads(r.stdout.strip().splitlines()[-1])
+    assert summary["bad_res_idx_rows"] == 0 and summary["responses"] == len(s["want"]), summary
+    if scenario == "offline" and split_len < 0:
+        assert summary["model_host_seconds"]["dense_pinned_calls"] == summary["batches"], summary
+    got = _responses(out)
+    for i, w in enumerate(s["want"]):
+        np.testing.assert_array_equal(got[i], w, err_msg=f"sample {i}")

@@ -10,7 +10,8 @@ featurizer output) and "lens" [N]; default: the synthetic calibration batch buil
 --amax: five comma-separated values to skip calibration (e.g. from an earlier export).
 The output (rnnt_amd.weights.save_prepared) is read by rnnt_amd.weights.load_prepared and handed
 to rnnt_amd.engine.Engine; --engine-file also writes the flat container the C ABI loads directly
-(rnnt_engine_create_from_file, for the C++ SUT).  One JSON line (amax, scales, digest) goes to stdout.
+(rnnt_engine_create_from_file, for the C++ SUT) and --processor-file the audio processor's (window +
+filterbank, rnnt_featurizer_create_from_file).  One JSON line (amax, scales, digest) goes to stdout.
 """
 import argparse
 import json
@@ -37,6 +38,8 @@ def main():
     ap.add_argument("--fp32-decoder", action="store_true", help="keep prediction/joint fp32 (enable_bf16 off)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--engine-file", help="also write the C-loadable engine model file (RNNTMI01)")
+    ap.add_argument("--processor-file", help="also write the audio processor file the C++ AudioProcessor drop-in "
+                                             "loads (configs/rnnt.toml [input_eval] geometry; RNNTMI01)")
     args = ap.parse_args()
 
     ckpt = weights.load_checkpoint(args.checkpoint) if args.checkpoint else synthetic.make_checkpoint(args.seed)
@@ -60,6 +63,10 @@ def main():
     if args.engine_file:
         weights.save_engine_file(pm, args.engine_file)
         meta["engine_file"] = args.engine_file
+    if args.processor_file:
+        from rnnt_amd.featurizer import write_processor_file
+        write_processor_file(args.processor_file)
+        meta["processor_file"] = args.processor_file
     print(json.dumps({"out": args.out, "amax": [float(v) for v in amax], "in_scale": [float(v) for v in pm.enc_in_s],
                       "rb_scale": [float(v) for v in pm.enc_rb], **meta}))
 
