@@ -222,7 +222,11 @@ class TorchModel {
     }
     const int rows = (int)state.batch_size_;
     const int n = pipe ? rows : (state.actual_batch_size_ > 0 ? std::min<int>(state.actual_batch_size_, rows) : rows);
-    const int max_frames = pipe ? std::max<int>(state.padded_fea_len_, mi355x::kMaxFeaLen) : mi355x::kMaxFeaLen;
+    // engines hold a multiple of 64 frames, at least MAX_FEA_LEN (the warmup's MAX_WAV_LEN dummy audio makes
+    // 501 frames, rnnt_qsl.cpp:140-141; a PipelineState pads to whole chunks, metadata.cpp:98-102)
+    int64_t frames = pipe ? (int64_t)state.padded_fea_len_ : 0;
+    for (const auto& c : chunks) frames += pipe ? 0 : c.f.size(0);
+    const int max_frames = (int)mi355x::round_up(std::max<int64_t>(frames, mi355x::kMaxFeaLen), 64);
     Lease ls = lease(which, &state, pipe, rows, max_frames, (int)state.max_res_len_);
     try {
       run_encode(ls, chunks, n, rows, pipe ? reset.data() : nullptr);

@@ -79,6 +79,7 @@ def _run(setup, name, env_extra=None, **kw):
     (8, 2, {}),                                  # run.sh's Offline shape: split_len 2, which = index & 1
     (4, 2, {"RNNT_ENGINES_PER_GPU": "1"}),       # more instances than engines: leases wait and are reused
     (6, 4, {"RNNT_ENCODE_TURNS": "0"}),          # encoders of one GPU overlapping
+    (8, 2, {"RNNT_GPUS": "0,0"}),                # two GPU pools (both on device 0): which = 0 / 1 -> one each
 ])
 def test_offline_state_protocol(setup, threads, split_len, env):
     assert os.path.exists(HARNESS), "harness not built (make -C rnnt-inference_amd/csrc)"
@@ -94,6 +95,8 @@ def test_offline_state_protocol(setup, threads, split_len, env):
         np.testing.assert_array_equal(got[i], setup["want"][i], err_msg=f"sample {i}")
     if "RNNT_ENGINES_PER_GPU" in env:
         assert summary["engines_per_gpu"] == [1], summary
+    if "RNNT_GPUS" in env:  # the socket's half of the node's GPUs: both pools served batches
+        assert len(summary["engines_per_gpu"]) == 2 and min(summary["engines_per_gpu"]) > 0, summary
 
 
 def test_offline_odd_split_rejected(setup):

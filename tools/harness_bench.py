@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--intra", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pinned", type=int, default=0, help="1: the harness assembles batches in pinned memory")
+    ap.add_argument("--wav", action="store_true",
+                    help="WAV=true: bench.py --wav's audio QSL in host memory, featurized by the AudioProcessor drop-in")
     ap.add_argument("--compare", default=None)
     ap.add_argument("--workdir", default=None)
     args = ap.parse_args()
@@ -45,17 +47,32 @@ def main():
     work = args.workdir or tempfile.mkdtemp(prefix="rnnt_harness_", dir="/tmp")
     os.makedirs(work, exist_ok=True)
     lens = synthetic.devclean_lengths(args.qsl, seed=4)
-    q = GpuQSL(lens, seed=4, device="cuda:0")  # bench.py's build_qsl: the same features
-    print(f"[harness_bench] QSL {args.qsl} samples, query {args.query}", file=sys.stderr, flush=True)
-    q.feats.cpu().numpy().tofile(os.path.join(work, "feats.bin"))
-    del q
-    torch.cuda.empty_cache()
-    lens.astype(np.int32).tofile(os.path.join(work, "lens.bin"))
+    if args.wav:  # bench.py's build_qsl(wav=True): the same audio
+        from rnnt_amd.featurizer import write_processor_file
+        wav_lens = synthetic.wav_lengths_for_frames(lens, seed=4)
+        wavs = synthetic.make_wavs(wav_lens, seed=4, device="cuda:0")
+        with open(os.path.join(work, "wav.bin"), "wb") as f:
+            for w in wavs:
+                f.write(w.cpu().numpy().astype(np.float32).tobytes())
+        del wavs
+        torch.cuda.empty_cache()
+        wav_lens.astype(np.int32).tofile(os.path.join(work, "wav_lens.bin"))
+        write_processor_file(os.path.join(work, "rnnt.processor"))
+    else:
+        q = GpuQSL(lens, seed=4, device="cuda:0")  # bench.py's build_qsl: the same features
+        print(f"[harness_bench] QSL {args.qsl} samples, query {args.query}", file=sys.stderr, flush=True)
+        q.feats.cpu().numpy().tofile(os.path.join(work, "feats.bin"))
+        del q
+        torch.cuda.empty_cache()
+        lens.astype(np.int32).tofile(os.path.join(work, "lens.bin"))
     (np.arange(args.query, dtype=np.int64) % args.qsl).astype(np.int32).tofile(os.path.join(work, "query.bin"))
     pm, _ = weights.build_model()
     eng = weights.save_engine_file(pm, os.path.join(work, "rnnt.engine"))
     out = os.path.join(work, "responses.bin")
-    cmd = [HARNESS, "--engine", eng, "--feats", os.path.join(work, "feats.bin"), "--lens", os.path.join(work, "lens.bin"),
+    src = (["--processor", os.path.join(work, "rnnt.processor"), "--wav", os.path.join(work, "wav.bin"), "--wav-lens",
+            os.path.join(work, "wav_lens.bin")] if args.wav else
+           ["--feats", os.path.join(work, "feats.bin"), "--lens", os.path.join(work, "lens.bin")])
+    cmd = [HARNESS, "--engine", eng] + src + [
            "--query", os.path.join(work, "query.bin"), "--scenario", "offline", "--threads", str(args.threads),
            "--batch", str(args.batch), "--split-len", str(args.split_len), "--intra", str(args.intra),
            "--warmup", str(args.warmup), "--pinned", str(args.pinned), "--out", out]
@@ -63,7 +80,9 @@ def main():
     if r.returncode != 0:
         sys.exit(r.returncode)
     res = json.loads(r.stdout.strip().splitlines()[-1])
-    res["workload"] = {"qsl": args.qsl, "query_samples": args.query, "features": "bench.py's GpuQSL (seed 4) in host memory",
+    res["workload"] = {"qsl": args.qsl, "query_samples": args.query,
+                       "features": ("bench.py --wav's audio (seed 4) in host memory, AudioProcessor drop-in" if args.wav
+                                    else "bench.py's GpuQSL (seed 4) in host memory"),
                        "rate": "host- and PCIe-inclusive: AssembleSamples on the host, the model's staged copy to HBM"}
     res["intra"] = args.intra
     if args.compare:
