@@ -375,7 +375,6 @@ constexpr int PRED_THREADS = 256;  // 4 waves, one gate tile each: 40 KB of weig
 // fragment) with 24 / 48 row groups -- isolated greedy 69.5 -> 66.7 ms per query vs 16 rows and
 // 48 / 96 groups (64 rows: 82 ms); the joint keeps 16-row tiles (JRT)
 constexpr int DEC_RT = 32;
-constexpr int DEC_SUB = DEC_RT / 16;
 // row groups (grid y) of the prediction / G launches and workgroups of the joint, at most: round-2
 // sweeps of 12-96 / 24-96 / 256-512 measured within +-1.5 %
 constexpr int PRED_ROW_GROUPS = 24;
@@ -420,29 +419,30 @@ struct PredRegs {
   bool wl = false;
 };
 constexpr int pred_xp(int layer) { return (layer ? 2 * P : P) + 16; }
-template <int LAYER, int NW, bool PS>
+template <int LAYER, int NW, bool PS, int RT = DEC_RT>
 __device__ __forceinline__ void dec_pred_body(const DecArgs& a, int parity, const GridXY gxy,
-                                              uint16_t (*X)[pred_xp(LAYER)], int (*ents_all)[DEC_RT], PredRegs<LAYER>& W) {
+                                              uint16_t (*X)[pred_xp(LAYER)], int (*ents_all)[RT], PredRegs<LAYER>& W) {
   constexpr int PRED_THREADS = NW * 64;
   constexpr int KX = LAYER ? 2 * P : P;  // staged k: layer 1 [x | h], layer 0 [h]
-  constexpr int NK = PRED_THREADS / DEC_RT;  // row tiles whose list entries load up front
+  constexpr int NK = PRED_THREADS / RT;  // row tiles whose list entries load up front
+  constexpr int DEC_SUB = RT / 16;
   const DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
   const int* list = s.list + parity * a.Npad;
   // the entries of this workgroup's first NK row tiles load beside the list length (one round
   // trip for all of them; indices past Npad -- XCD rounding, long strides -- are guarded)
-  const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
+  const int i0 = (gxy.y + (tid / RT) * gxy.ny) * RT + tid % RT;
   const int e0 = i0 < a.Npad ? list[i0] : -1;
   const int cnt = s.count[EMIT_N(parity)];
-  const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
+  const int ntiles = (cnt + RT - 1) / RT;
   if (gxy.y >= ntiles) return;
-  ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
+  ents_all[tid / RT][tid % RT] = i0 < cnt ? e0 : -1;
   const int t0 = gxy.x * (PRED_THREADS / 64) + wave;  // this wave's gate tile
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
-    if (it >= NK && tid < DEC_RT)  // past the prefetched tiles (the slot's tile is done)
-      ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 3) ? list[rt * DEC_RT + tid] : -1;
+    if (it >= NK && tid < RT)  // past the prefetched tiles (the slot's tile is done)
+      ents[tid] = rt * RT + tid < cnt && dec_ok(rt * RT + tid < a.Npad, 3) ? list[rt * RT + tid] : -1;
     lds_barrier();
     ST_MARK(st1);
     // this lane's committed cell states (sub-tile st: row ents[16 st + c]) and, layer 0, its
@@ -460,7 +460,7 @@ __device__ __forceinline__ void dec_pred_body(const DecArgs& a, int parity, cons
     // [h0 of the candidate slot | h1 committed]
     // every load of the tile first (one memory round trip); entries past the list end read row
     // 0 (a safe cached address) and stage zeros
-    constexpr int NX = DEC_RT * (KX / 8), NIT = (NX + PRED_THREADS - 1) / PRED_THREADS;
+    constexpr int NX = RT * (KX / 8), NIT = (NX + PRED_THREADS - 1) / PRED_THREADS;
     uint4 xv[NIT];
     int emv[NIT];
 #pragma unroll
@@ -573,10 +573,11 @@ struct GRegs {
   float4 b0;
   bool wl = false;
 };
-template <bool PS>
+template <bool PS, int RT = DEC_RT>
 __device__ __forceinline__ void dec_g_body(const DecArgs& a, int parity, const GridXY gxy, bool reset,
-                                           uint16_t (*X)[GXP], int (*ents_all)[DEC_RT], GRegs& W) {
-  constexpr int NK = G_THREADS / DEC_RT;  // row tiles whose list entries load up front
+                                           uint16_t (*X)[GXP], int (*ents_all)[RT], GRegs& W) {
+  constexpr int NK = G_THREADS / RT;  // row tiles whose list entries load up front
+  constexpr int DEC_SUB = RT / 16;
   const DecState& s = a.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
   ST_MARK(st0);
@@ -585,19 +586,19 @@ __device__ __forceinline__ void dec_g_body(const DecArgs& a, int parity, const G
     st_b32<PS>(&s.count[LIVE_N(parity ^ 1)], 0u);
   }
   const int* list = s.list + parity * a.Npad;
-  const int i0 = (gxy.y + (tid / DEC_RT) * gxy.ny) * DEC_RT + tid % DEC_RT;
+  const int i0 = (gxy.y + (tid / RT) * gxy.ny) * RT + tid % RT;
   const int e0 = i0 < a.Npad ? list[i0] : -1;
   const int cnt = s.count[EMIT_N(parity)];
-  const int ntiles = (cnt + DEC_RT - 1) / DEC_RT;
+  const int ntiles = (cnt + RT - 1) / RT;
   if (gxy.y >= ntiles) return;
-  ents_all[tid / DEC_RT][tid % DEC_RT] = i0 < cnt ? e0 : -1;
+  ents_all[tid / RT][tid % RT] = i0 < cnt ? e0 : -1;
   const int jt = gxy.x * (G_THREADS / 64) + wave;  // this wave's column tile
   for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
     int* ents = ents_all[it % NK];
-    if (it >= NK && tid < DEC_RT) ents[tid] = rt * DEC_RT + tid < cnt && dec_ok(rt * DEC_RT + tid < a.Npad, 6) ? list[rt * DEC_RT + tid] : -1;
+    if (it >= NK && tid < RT) ents[tid] = rt * RT + tid < cnt && dec_ok(rt * RT + tid < a.Npad, 6) ? list[rt * RT + tid] : -1;
     lds_barrier();
     ST_MARK(st1);
-    constexpr int NX = DEC_RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
+    constexpr int NX = RT * (P / 8), NIT = (NX + G_THREADS - 1) / G_THREADS;
     uint4 xv[NIT];
     int emv[NIT];
 #pragma unroll
@@ -659,6 +660,140 @@ __global__ void __launch_bounds__(G_THREADS) dec_g_kernel(DecArgs a, int parity)
   __shared__ int ents_all[G_THREADS / DEC_RT][DEC_RT];
   GRegs W;
   dec_g_body<false>(a, parity, xcd_grid(J / (16 * (G_THREADS / 64))), blockIdx.x == 0, X, ents_all, W);
+}
+
+// Co-resident step kernels (SLIM): 16-row tiles and a register cap, so a workgroup fits on a CU
+// beside a 256x256 encoder tick workgroup (147456 B of LDS, 2 waves x 200 VGPRs per SIMD: 16 KiB of
+// LDS and 112 VGPRs per SIMD left).  The same bodies, the same instruction sequence per row: identical
+// results.  While an encoder runs, the step kernels above wait for a tick workgroup to give up a CU.
+constexpr int SLIM_RT = 16;
+#ifndef RNNT_EMU
+#define SLIM_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(56)))  // 112 on gfx950 (the attribute counts half)
+#else
+#define SLIM_BOUNDS __launch_bounds__(256)
+#endif
+template <int LAYER>
+__global__ void SLIM_BOUNDS dec_pred_slim_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) uint16_t X[SLIM_RT][pred_xp(LAYER)];
+  __shared__ int ents_all[256 / SLIM_RT][SLIM_RT];
+  PredRegs<LAYER> W;
+  dec_pred_body<LAYER, 4, false, SLIM_RT>(a, parity, xcd_grid(PG4 / 64), X, ents_all, W);
+}
+// Layer 1 does not fit that way (its [x | h] staging alone is 21 KB at 16 rows, its 640-k weight
+// slice 80 VGPRs per wave), so its two chains are split over the two launches: the h chain (b_hh +
+// h1.W_hh^T) reads only the committed h1, known before the step, so it runs in the layer-0 launch
+// (gate groups 20..39 of that grid) and leaves its sums in PH; the layer-1 launch runs the x chain
+// (b_ih + h0'.W_ih^T, h0' = layer 0's new h) and adds PH, x + h as the step kernel adds them.  Each
+// role is a 320-k chain like the G kernel's.
+enum { SLIM_H1 = 0, SLIM_X1 = 1 };
+template <int ROLE>
+__device__ __forceinline__ void dec_l1_slim_body(const DecArgs& a, int parity, const GridXY gxy, uint16_t (*X)[GXP],
+                                                 int (*ents_all)[SLIM_RT]) {
+  constexpr int RT = SLIM_RT, NK = 256 / RT;
+  const DecState& s = a.s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  const int* list = s.list + parity * a.Npad;
+  const int i0 = (gxy.y + (tid / RT) * gxy.ny) * RT + tid % RT;
+  const int e0 = i0 < a.Npad ? list[i0] : -1;
+  const int cnt = s.count[EMIT_N(parity)];
+  const int ntiles = (cnt + RT - 1) / RT;
+  if (gxy.y >= ntiles) return;
+  ents_all[tid / RT][tid % RT] = i0 < cnt ? e0 : -1;
+  const int t0 = gxy.x * 4 + wave;  // this wave's gate tile
+  uint4 wv[P / 32];
+  float4 b0 = float4{0.0f, 0.0f, 0.0f, 0.0f};
+  bool wl = false;
+  for (int rt = gxy.y, it = 0; rt < ntiles; rt += gxy.ny, ++it) {
+    int* ents = ents_all[it % NK];
+    if (it >= NK && tid < RT) ents[tid] = rt * RT + tid < cnt && dec_ok(rt * RT + tid < a.Npad, 6) ? list[rt * RT + tid] : -1;
+    lds_barrier();
+    // this lane's row (column c of the tile) and, x chain, its cell state and h-chain sums
+    int ec = ents[c];
+    if (ec >= 0 && !dec_ok(entry_row(ec) < a.Npad && entry_label(ec) <= 28, 0)) ec = -1;
+    const int erow = ec >= 0 ? entry_row(ec) : 0, esl = ec >= 0 ? entry_slot(ec) : 0;
+    float cp = 0.0f;
+    float4 ph = float4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (ROLE == SLIM_X1 && ec >= 0) {
+      cp = hc_part(a.hc, erow, esl, 3)[t0 * 4 + q];
+      ph = *(const float4*)(a.PH + (size_t)erow * PG4 + t0 * 16 + 4 * q);
+    }
+    constexpr int NX = RT * (P / 8), NIT = (NX + 255) / 256;
+    uint4 xv[NIT];
+    int emv[NIT];
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int i = tid + 256 * u;
+      emv[u] = (NX % 256 == 0 || i < NX) ? ents[i / (P / 8)] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {  // every load first (one round trip); past the list end: row 0, zeros staged
+      const int i = tid + 256 * u;
+      if (NX % 256 == 0 || i < NX) {
+        const int k = (i % (P / 8)) * 8, em = emv[u];
+        const bool okr = em >= 0 && dec_ok(entry_row(em) < a.Npad, 1);
+        const int r = okr ? entry_row(em) : 0, sm = okr ? entry_slot(em) : 0;
+        xv[u] = *(const uint4*)((ROLE == SLIM_H1 ? h_bf(a.hc, r, sm, 1) : h_bf(a.hc, r, sm ^ 1, 0)) + k);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the weight loads behind the input loads
+    if (!wl) {
+      wl = true;
+      const uint16_t* wr = a.w.wp[1] + (size_t)(t0 * 16 + c) * 640 + 8 * q + (ROLE == SLIM_H1 ? P : 0);
+#pragma unroll
+      for (int b = 0; b < P / 32; ++b) wv[b] = *(const uint4*)(wr + 32 * b);
+      b0 = *(const float4*)((ROLE == SLIM_H1 ? a.w.bhh_p[1] : a.w.bih_p[1]) + t0 * 16 + 4 * q);
+    }
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int i = tid + 256 * u;
+      if (NX % 256 == 0 || i < NX) {
+        const int m = i / (P / 8), k = (i % (P / 8)) * 8;
+        *(uint4*)&X[m][k] = emv[u] >= 0 ? xv[u] : uint4{0u, 0u, 0u, 0u};
+      }
+    }
+    lds_barrier();
+    v4f acc = v4f{b0.x, b0.y, b0.z, b0.w};
+#pragma unroll
+    for (int b = 0; b < P / 32; ++b) acc = mfma_bf16(wv[b], *(const uint4*)(&X[c][8 * q] + 32 * b), acc);
+    if (ec >= 0) {
+      if (ROLE == SLIM_H1) {
+        *(v4f*)(a.PH + (size_t)erow * PG4 + t0 * 16 + 4 * q) = acc;
+      } else {
+        const v4f gs = acc + v4f{ph.x, ph.y, ph.z, ph.w};
+        const int u = t0 * 4 + q;
+        const float ig = det_sigmoid(gs[0]), fg = det_sigmoid(gs[1]), gg = det_tanh(gs[2]), og = det_sigmoid(gs[3]);
+        const float cn = fg * cp + ig * gg;
+        const float hh = bf_round_ftz(og * det_tanh(cn));
+        hc_part(a.hc, erow, esl ^ 1, 3)[u] = cn;
+        h_bf(a.hc, erow, esl ^ 1, 1)[u] = (uint16_t)(__float_as_uint(hh) >> 16);
+      }
+    }
+    lds_barrier();  // X and this entry slot are restaged by the next tile
+  }
+}
+// layer 0 (gate groups 0..19) and layer 1's h chain (20..39) in one launch
+__global__ void SLIM_BOUNDS dec_pred0h_slim_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) uint16_t X[SLIM_RT][GXP];
+  __shared__ int ents_all[256 / SLIM_RT][SLIM_RT];
+  GridXY g = xcd_grid(2 * (PG4 / 64));
+  if (g.x < PG4 / 64) {
+    PredRegs<0> W;
+    dec_pred_body<0, 4, false, SLIM_RT>(a, parity, g, X, ents_all, W);
+  } else {
+    g.x -= PG4 / 64;
+    dec_l1_slim_body<SLIM_H1>(a, parity, g, X, ents_all);
+  }
+}
+__global__ void SLIM_BOUNDS dec_pred1x_slim_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) uint16_t X[SLIM_RT][GXP];
+  __shared__ int ents_all[256 / SLIM_RT][SLIM_RT];
+  dec_l1_slim_body<SLIM_X1>(a, parity, xcd_grid(PG4 / 64), X, ents_all);
+}
+__global__ void SLIM_BOUNDS dec_g_slim_kernel(DecArgs a, int parity) {
+  __shared__ __attribute__((aligned(16))) uint16_t X[SLIM_RT][GXP];
+  __shared__ int ents_all[G_THREADS / SLIM_RT][SLIM_RT];
+  GRegs W;
+  dec_g_body<false, SLIM_RT>(a, parity, xcd_grid(J / (16 * (G_THREADS / 64))), blockIdx.x == 0, X, ents_all, W);
 }
 
 // joint (y1 = bf16(relu(F[t] + G)), logits = b2 + y1.W2^T) + argmax + greedy_decode_update
@@ -891,6 +1026,192 @@ __global__ void __launch_bounds__(256) dec_joint_kernel(DecArgs a, int parity) {
   dec_joint_body<false>(a, parity, blockIdx.x, gridDim.x, L, W);
 }
 
+// Co-resident joint (SLIM): 9 KB of LDS and at most 112 VGPRs, so it fits beside an encoder tick
+// workgroup.  No y1 staging: wave w takes k block w (k = 128w .. 128w + 127) for both label halves and
+// builds its B fragments in registers straight from F and G (the 8 k of row c that the MFMA's lane
+// (q, c) takes: F and G for 16 rows x 128 k per wave, each element loaded once per tile); its two
+// chains are s_w of the step kernel (from b2 on block 0, from 0 on the others), so the logits
+// ((s0 + s1) + s2) + s3 and everything after them are the step kernel's.  G is re-read each walk
+// iteration (the step kernel keeps it in registers).
+struct JointSlimLds {
+  float Lp[4][JRT][NLAB_PAD + 1];
+  int rows[JRT], walking[JRT], tidx[JRT], emit_e[JRT];
+  int slot_[JRT], add_[JRT], flen_[JRT], idx_[JRT];
+};
+__global__ void SLIM_BOUNDS dec_joint_slim_kernel(DecArgs a, int parity) {
+  __shared__ JointSlimLds L;
+  const DecState& s = a.s;
+  const int jg = blockIdx.x, njg = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, c = lane & 15;
+  const int4* llist = s.live + parity * a.Npad;
+  int4* nlist = s.live + (parity ^ 1) * a.Npad;
+  const int4 r_first = tid < JRT ? llist[jg * JRT + tid] : int4{0, 0, 0, 0};
+  const int lcnt = s.count[LIVE_N(parity)];
+  const int ntiles = (lcnt + JRT - 1) / JRT;
+  if (jg >= ntiles) return;
+  for (int rt = jg; rt < ntiles; rt += njg) {
+    if (tid < JRT) {
+      const int i = rt * JRT + tid;
+      const int4 e = i < lcnt && dec_ok(i < a.Npad, 7) ? (rt == jg ? r_first : llist[i]) : int4{-1, 0, 0, 0};
+      int r = e.x < 0 ? -1 : entry_row(e.x);
+      if (r >= 0 && !dec_ok(r < a.Npad && (e.y & 0xffff) < ((e.y >> 16) & 0xffff), 8)) r = -1;
+      L.rows[tid] = r;
+      L.walking[tid] = r >= 0;
+      L.emit_e[tid] = -1;
+      L.slot_[tid] = (e.x >> 24) & 1;
+      L.add_[tid] = (e.x >> 25) & 31;
+      L.tidx[tid] = e.y & 0xffff;
+      L.flen_[tid] = (e.y >> 16) & 0xffff;
+      L.idx_[tid] = e.z;
+    }
+    lds_barrier();
+#pragma unroll 1
+    for (int it = 0; it < JOINT_ITERS; ++it) {
+      bool any = false;
+      for (int m = 0; m < JRT; ++m) any |= L.walking[m] != 0;
+      if (!any) break;
+      // this lane's row: F at its walk frame and G (rows not walking read row 0 of frame 0: their
+      // columns are computed and dropped)
+      const bool wk = L.walking[c] != 0;
+      const int row = wk ? L.rows[c] : 0, tm = wk ? L.tidx[c] : 0;
+      const float* fr = a.F + ((size_t)tm * a.Npad + row) * J + 128 * wave + 8 * q;
+      const float* gr = a.G + (size_t)row * J + 128 * wave + 8 * q;
+      // W2 fragments (label half h, k = 128 wave + 32 b + 8 q; re-read each iteration, L1 / L2
+      // hits) and F and G in two halves: the first half goes to bf16 before the second loads --
+      // 64 VGPRs of F and G at once would not fit beside the weights
+      uint4 wv[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint16_t* wr = a.w.w2 + (size_t)(h * 16 + c) * J + 128 * wave + 8 * q;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) wv[h][b] = *(const uint4*)(wr + 32 * b);
+      }
+      // chains from b2 on block 0 (re-read each iteration: registers are the budget here)
+      v4f s0 = v4f{0.0f, 0.0f, 0.0f, 0.0f}, s1 = s0;
+      if (wave == 0) {
+        s0 = *(const v4f*)(a.w.b2 + 4 * q);
+        s1 = *(const v4f*)(a.w.b2 + 16 + 4 * q);
+      }
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        v4f f4[2][2];
+        float4 g4[2][2];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const int b = 2 * hb + bb;
+          f4[bb][0] = __builtin_nontemporal_load((const v4f*)(fr + 32 * b));  // streamed once
+          f4[bb][1] = __builtin_nontemporal_load((const v4f*)(fr + 32 * b + 4));
+          g4[bb][0] = *(const float4*)(gr + 32 * b);
+          g4[bb][1] = *(const float4*)(gr + 32 * b + 4);
+        }
+        uint4 yb[2];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          float y[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const v4f f = f4[bb][h];
+            const float4 g = g4[bb][h];
+            const float t0 = f[0] + g.x, t1 = f[1] + g.y, t2 = f[2] + g.z, t3 = f[3] + g.w;
+            y[4 * h + 0] = bf_round_ftz(t0 > 0.0f ? t0 : 0.0f);
+            y[4 * h + 1] = bf_round_ftz(t1 > 0.0f ? t1 : 0.0f);
+            y[4 * h + 2] = bf_round_ftz(t2 > 0.0f ? t2 : 0.0f);
+            y[4 * h + 3] = bf_round_ftz(t3 > 0.0f ? t3 : 0.0f);
+          }
+          yb[bb] = pack8(float4{y[0], y[1], y[2], y[3]}, float4{y[4], y[5], y[6], y[7]});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          s0 = mfma_bf16(wv[0][2 * hb + bb], yb[bb], s0);
+          s1 = mfma_bf16(wv[1][2 * hb + bb], yb[bb], s1);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        L.Lp[wave][c][4 * q + r] = s0[r];
+        L.Lp[wave][c][16 + 4 * q + r] = s1[r];
+      }
+      lds_barrier();
+      // the step kernel's argmax and greedy_decode_update (dec_joint_body)
+      {
+        const int m = 4 * wave + (lane >> 4), l2 = 2 * (lane & 15);
+        float bv = 0.0f;
+        int bl = -1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int j = l2 + e;
+          const float v = ((L.Lp[0][m][j] + L.Lp[1][m][j]) + L.Lp[2][m][j]) + L.Lp[3][m][j];
+          if (j < NLAB && (bl < 0 || v > bv)) {
+            bv = v;
+            bl = j;
+          }
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          const float ov = __shfl_xor(bv, off);
+          const int ol = __shfl_xor(bl, off);
+          if (ol >= 0 && (bl < 0 || ov > bv || (ov == bv && ol < bl))) {
+            bv = ov;
+            bl = ol;
+          }
+        }
+        if ((lane & 15) == 0 && L.walking[m]) {
+          const int row = L.rows[m], best = bl;
+          if (best != BLANK && L.add_[m] != MAXSYM) {
+            const int id = L.idx_[m] + 1;
+            L.idx_[m] = id;
+            s.idx[row] = id;
+            if (id < a.max_res) a.res[(size_t)row * a.max_res + id] = best;
+            s.added[row] = ++L.add_[m];
+            s.preg[row] = best;
+            const int nsl = L.slot_[m] ^ 1;  // commit the candidate (hg, cg) as (pre_hg, pre_cg)
+            L.slot_[m] = nsl;
+            s.slot[row] = nsl;
+            L.emit_e[m] = emit_entry(row, nsl, best);
+            L.walking[m] = 0;
+          } else {
+            const int fl = L.flen_[m];
+            int t = L.tidx[m] + 1;
+            if (t >= fl) {
+              s.fin[row] = 1;
+              L.walking[m] = 0;
+              L.rows[m] = -1;  // finished: not in the next live list
+              t = fl - 1;
+            }
+            L.tidx[m] = t;
+            s.time[row] = t;
+            s.added[row] = 0;
+            L.add_[m] = 0;
+          }
+        }
+      }
+      lds_barrier();
+    }
+    // the tile's emitting rows -> next emit list, its unfinished rows -> next live list (one 64-bit atomic)
+    if (wave == 0) {
+      const int e = lane < JRT ? L.emit_e[lane] : -1;
+      const int r = lane < JRT ? L.rows[lane] : -1;
+      const unsigned long long me = __ballot(e >= 0), mr = __ballot(r >= 0);
+      unsigned long long base = 0;
+      if (lane == 0 && (me | mr)) {
+        const unsigned long long inc = (unsigned long long)__popcll(me) | ((unsigned long long)__popcll(mr) << 32);
+        base = atomicAdd((unsigned long long*)&s.count[EMIT_N(parity ^ 1)], inc);
+      }
+      base = __shfl(base, 0);
+      const unsigned long long below = (1ull << lane) - 1;
+      if (lane == 0) dec_ok(false, 31);  // ran (the emulator's check that the joint executed)
+      if (e >= 0 && dec_ok((int)(base & 0xffffffffu) + __popcll(me & below) < a.Npad, 9))
+        s.list[(parity ^ 1) * a.Npad + (int)(base & 0xffffffffu) + __popcll(me & below)] = e;
+      if (r >= 0 && dec_ok((int)(base >> 32) + __popcll(mr & below) < a.Npad, 10)) {
+        const int4 le = live_entry(r, L.slot_[lane], L.add_[lane], L.tidx[lane], L.flen_[lane], L.idx_[lane]);
+        nlist[(int)(base >> 32) + __popcll(mr & below)] = le;
+      }
+    }
+    lds_barrier();  // rows / walking / tidx are reused by the next row tile
+  }
+}
+
 #ifndef RNNT_EMU
 // ---------------------------------------------------------------- persistent tail decode
 // Once few rows are live (the long tail of a length-sorted batch, where a step is four dependent
@@ -1018,7 +1339,7 @@ __global__ void dec_finish_kernel(DecArgs a) {
 
 int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs, hipStream_t st, const int32_t* reset) {
   // every buffer the step kernels address (a missing one is a host error here, not a GPU fault)
-  const void* need[] = {a.F, a.f_lens, a.hc, a.G, a.res, a.res_len, a.w.xtab, a.w.wp[0], a.w.wp[1], a.w.bih_p[1],
+  const void* need[] = {a.F, a.f_lens, a.hc, a.G, a.PH, a.res, a.res_len, a.w.xtab, a.w.wp[0], a.w.wp[1], a.w.bih_p[1],
                         a.w.bhh_p[0], a.w.bhh_p[1], a.w.w1p, a.w.bp, a.w.w2, a.w.b2, a.s.time, a.s.added, a.s.idx,
                         a.s.preg, a.s.slot, a.s.fin, a.s.list, a.s.live, a.s.count, a.s.pc};
   for (const void* p : need)
@@ -1062,6 +1383,14 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     }
     return rg;
   }();
+  // the co-resident step kernels (SLIM_BOUNDS): pred0 (1), pred1 with layer 1's h chain moved into the
+  // layer-0 launch (2), G (4), joint (8) -- all four by default: 121.1-121.6k -> 122.9-123.1k utt/s,
+  // overlapped greedy decode 2236 -> 1488 ms per query, isolated 656 -> 726 (MEASUREMENTS section 9).
+  // Development knob RNNT_DEC_SLIM=mask selects a subset (0: the step kernels above alone).
+  static const int SLIM = [] {
+    const char* v = dev_env("RNNT_DEC_SLIM");
+    return v ? atoi(v) : 15;
+  }();
   // persistent tail (dec_persist_kernel): once the live rows read back fit a.persist_rows, one launch
   // runs every remaining step (0 = off; at most DEC_PERSIST_MAX rows)
 #ifndef RNNT_EMU
@@ -1101,15 +1430,33 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_g = lt1 < RG[1] ? lt1 : RG[1];
     const int ljt = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
     const int rg_joint = ljt < RG[2] ? ljt : RG[2];
+    // co-resident kernels: 16-row tiles, twice the row groups
+    const int ls = (live_bound + SLIM_RT - 1) / SLIM_RT < a.Npad / SLIM_RT ? (live_bound + SLIM_RT - 1) / SLIM_RT : a.Npad / SLIM_RT;
+    const int ls1 = ls > 0 ? ls : 1;
+    const int sg_pred = ls1 < 2 * RG[0] ? ls1 : 2 * RG[0], sg_g = ls1 < 2 * RG[1] ? ls1 : 2 * RG[1];
     for (int i = 0; i < csz && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
-      hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                         dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
-                         dim3(PRED_THREADS), 0, st, a, p);
-      hipLaunchKernelGGL(dec_g_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), rg_g)), dim3(G_THREADS), 0, st, a,
-                         p);
-      hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
+      if (SLIM & 2)
+        hipLaunchKernelGGL(dec_pred0h_slim_kernel, dim3(xcd_grid_size(2 * (PG4 / 64), sg_pred)), dim3(256), 0, st, a, p);
+      else if (SLIM & 1)
+        hipLaunchKernelGGL((dec_pred_slim_kernel<0>), dim3(xcd_grid_size(PG4 / 64, sg_pred)), dim3(256), 0, st, a, p);
+      else
+        hipLaunchKernelGGL((dec_pred_kernel<0, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                           dim3(PRED_THREADS), 0, st, a, p);
+      if (SLIM & 2)
+        hipLaunchKernelGGL(dec_pred1x_slim_kernel, dim3(xcd_grid_size(PG4 / 64, sg_pred)), dim3(256), 0, st, a, p);
+      else
+        hipLaunchKernelGGL((dec_pred_kernel<1, PRED_THREADS / 64>), dim3(xcd_grid_size(PG4 / (16 * (PRED_THREADS / 64)), rg_pred)),
+                           dim3(PRED_THREADS), 0, st, a, p);
+      if (SLIM & 4)
+        hipLaunchKernelGGL(dec_g_slim_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), sg_g)), dim3(G_THREADS), 0, st, a, p);
+      else
+        hipLaunchKernelGGL(dec_g_kernel, dim3(xcd_grid_size(J / (16 * (G_THREADS / 64)), rg_g)), dim3(G_THREADS), 0, st, a,
+                           p);
+      if (SLIM & 8)
+        hipLaunchKernelGGL(dec_joint_slim_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
+      else
+        hipLaunchKernelGGL(dec_joint_kernel, dim3(rg_joint), dim3(256), 0, st, a, p);
     }
     // poll the live-row count one chunk behind, so the host never drains the queue: the length of
     // the live list the chunk's last joint wrote (parity step & 1; the next step's G kernel resets

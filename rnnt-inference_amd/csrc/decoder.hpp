@@ -39,6 +39,7 @@ struct DecArgs {
   const int32_t* f_lens;   // [Npad]
   float* hc;               // [Npad][2 slots][4][320] (h0, h1, c0, c1) prediction state
   float* G;                // [Npad][512] joint pred half of the current candidate
+  float* PH;               // [Npad][1280] layer-1 h-chain gate sums (b_hh + h1.W_hh^T) of the emitting rows
   int32_t* res;            // [N][max_res]
   int32_t* res_len;        // [N]
   DecState s;

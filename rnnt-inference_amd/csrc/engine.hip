@@ -65,7 +65,7 @@ struct rnnt_engine {
   int8_t* h[5][2] = {};
   uint16_t* c[5] = {};
   uint16_t* fbf = nullptr;
-  float *F = nullptr, *hc = nullptr, *G = nullptr;
+  float *F = nullptr, *hc = nullptr, *G = nullptr, *PH = nullptr;
   int32_t* flen = nullptr;
   DecState ds{};
   int32_t* host_flags = nullptr;
@@ -339,6 +339,7 @@ static int alloc_workspace(rnnt_engine* e) {
   r = r ? r : dev_alloc(e, &e->F, TPM * NP * J);
   r = r ? r : dev_alloc(e, &e->hc, NP * 2 * 4 * P);
   r = r ? r : dev_alloc(e, &e->G, NP * J);
+  r = r ? r : dev_alloc(e, &e->PH, NP * PG4);
   r = r ? r : dev_alloc(e, &e->flen, NP);
   int32_t** ints[] = {&e->ds.time, &e->ds.added, &e->ds.idx, &e->ds.preg, &e->ds.slot, &e->ds.fin};
   for (auto pp : ints) r = r ? r : dev_alloc(e, pp, NP);
@@ -1004,6 +1005,7 @@ static int decode_core(rnnt_engine* e, int32_t* res, int32_t* res_len, int max_r
   a.f_lens = flen;
   a.hc = e->hc;
   a.G = e->G;
+  a.PH = e->PH;
   a.res = res;
   a.res_len = res_len;
   a.N = n;

@@ -20,16 +20,19 @@ def emu(tmp_path_factory):
     if not os.path.exists(CLANG) or not shutil.which("python3"):
         pytest.skip("no ROCm clang++")
     out = tmp_path_factory.mktemp("emu")
-    env = dict(os.environ, EMU_ASAN="0", EMU_OUT=str(out))
+    env = dict(os.environ, EMU_ASAN="0", EMU_OUT=str(out), EMU_CFLAGS="-DRNNT_DEV_KNOBS")  # RNNT_DEC_SLIM below
     subprocess.run(["bash", os.path.join(REPO, "tools", "emu", "build.sh")], check=True, env=env,
                    capture_output=True, timeout=600)
     return str(out / "dec_emu")
 
 
 @pytest.mark.parametrize("server", [0, 1])
-def test_decode_kernels_match_oracle_on_the_emulator(emu, server):
-    # 6 rows (two with the same length ratio as a real batch's tail), 4 frames, blank-biased joint
-    r = subprocess.run([emu, "6", "4", "5", str(server), "12"], capture_output=True, text=True, timeout=600)
+@pytest.mark.parametrize("slim", ["15", "0"])
+def test_decode_kernels_match_oracle_on_the_emulator(emu, server, slim):
+    # 6 rows (two with the same length ratio as a real batch's tail), 4 frames, blank-biased joint;
+    # slim 15: the co-resident step kernels (the default), 0: the big-tile step kernels
+    r = subprocess.run([emu, "6", "4", "5", str(server), "12"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, RNNT_DEC_SLIM=slim))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bounds checks: ok" in r.stdout, r.stdout
     assert "tokens identical" in r.stdout, r.stdout

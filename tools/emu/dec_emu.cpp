@@ -138,6 +138,7 @@ int main(int argc, char** argv) {
   a.f_lens = d_flen;
   a.hc = dalloc<float>((size_t)Npad * 2 * 4 * P);
   a.G = dalloc<float>((size_t)Npad * J);
+  a.PH = dalloc<float>((size_t)Npad * PG4);
 #ifdef EMU_HAS_AH
   a.ah0 = dalloc<float>((size_t)Npad * PG4);
   a.ah1 = dalloc<float>((size_t)Npad * PG4);
