@@ -62,8 +62,6 @@ def parse():
                     help="utterances per encode+decode call (300000-sample query, 4 in flight, one box: 6144 "
                          "123.1-124.9k utt/s, 4096 121.4-122.6k, 8192 x 3 122.0-123.3k, 8192 x 2 105.5k: with two "
                          "engines the encoder waits for a free one; MEASUREMENTS.md section 8)")
-    ap.add_argument("--encode-priority", action="store_true",
-                    help="encoders on high-priority HIP streams, decodes on normal ones (OfflineSUT encode_priority)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="engines per GPU (one HIP stream + host thread each): one batch's latency-bound greedy "
                          "decode overlaps the next batch's encoder")
@@ -489,7 +487,7 @@ def main():
     ids, idx = dist.query_arrays(args.qsl, query)
     max_b = max([args.batch] + ([int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else []))
     engines = [Engine(pm, device=dev, max_batch=min(max_b, query), max_frames=500) for _ in range(args.inflight)]
-    sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes, encode_priority=args.encode_priority)
+    sut = OfflineSUT(engines, qsl, early_decodes=args.early_decodes)
     if args.sut_warmup:  # OfflineSUT::warmup (torch_sut.cpp:124-138), before any query
         sut.warmup(iters=args.sut_warmup, batch_size=args.batch, frames=args.sut_warmup_frames)
     sizes = [int(v) for v in args.batch_sizes.split(",")] if args.batch_sizes else None

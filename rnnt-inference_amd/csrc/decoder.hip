@@ -1430,10 +1430,11 @@ int launch_greedy_decode(const DecArgs& a, int32_t* host_flags, hipEvent_t* evs,
     const int rg_g = lt1 < RG[1] ? lt1 : RG[1];
     const int ljt = (live_bound + JRT - 1) / JRT > 0 ? (live_bound + JRT - 1) / JRT : 1;
     const int rg_joint = ljt < RG[2] ? ljt : RG[2];
-    // co-resident kernels: 16-row tiles, twice the row groups
+    // co-resident kernels: 16-row tiles, the same row-group caps (twice as many: 120.4-122.8k vs 122.4-
+    // 123.6k utt/s on one box; 6-8 pred groups lose 9 % isolated, MEASUREMENTS section 9)
     const int ls = (live_bound + SLIM_RT - 1) / SLIM_RT < a.Npad / SLIM_RT ? (live_bound + SLIM_RT - 1) / SLIM_RT : a.Npad / SLIM_RT;
     const int ls1 = ls > 0 ? ls : 1;
-    const int sg_pred = ls1 < 2 * RG[0] ? ls1 : 2 * RG[0], sg_g = ls1 < 2 * RG[1] ? ls1 : 2 * RG[1];
+    const int sg_pred = ls1 < RG[0] ? ls1 : RG[0], sg_g = ls1 < RG[1] ? ls1 : RG[1];
     for (int i = 0; i < csz && step < a.max_iter; ++i, ++step) {
       const int p = step & 1;
       if (SLIM & 2)

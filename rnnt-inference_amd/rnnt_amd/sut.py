@@ -112,19 +112,14 @@ def make_batches(qsl, ids, idx, batch_size, sizes=None):
 
 
 class OfflineSUT:
-    def __init__(self, engines, qsl, batch_size=1024, batch_sizes=None, on_complete=None, early_decodes=None,
-                 encode_priority=False):
+    def __init__(self, engines, qsl, batch_size=1024, batch_sizes=None, on_complete=None, early_decodes=None):
         """engines: one Engine or a list (several per GPU keep batches in flight; engines on
         different devices serve one query together).  qsl: one QSL, or {device: QSL} when each
         GPU holds its own copy of the samples (GpuQSL replicas).  early_decodes: None = every
         batch decodes right after its encode (beside the next batch's encoder); k = when the query
         has no more batches than engines, only the first k batches do, the others' decodes wait
-        until every encode is done (they then run beside each other, not beside an encoder).
-        encode_priority: each engine encodes on a high-priority HIP stream and decodes on a second,
-        normal one (the dispatcher then hands a freed CU to a tick workgroup first)."""
+        until every encode is done (they then run beside each other, not beside an encoder)."""
         self.early_decodes = early_decodes
-        self.encode_priority = bool(encode_priority)
-        self._dec_streams = {}
         self.engines = list(engines) if isinstance(engines, (list, tuple)) else [engines]
         self.engine = self.engines[0]
         self.qsl, self.batch_size, self.batch_sizes = qsl, batch_size, batch_sizes
@@ -251,17 +246,8 @@ class OfflineSUT:
     def _stream_for(self, eng):
         import torch
         if id(eng) not in self._streams:
-            self._streams[id(eng)] = torch.cuda.Stream(device=eng.device, priority=-1 if self.encode_priority else 0)
+            self._streams[id(eng)] = torch.cuda.Stream(device=eng.device)
         return self._streams[id(eng)]
-
-    def _dec_stream_for(self, eng):
-        """The decode's stream: the engine's stream, or with encode_priority a second, normal-priority one."""
-        import torch
-        if not self.encode_priority:
-            return self._stream_for(eng)
-        if id(eng) not in self._dec_streams:
-            self._dec_streams[id(eng)] = torch.cuda.Stream(device=eng.device)
-        return self._dec_streams[id(eng)]
 
     def _device_scope(self, eng, st):
         import contextlib
@@ -343,12 +329,7 @@ class OfflineSUT:
                         h["cv"].wait_for(lambda: h["done"] == h["nb"] or h["failed"])
                         if h["failed"]:
                             raise RuntimeError("OfflineSUT: an encode of this query failed; held decode abandoned")
-                sd = self._dec_stream_for(eng)
-                if sd is st:
-                    rlh, toks = self._decode(eng, st, enc)
-                else:  # the encode is complete (_encode synchronised): the decode needs no event
-                    with self._device_scope(eng, sd):
-                        rlh, toks = self._decode(eng, sd, enc)
+                rlh, toks = self._decode(eng, st, enc)
         finally:
             hand_on()
         self.query_samples_complete(ids, idx, toks, rlh)
