@@ -16,6 +16,7 @@
 // (stream, pinned staging, device buffers) on the least-loaded GPU of the group.
 #pragma once
 #include <ATen/ATen.h>
+#include <ATen/Parallel.h>
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -86,7 +87,11 @@ class AudioProcessor {
     std::memcpy(s.stage.host, off.data(), o_len);
     if (n) std::memcpy(s.stage.host + o_len, lens, sizeof(int32_t) * n);
     float* w = (float*)(s.stage.host + o_wav);
-    for (int i = 0; i < n; ++i) std::memcpy(w + off[i], x.data_ptr<float>() + (int64_t)i * x.size(1), sizeof(float) * lens[i]);
+    const float* xs = x.data_ptr<float>();
+    const int64_t pitch = x.size(1);
+    at::parallel_for(0, n, 16, [&](int64_t b, int64_t e) {  // the rows' audio back to back (the batch's bulk copy)
+      for (int64_t i = b; i < e; ++i) std::memcpy(w + off[i], xs + i * pitch, sizeof(float) * lens[i]);
+    });
     mi355x::hcheck(hipMemcpyAsync(s.stage.dev, s.stage.host, bytes, hipMemcpyHostToDevice, s.st), "copy wav");
     const size_t fbytes = (size_t)T * n_out * 256 * sizeof(float);
     if (fbytes > s.feats_cap) {
