@@ -176,3 +176,50 @@ def test_no_packed_fp32_in_built_objects():
             if hits:
                 bad[os.path.basename(o)] = hits
     assert not bad, f"packed FP32 in built objects (rebuild: make -C {CSRC}): {bad}"
+
+
+def _kernel_resources(obj):
+    """{kernel name: {agpr_count, vgpr_count, group_segment_fixed_size, private_segment_fixed_size}}
+    from the AMDGPU metadata note of an object's gfx950 code object."""
+    with tempfile.TemporaryDirectory() as td:
+        b, co = os.path.join(td, "x.bundle"), os.path.join(td, "x.co")
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={b}", obj], check=True, capture_output=True)
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={b}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+        notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True, capture_output=True,
+                               text=True).stdout
+    out = {}
+    for blk in re.split(r"\n  - (?=\.agpr_count:)", notes)[1:]:
+        name = re.search(r"^    \.name:\s+(\S+)", blk, re.M)
+        if not name:
+            continue
+        out[name.group(1)] = {k: int(re.search(rf"^\s*\.{k}:\s+(\d+)", blk, re.M).group(1))
+                              for k in ("agpr_count", "vgpr_count", "group_segment_fixed_size",
+                                        "private_segment_fixed_size")}
+    return out
+
+
+def test_coresident_decode_kernels_fit_beside_a_tick():
+    """The decode step kernels the engine launches (decoder.hip SLIM_BOUNDS) must fit on a CU beside a
+    256x256 encoder tick workgroup, or every decode launch waits for ticks to give up CUs again
+    (MEASUREMENTS section 9).  Budget per CU: 160 KiB of LDS minus the tick's
+    147456 B (TileCfg<4, 8, 2>::SMEM: two 64 KiB stages + the 16 KiB sigma table, dynamic LDS), and per
+    SIMD 512 VGPRs minus the tick's two waves (8-VGPR granules, AGPRs included); no scratch."""
+    objs = {n: os.path.join(CSRC, n + ".o") for n in ("encoder", "decoder")}
+    if not all(os.path.exists(o) for o in objs.values()) or not os.path.exists(os.path.join(LLVM, "clang-offload-bundler")):
+        pytest.skip("library not built here")
+    enc, dec = _kernel_resources(objs["encoder"]), _kernel_resources(objs["decoder"])
+    alloc = lambda r: -(-(r["vgpr_count"] + r["agpr_count"]) // 8) * 8  # noqa: E731
+    tick = [r for n, r in enc.items() if "lstm_i8_tick_kernel" in n and "ILi4ELi8ELi2E" in n]
+    assert len(tick) == 1, sorted(enc)
+    tick_lds, tick_vgprs = 147456, 2 * alloc(tick[0])
+    slim = {n: r for n, r in dec.items() if "_slim_kernel" in n}
+    for want in ("dec_pred0h_slim_kernel", "dec_pred1x_slim_kernel", "dec_g_slim_kernel", "dec_joint_slim_kernel"):
+        assert any(want in n for n in slim), (want, sorted(dec))
+    for n, r in slim.items():
+        assert r["group_segment_fixed_size"] + tick_lds <= 160 * 1024, (n, r)
+        assert alloc(r) + tick_vgprs <= 512, (n, r, tick[0])
+        assert r["private_segment_fixed_size"] == 0, (n, r)
+    # the check can fail: the big-tile layer-1 step kernel does not fit (43 KiB of LDS, 218 VGPRs)
+    big = [r for n, r in dec.items() if "dec_pred_kernelILi1E" in n]
+    assert big and (big[0]["group_segment_fixed_size"] + tick_lds > 160 * 1024 or alloc(big[0]) + tick_vgprs > 512)
