@@ -115,6 +115,8 @@ struct Slot {
   int32_t* d_res = nullptr;   // [rows][max_res]
   int32_t* d_len = nullptr;   // [rows]
   int32_t* h_len = nullptr;   // pinned [rows]
+  int32_t* h_res = nullptr;   // pinned [rows][widest]: the written columns, copied on to the State's res_
+  size_t h_res_cap = 0;
   int32_t* d_reset = nullptr; // points into dev (stream calls)
   float* dense = nullptr;     // [T][rows][256] device input of a batch the SUT assembled in pinned memory
   size_t dense_cap = 0;
@@ -139,10 +141,20 @@ struct Slot {
     hcheck(hipMalloc((void**)&dense, bytes), "hipMalloc dense input");
     dense_cap = bytes;
   }
+  void grow_res(size_t bytes) {
+    if (bytes <= h_res_cap) return;
+    if (h_res) hcheck(hipHostFree(h_res), "hipHostFree");
+    h_res = nullptr;
+    h_res_cap = 0;
+    const size_t c = (size_t)round_up((int64_t)bytes, 1 << 20);
+    hcheck(hipHostMalloc((void**)&h_res, c, hipHostMallocDefault), "hipHostMalloc results");
+    h_res_cap = c;
+  }
   ~Slot() {  // torn down by ~TorchModel, while the HIP runtime is up
     if (st) (void)hipStreamSynchronize(st);
     if (host) (void)hipHostFree(host);
     if (h_len) (void)hipHostFree(h_len);
+    if (h_res) (void)hipHostFree(h_res);
     for (void* p : {(void*)dev, (void*)d_res, (void*)d_len, (void*)dense})
       if (p) (void)hipFree(p);
     if (st) (void)hipStreamDestroy(st);
@@ -267,12 +279,17 @@ class TorchModel {
         idx[i] = len - 1;  // metadata.cpp:59-60; QuerySamplesComplete sends (res_idx_ + 1) * 4 bytes
         widest = std::max(widest, len);
       }
-      if (widest > 0)  // only the written columns travel
-        hcheck(hipMemcpy2DAsync(res.data_ptr<int32_t>(), (size_t)res.size(1) * sizeof(int32_t), s.d_res,
-                                (size_t)s.max_res * sizeof(int32_t), (size_t)widest * sizeof(int32_t), (size_t)n,
-                                hipMemcpyDeviceToHost, s.st),
+      if (widest > 0) {  // only the written columns travel, through pinned memory (a 2-D copy straight into the
+                         // State's pageable res_ goes through the runtime's staging, row by row)
+        s.grow_res((size_t)n * widest * sizeof(int32_t));
+        hcheck(hipMemcpy2DAsync(s.h_res, (size_t)widest * sizeof(int32_t), s.d_res, (size_t)s.max_res * sizeof(int32_t),
+                                (size_t)widest * sizeof(int32_t), (size_t)n, hipMemcpyDeviceToHost, s.st),
                "copy res");
-      hcheck(hipStreamSynchronize(s.st), "sync");
+        hcheck(hipStreamSynchronize(s.st), "sync");
+        int32_t* rp = res.data_ptr<int32_t>();
+        const int64_t pitch = res.size(1);
+        for (int i = 0; i < n; ++i) std::memcpy(rp + i * pitch, s.h_res + (size_t)i * widest, sizeof(int32_t) * widest);
+      }
     } catch (...) {
       release(&state, true);
       throw;

@@ -21,7 +21,8 @@
 // --feats: fp32 [sum(lens)][240], the samples' frames back to back; --lens: int32 [N]; --query: int32 QSL
 // indices (default 0..N-1).  --pinned 1: each instance assembles its batches into a reused pinned buffer
 // (a SUT choice the reference does not make; the model then DMAs the batch as it is instead of packing
-// it).  WAV mode (--processor F --wav F --wav-lens F: fp32 16 kHz audio back to back, int32 samples per
+// it).  --preassemble 1 (Offline, features): every batch is assembled before the timed region, so the
+// line is the model's own rate with the SUT's batches ready.  WAV mode (--processor F --wav F --wav-lens F: fp32 16 kHz audio back to back, int32 samples per
 // utterance): AssembleSamples gathers audio and the AudioProcessor drop-in (rnnt_processor_mi355x.hpp)
 // featurizes each batch on the GPU before the model, as the SUT does with WAV=true (torch_sut.cpp:192-200,
 // 442-461).  Prints one JSON line.
@@ -199,7 +200,7 @@ int usage(const char* argv0) {
   std::fprintf(stderr,
                "usage: %s --engine F --feats F --lens F --out F [--query F] [--scenario offline|server] [--threads K]\n"
                "          [--batch B] [--split-len L] [--response R] [--pro-batch P] [--warmup W] [--intra C] [--progress S]\n"
-               "          [--pinned 0|1]\n"
+               "          [--pinned 0|1] [--preassemble 0|1] [--check-fill 0|1]\n"
                "   or (WAV=true) --wav F --wav-lens F --processor F in place of --feats / --lens\n",
                argv0);
   return 2;
@@ -227,12 +228,30 @@ void guarded(F f) {
 }
 
 // OfflineSUT::thInstance (torch_sut.cpp:140-219)
+// --preassemble 1: the query's batches assembled before the timed region (instance i assembles batches
+// i, i + threads, ...), then taken in order from a shared counter -- what the model sustains when the SUT
+// has its batches ready (the harness's own measurement; the reference assembles inside the loop)
+struct Preassembled {
+  std::vector<std::vector<rnnt::Sample>> samples;
+  std::vector<std::pair<at::Tensor, at::Tensor>> batch;
+  std::atomic<size_t> next{0};
+};
+
 void offline_instance(int index, rnnt::models::TorchModel& model, const Qsl& qsl, std::list<rnnt::Sample>& queue,
                       std::mutex& qmu, Responder& resp, int bs, int split_len, int warmup, int intra,
-                      std::atomic<int>& warm, std::atomic<bool>& go, std::atomic<int64_t>& batches) {
+                      std::atomic<int>& warm, std::atomic<bool>& go, std::atomic<int64_t>& batches,
+                      Preassembled* pre, int threads) {
   const int which = index & 1;
   if (intra > 0) at::set_num_threads(intra);  // this instance's team (the reference pins INTRA threads, :143-149)
   at::Tensor xbuf;
+  if (pre)
+    for (size_t j = (size_t)index; j < pre->samples.size(); j += (size_t)threads) {
+      std::vector<int64_t> idx;
+      for (const auto& smp : pre->samples[j]) idx.push_back((int64_t)smp.index);
+      const int64_t n = (int64_t)idx.size();
+      at::Tensor buf;  // a buffer of its own per batch (pinned with --pinned 1)
+      pre->batch[j] = qsl.assemble(idx, (n + 31) / 32 * 32, &buf);
+    }
   for (int i = 0; i < warmup; ++i) {  // OfflineSUT::warmup (:124-138), GenerateDummySamples (rnnt_qsl.cpp:136-147)
     rnnt::State ws(bs, split_len);
     at::Tensor x, x_lens;
@@ -252,6 +271,22 @@ void offline_instance(int index, rnnt::models::TorchModel& model, const Qsl& qsl
   rnnt::State state(bs, split_len);
   while (true) {
     std::vector<rnnt::Sample> samples;
+    if (pre) {
+      const size_t j = pre->next++;
+      if (j >= pre->samples.size()) break;
+      samples = pre->samples[j];
+      const int n = (int)samples.size();
+      at::Tensor x = pre->batch[j].first, x_lens = pre->batch[j].second;
+      state.update(x, x_lens, split_len, n);
+      model.encode(which, state);
+      model.decode(which, state);
+      const at::Tensor res_lens = state.res_idx_ + 1;
+      for (int i = 0; i < n; ++i)
+        resp.complete(samples[i], state.res_[i], res_lens.data_ptr<int32_t>()[i], state.max_res_len_);
+      // (the batch's memory is kept until the run ends: freeing pinned memory synchronises the device)
+      batches++;
+      continue;
+    }
     {
       std::lock_guard<std::mutex> l(qmu);
       if (queue.empty()) break;
@@ -277,7 +312,7 @@ void offline_instance(int index, rnnt::models::TorchModel& model, const Qsl& qsl
     model.decode(which, state);
     const at::Tensor res_lens = state.res_idx_ + 1;
     for (int i = 0; i < n; ++i)
-      resp.complete(samples[i], state.res_[i], res_lens[i].item<int32_t>(), state.max_res_len_);
+      resp.complete(samples[i], state.res_[i], res_lens.data_ptr<int32_t>()[i], state.max_res_len_);
     batches++;
   }
 }
@@ -327,7 +362,7 @@ void server_consumer(int index, rnnt::models::TorchModel& model, std::deque<rnnt
     const bool* fin = state.finish_idx_.data_ptr<bool>();
     const int32_t* Fl = state.F_lens_.data_ptr<int32_t>();
     for (int i = 0; i < bs; ++i)
-      if (fin[i] && Fl[i] > 0) resp.complete(samples[i], state.res_[i], res_lens[i].item<int32_t>(), state.max_res_len_);
+      if (fin[i] && Fl[i] > 0) resp.complete(samples[i], state.res_[i], res_lens.data_ptr<int32_t>()[i], state.max_res_len_);
     batches++;
   }
 }
@@ -357,6 +392,7 @@ int main(int argc, char** argv) {
     if (intra > 0) at::set_num_threads(intra);
     Qsl qsl;
     qsl.pinned = a.num("pinned", 0) != 0;
+    const bool check_fill = a.num("check-fill", 1) != 0;  // 0: throughput lines skip the per-row SOS scan
     if (wav_mode) {  // the sort key is the feature length the processor will produce
       qsl.wav_lens = read_file<int32_t>(a.get("wav-lens"));
       qsl.wav = read_file<float>(a.get("wav"));
@@ -398,6 +434,7 @@ int main(int argc, char** argv) {
       g_processor = processor.get();
     }
     Responder resp;
+    resp.check_fill = check_fill;
     // progress on stderr every --progress seconds (a long run stays visibly alive)
     const int progress = a.num("progress", 10);
     std::atomic<bool> done{false};
@@ -442,9 +479,20 @@ int main(int argc, char** argv) {
       });
       std::list<rnnt::Sample> queue(s.begin(), s.end());
       std::mutex qmu;
+      std::unique_ptr<Preassembled> pre;
+      if (a.num("preassemble", 0) != 0) {
+        if (wav_mode) throw std::runtime_error("--preassemble is for feature input");
+        pre = std::make_unique<Preassembled>();
+        for (size_t b = 0; b < s.size(); b += (size_t)bs)
+          pre->samples.emplace_back(s.begin() + (long)b, s.begin() + (long)std::min(s.size(), b + (size_t)bs));
+        pre->batch.resize(pre->samples.size());
+      }
       for (int i = 0; i < threads; ++i)
         th.emplace_back([&, i] {
-          guarded([&] { offline_instance(i, model, qsl, queue, qmu, resp, bs, split_len, warmup, intra, warm, go, batches); });
+          guarded([&] {
+            offline_instance(i, model, qsl, queue, qmu, resp, bs, split_len, warmup, intra, warm, go, batches, pre.get(),
+                             threads);
+          });
         });
       while (warm < threads && !failed()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
       model.stats(/*reset=*/true);  // the warmups' calls are not counted
@@ -505,7 +553,9 @@ int main(int argc, char** argv) {
     std::cout << "], \"model_host_seconds\": {\"pack\": " << cs.pack << ", \"copy\": " << cs.copy
               << ", \"turn_wait\": " << cs.turn_wait << ", \"encode\": " << cs.encode << ", \"decode\": " << cs.decode
               << ", \"encode_calls\": " << cs.calls << ", \"dense_pinned_calls\": " << cs.dense_calls
-              << ", \"frames\": " << cs.frames << "}, \"pinned_assembly\": " << (qsl.pinned ? "true" : "false") << "}"
+              << ", \"frames\": " << cs.frames << "}, \"pinned_assembly\": " << (qsl.pinned ? "true" : "false")
+              << ", \"preassembled\": " << (a.num("preassemble", 0) != 0 ? "true" : "false")
+              << ", \"sos_fill_checked\": " << (resp.check_fill ? "true" : "false") << "}"
               << std::endl;
     return 0;
   } catch (const std::exception& ex) {

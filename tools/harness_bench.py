@@ -35,6 +35,11 @@ def main():
     ap.add_argument("--intra", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pinned", type=int, default=0, help="1: the harness assembles batches in pinned memory")
+    ap.add_argument("--check-fill", type=int, default=0,
+                    help="1: the harness also scans every answered row's SOS fill (the tests do; 184 MB per 6144-row "
+                         "batch, not part of the reference's response path)")
+    ap.add_argument("--preassemble", type=int, default=0,
+                    help="1: every batch assembled before the timed region (the model's own rate, host assembly excluded)")
     ap.add_argument("--wav", action="store_true",
                     help="WAV=true: bench.py --wav's audio QSL in host memory, featurized by the AudioProcessor drop-in")
     ap.add_argument("--compare", default=None)
@@ -75,7 +80,8 @@ def main():
     cmd = [HARNESS, "--engine", eng] + src + [
            "--query", os.path.join(work, "query.bin"), "--scenario", "offline", "--threads", str(args.threads),
            "--batch", str(args.batch), "--split-len", str(args.split_len), "--intra", str(args.intra),
-           "--warmup", str(args.warmup), "--pinned", str(args.pinned), "--out", out]
+           "--warmup", str(args.warmup), "--pinned", str(args.pinned), "--preassemble", str(args.preassemble),
+           "--check-fill", str(args.check_fill), "--out", out]
     r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)  # progress lines pass through on stderr
     if r.returncode != 0:
         sys.exit(r.returncode)
